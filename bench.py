@@ -1,0 +1,317 @@
+#!/usr/bin/env python3
+"""Benchmark: train images/sec of the VanillaVAE training step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|f32] [--arch vanilla|betaH|iwae]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1]): VanillaVAE latent_dim=128, 64x64x3 synthetic images, batch 64
+per GPU (weak scaling, data parallel over ranks, RCCL gradient all-reduce), bf16 MFMA with fp32
+accumulation / statistics / optimizer.  A "step" = forward + ELBO + backward + [all-reduce] + Adam
+(experiment.py:45-86 + :308-311), inputs already resident in HBM, the whole step replayed from
+HIP graphs.  Prints ONE JSON line on rank 0.
+
+roofline: the dominant kernel of the step (largest time per step, measured with HIP events on the
+stream it runs on, each launch isolated behind a spin kernel so the events bracket only it) with
+its algorithmic FLOPs/bytes per launch; `traffic` comes from the committed
+rocprofv3 --pmc summary in profiles/ when present.
+cpu_baseline: the oracle (oracle/vae_oracle.py, a PyTorch-CPU fp32 restatement pinned against the
+reference) timed on this host's cores on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "pytorch-vae_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train images/sec (node) VanillaVAE 64×64 bs=64 at 1/2/4/8 GPU; ELBO match"
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # dense, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--kernel-breakdown", action="store_true", help="print per-kernel times to stderr")
+    return ap.parse_args()
+
+
+# ----------------------------------------------------------------------------- kernels
+def conv_cost(fn, a, dsz):
+    """(flops, bytes) per launch by the counting rules of BASELINE.md §3 / SURVEY §8(d)."""
+    R = a.r
+    n, h, w, c, k, p, q = a.n, a.h, a.w, a.c, a.k, a.p, a.q
+    if fn.startswith("vae_conv2d"):
+        macs = n * p * q * k * c * R * R
+        x_b, y_b = n * h * w * c * (4 if a.x_nchw_f32 else dsz), n * p * q * k * dsz
+    else:  # transposed: 2*N*Cin*Hin*Win*Cout*R*S
+        macs = n * h * w * c * k * R * R
+        x_b, y_b = n * h * w * c * dsz, n * p * q * k * dsz
+    w_b = k * c * R * R * dsz
+    if fn.endswith("_fwd"):
+        return 2 * macs, x_b + w_b + y_b
+    if fn.endswith("_bwd_data"):
+        return 2 * macs, y_b + w_b + x_b
+    return 2 * macs, x_b + y_b + k * c * R * R * 4          # bwd_filter writes fp32 dW
+
+
+def linear_cost(fn, a, dsz):
+    macs = a.m * a.n * a.k
+    if fn.endswith("_fwd"):
+        return 2 * macs, a.m * a.k * dsz + a.n * a.k * dsz + a.m * a.n * (4 if a.y_f32 else dsz)
+    if fn.endswith("_bwd_data"):
+        return 2 * macs, a.m * a.n * (4 if a.dy_f32 else dsz) + a.n * a.k * dsz + a.m * a.k * dsz
+    return 2 * macs, a.m * a.n * (4 if a.dy_f32 else dsz) + a.m * a.k * dsz + a.n * a.k * 4
+
+
+def head_cost(fn, a, dsz):
+    macs = a.n * a.h * a.w * 3 * a.c * 9
+    x_b = a.n * a.h * a.w * a.c * dsz
+    img = a.n * 3 * a.h * a.w * 4
+    if fn == "vae_head_fwd":
+        return 2 * macs, x_b + 2 * img          # reads x, target; writes recon
+    if fn == "vae_head_bwd_data":
+        return 2 * macs, 2 * img + x_b + x_b    # recon, target, y (epilogue) -> dx
+    return 2 * macs, x_b + 2 * img + 3 * a.c * 9 * 4
+
+
+def kernel_costs(plan, dsz):
+    from vae_amd import _lib as L
+    out = []
+    for fn, ref in plan.fwd_calls + plan.bwd_calls:
+        if fn == "vae_reparam_fwd" or ref is None:
+            out.append((fn, None, 0, 0))
+            continue
+        a = ref._obj
+        if isinstance(a, L.ConvArgs):
+            f, b = conv_cost(fn, a, dsz)
+        elif isinstance(a, L.LinearArgs):
+            f, b = linear_cost(fn, a, dsz)
+        elif isinstance(a, L.HeadArgs):
+            f, b = head_cost(fn, a, dsz)
+        else:
+            f, b = 0, 0
+        out.append((fn, ref, f, b))
+    return out
+
+
+def time_kernels(plan, reps=20):
+    """Per-launch duration of every kernel of the step, each bracketed by HIP events on the
+    stream it runs on, queued behind a spin kernel so host launch latency is not measured."""
+    from vae_amd import _lib as L
+    st = torch.cuda.current_stream()
+    sp = st.cuda_stream
+    res = []
+    for fn, ref in plan.fwd_calls + plan.bwd_calls:
+        times = []
+        for _ in range(reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(200000)           # ~100 µs spin: everything below is queued behind it
+            e0.record(st)
+            if fn == "vae_reparam_fwd":
+                L.call(fn, *plan._reparam, sp)
+            else:
+                L.call(fn, ref, sp)
+            e1.record(st)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) * 1e3)   # µs
+        times.sort()
+        res.append((fn, ref, times[len(times) // 2]))
+    return res
+
+
+def pmc_traffic(kernel_symbol_hint: str):
+    """HBM bytes per launch of the dominant kernel from profiles/*pmc*.json (tools/pmc_traffic.py),
+    corrected per MI355X_MICROARCH.md §HBM (FETCH_SIZE x2).  None when not collected."""
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel_symbol_hint in k:
+                return v.get("hbm_bytes_per_launch")
+    return None
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(batch, seconds):
+    """The oracle's fp32 step (fwd + ELBO + bwd + Adam) on the host cores, bounded sample."""
+    from oracle import vae_oracle as O
+    threads = torch.get_num_threads()
+    sd = O.make_params(O.vanilla_param_spec(), 1265)
+    P = {k: (v.clone().requires_grad_(True) if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))
+             else v.clone()) for k, v in sd.items()}
+    leaves = [v for v in P.values() if v.requires_grad]
+    m = [torch.zeros_like(v) for v in leaves]
+    v2 = [torch.zeros_like(v) for v in leaves]
+    x, eps = O.make_inputs(batch, 128, 1265)
+    hd = O.DEFAULT_HIDDEN
+
+    def step(it):
+        stats = {}
+        mu, lv = O.vanilla_encode(P, x, hd, True, stats)
+        z = O.reparameterize(mu, lv, eps)
+        rec = O.vanilla_decode(P, z, hd, True, stats)
+        ld = O.vanilla_loss(rec, x, mu, lv, 1e-8)
+        for t in leaves:
+            t.grad = None
+        ld["loss"].backward()
+        with torch.no_grad():
+            for i, t in enumerate(leaves):
+                O.adam_step(t, t.grad, m[i], v2[i], it, 0.005)
+        return ld
+
+    step(1)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step(n + 2)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    return {"value": round(n * batch / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle VanillaVAE fp32 train step (fwd+ELBO+bwd+Adam), B={batch}, {n} steps / {el:.1f}s "
+                      f"on {threads} threads ({os.cpu_count()} visible CPUs)"}
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    distributed = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if distributed:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        rank, world = dist.get_rank(), dist.get_world_size()
+    else:
+        rank, world = 0, 1
+        torch.cuda.set_device(0)
+    from vae_amd import _lib as L
+    from vae_amd.engine import FusedAdam, TrainStep
+    from vae_amd.net import StepPlan, VAENet
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dsz = 2 if args.dtype == "bf16" else 4
+    gen = torch.Generator().manual_seed(1265)                     # same init on every rank
+    net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
+    S = 5 if args.arch == "iwae" else 1
+    loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
+    kld = {"vanilla": 1e-8, "betaH": 2.5e-4, "iwae": 2.5e-4}[args.arch]
+    lr = {"vanilla": 0.005, "betaH": 0.005, "iwae": 0.007}[args.arch]
+    plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S)
+    opt = FusedAdam(net, lr=lr)
+    # synthetic data resident in HBM (per-rank seed 1265+rank): U[0,1) images, N(0,1) eps
+    g = torch.Generator(device="cuda").manual_seed(1265 + rank)
+    plan.x.copy_(torch.rand(plan.x.shape, generator=g, device="cuda"))
+    plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
+    step = TrainStep(net, plan, opt, graph=not args.no_graph)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_terms = plan.out.tolist()
+    finite = all(math.isfinite(v) for v in loss_terms)
+
+    if rank != 0:
+        if distributed:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # ---- dominant kernel: per-launch time with HIP events on the step's stream
+    times = time_kernels(plan)
+    costs = kernel_costs(plan, dsz)
+    rows = []
+    for (fn, ref, us), (_, _, fl, by) in zip(times, costs):
+        rows.append((us, fn, fl, by))
+    if args.kernel_breakdown:
+        for us, fn, fl, by in rows:
+            print(f"{fn:28s} {us:9.2f} us  {fl / 1e9:8.3f} GF  {by / 1e6:8.2f} MB  "
+                  f"{(fl / us / 1e6) if us else 0:8.1f} TF/s  {(by / us / 1e3) if us else 0:8.1f} GB/s",
+                  file=sys.stderr)
+    us, fn, fl, by = max(rows, key=lambda r: r[0])
+    ai = fl / by if by else 0.0
+    peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
+    ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
+    idx = [r[1] for r in rows].index(fn)
+    if ai >= ridge:
+        roof = {"bound": "mfma", "achieved": round(fl / (us * 1e-6) / 1e12, 3), "peak": peak_tf, "unit": "TFLOP/s"}
+    else:
+        roof = {"bound": "hbm", "achieved": round(by / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["traffic"] = pmc_traffic(fn)
+    roof["kernel"] = f"{fn} (launch #{idx} of the step)"
+    roof["us_per_launch"] = round(us, 2)
+    roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}
+    step_kernel_us = sum(r[0] for r in rows)
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.batch, args.cpu_seconds)
+
+    ms = elapsed / args.steps * 1e3
+    value = world * args.batch * args.steps / elapsed
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic: U[0,1) 64x64x3 images + N(0,1) eps resident in HBM, random-init weights",
+        "config": {"workload": f"{'VanillaVAE' if args.arch == 'vanilla' else args.arch} latent_dim=128 "
+                               f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}",
+                   "per_gpu_batch": args.batch, "global_batch": world * args.batch,
+                   "parallelism": f"dp{world}", "graph": not args.no_graph},
+        "elbo": {"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1], "KLD": loss_terms[2], "finite": finite},
+        "sum_kernel_us_isolated": round(step_kernel_us, 1),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

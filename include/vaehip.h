@@ -1,0 +1,215 @@
+/*
+ * vaehip.h — C ABI of libvaehip.so, the MI355X (gfx950) kernels of the VAE training step.
+ *
+ * The reference (bplaut/PyTorch-VAE) has no native code and no FFI: its hot path is the
+ * models.base.BaseVAE interface (models/base.py:5-28) implemented with torch.nn modules
+ * (models/vanilla_vae.py:8-173, beta_vae.py, iwae.py, vq_vae.py) and driven by
+ * experiment.VAEXperiment.training_step (experiment.py:45-86).  Each entry point below
+ * replaces the forward or backward of one of those nn ops; the comment on each names the
+ * reference line whose op it replaces.  The Python host (pytorch-vae_amd/vae_amd) binds
+ * them with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - Return 0 on success, a negative VAE_E_* code on a bad argument, or a positive
+ *     hipError_t.  vae_last_error() gives a thread-local message.  Nothing aborts.
+ *   - The caller owns all memory (PyTorch caching allocator); the library never allocates,
+ *     frees or synchronises.  Every launch goes on `stream` (a hipStream_t), so a caller may
+ *     capture any sequence of calls into a HIP graph.
+ *   - Activations are NHWC.  The only NCHW tensors are the user-facing image x and the
+ *     reconstruction (the reference's [B,3,H,W] fp32 tensors).
+ *   - `dtype` selects the storage/MFMA type of activations and weight copies:
+ *     VAE_F32 (v_mfma_f32_16x16x4_f32, exact fp32 — parity mode) or VAE_BF16
+ *     (v_mfma_f32_16x16x32_bf16, fp32 accumulate — throughput mode).  Per-channel
+ *     statistics, gradients of weights, losses and optimizer state are always fp32.
+ *   - Native weight layouts (state-dict conversion in vae_amd/layout.py):
+ *       Conv2d          torch [Co][Ci][R][S]  -> native [Co][R][S][Ci]
+ *       ConvTranspose2d torch [Ci][Co][R][S]  -> native [Ci][R][S][Co]
+ *       Linear          torch [Out][In]       -> native [Out][In'] (In' = NHWC order of a
+ *                                                flattened [C,2,2] map where applicable)
+ */
+#ifndef VAEHIP_H
+#define VAEHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAE_ABI_VERSION 1
+
+enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
+
+enum vae_status {
+  VAE_OK = 0,
+  VAE_E_BADARG = -1,     /* null pointer / inconsistent sizes              */
+  VAE_E_BADSHAPE = -2,   /* shape not supported by the kernels             */
+  VAE_E_BADDTYPE = -3,
+  VAE_E_UNSUPPORTED = -4
+};
+
+/* Per-channel transform applied to a tensor element when a kernel loads it (it is how
+ * BatchNorm + LeakyReLU of the reference, vanilla_vae.py:30-31, are fused into the
+ * consumer instead of being separate passes).  `t` is the stored element, c its channel. */
+enum vae_xform_kind {
+  VAE_X_NONE = 0,    /* v = t                                                            */
+  VAE_X_ACT = 1,     /* v = lrelu(t, slope)           (slope 0 = ReLU)                   */
+  VAE_X_BN_ACT = 2,  /* v = lrelu(gamma_c*(t-mean_c)*invstd_c + beta_c, slope)  — BN train */
+  VAE_X_BN_DY = 3    /* v = gamma_c*invstd_c*(t - dbeta_c/M - xhat*dgamma_c/M),           */
+                     /*     xhat = (aux - mean_c)*invstd_c          — BN backward to dy    */
+};
+
+typedef struct vae_xform {
+  int32_t kind;            /* vae_xform_kind */
+  int32_t channels;        /* channel count C (channel of an element = index % C) */
+  float slope;             /* LeakyReLU negative slope (reference default 0.01) */
+  float count;             /* M = elements per channel in the BN reduction (N*H*W) */
+  float eps;               /* BN eps (1e-5) */
+  float momentum;          /* BN momentum (0.1), used only when running_* are set */
+  const float* sum;        /* [C] Σ(y - shift)   written by the producing kernel */
+  const float* sumsq;      /* [C] Σ(y - shift)^2 */
+  const float* shift;      /* [C] shift the sums are taken against (the conv bias) or NULL */
+  const float* gamma;      /* [C] BN weight */
+  const float* beta;       /* [C] BN bias */
+  const float* dgamma;     /* [C] BN_DY: Σ g*xhat (== dL/dgamma) */
+  const float* dbeta;      /* [C] BN_DY: Σ g      (== dL/dbeta)  */
+  const void* aux;         /* BN_DY: pre-BN tensor y, indexed like the operand (dtype) */
+  float* running_mean;     /* optional: updated once per call (unbiased var, as torch) */
+  float* running_var;
+} vae_xform;
+
+/* One convolution-family operation.  Geometry is that of the reference layer:
+ *   Conv2d:          x [n,h,w,c] -> y [n,p,q,k]
+ *   ConvTranspose2d: x [n,h,w,c] -> y [n,p,q,k]   (p = 2h for k3 s2 p1 op1 and k4 s2 p1)
+ * Fields unused by an entry point are ignored. */
+typedef struct vae_conv_args {
+  int32_t dtype;           /* vae_dtype of activations / weight copies */
+  int32_t n, h, w, c;      /* input of the layer (as in the reference) */
+  int32_t k, p, q;         /* output channels / spatial */
+  int32_t r, stride, pad;  /* square kernel, stride, padding (output_padding implied) */
+  int32_t x_nchw_f32;      /* 1: x is the fp32 NCHW image (first layer), 0: NHWC dtype */
+  /* tensors */
+  const void* x;           /* layer input (stored pre-activation; see x_xf) */
+  vae_xform x_xf;          /* transform applied to x elements on load */
+  const void* wt;          /* weights in native layout (dtype) */
+  const float* bias;       /* [k] or NULL */
+  void* y;                 /* fwd: output pre-activation (NHWC, dtype) */
+  float* y_sum;            /* fwd: optional per-channel Σ(acc), Σ(acc^2) for the next BN */
+  float* y_sumsq;
+  const void* residual;    /* fwd: optional y += xf(residual) (VQ-VAE ResidualLayer) */
+  vae_xform residual_xf;
+  /* backward */
+  const void* dy;          /* gradient w.r.t. the layer output (stored, dtype) */
+  vae_xform dy_xf;         /* e.g. BN_DY: dy = BN-backward(g, y) computed on load */
+  void* dx;                /* bwd_data: gradient w.r.t. the layer input (dtype) */
+  vae_xform dx_epi;        /* bwd_data epilogue: how x was activated (BN_ACT/ACT/NONE);
+                              BN_ACT/ACT need aux = stored pre-activation x; the kernel
+                              writes g = dL/dz of that activation and, for BN_ACT,
+                              accumulates Σg -> dx_dbeta, Σg*xhat -> dx_dgamma */
+  float* dx_dgamma;
+  float* dx_dbeta;
+  float* dw;               /* bwd_filter: fp32 weight gradient, native layout (accumulated) */
+  float* db;               /* bwd_filter: fp32 bias gradient (accumulated) or NULL */
+  int32_t split_k;         /* bwd_filter: 0 = choose automatically */
+} vae_conv_args;
+
+/* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,
+ * decoder_input).  Same transform / epilogue conventions as vae_conv_args. */
+typedef struct vae_linear_args {
+  int32_t dtype;
+  int32_t m, n, k;         /* rows (batch), out features, in features */
+  const void* x; vae_xform x_xf;
+  const void* wt; const float* bias;
+  void* y;
+  int32_t y_f32;           /* fwd: write y as fp32 (fc_mu|fc_var output) instead of dtype */
+  const void* dy;          /* [m][n] */
+  int32_t dy_f32;          /* bwd: dy is fp32 (d[mu|logvar]) instead of dtype */
+  void* dx; vae_xform dx_epi; float* dx_dgamma; float* dx_dbeta;
+  float* dw; float* db;
+  /* reparameterization backward epilogue (decoder_input bwd_data): when mulv != NULL the
+   * kernel turns dz into d[mu|logvar] (vanilla_vae.py:107-117 + the analytic KL of :143) */
+  const float* mulv;       /* [rows_mu][2*k] fc output (mu | log_var) */
+  const float* eps;        /* [m][k] */
+  const float* kl_coef;    /* [m] per-row coefficient of dKL (see vae_elbo_fwd) or NULL */
+  float* dmulv;            /* [rows_mu][2*k], accumulated */
+  int32_t samples;         /* rows per mu row (IWAE S; 1 otherwise) */
+} vae_linear_args;
+
+/* Final layer of the decoder: Conv2d(C->3, k3, s1, p1) + Tanh (vanilla_vae.py:73-75) and the
+ * reconstruction term of the ELBO (F.mse_loss, vanilla_vae.py:140) — VALU kernels. */
+typedef struct vae_head_args {
+  int32_t dtype;
+  int32_t n, h, w, c;      /* input of the conv (NHWC, pre-activation, see x_xf) */
+  const void* x; vae_xform x_xf;
+  const float* wt;         /* fp32 native [3][3][3][c] */
+  const float* bias;       /* [3] */
+  const float* target;     /* fp32 NCHW [n,3,h,w] image the reconstruction is scored against;
+                              for IWAE row i is scored against image i / samples */
+  int32_t samples;         /* IWAE S (1 otherwise) */
+  float* recon;            /* fp32 NCHW [n,3,h,w] */
+  float* sse;              /* [n] Σ(recon-target)^2 per image, accumulated */
+  const float* coef;       /* bwd: [n] dL/d(sse_i); g = coef*(recon-target)*(1-recon^2) */
+  void* dx; vae_xform dx_epi; float* dx_dgamma; float* dx_dbeta;
+  float* dw; float* db;
+  const float* grad_recon; /* bwd alternative to coef: dL/drecon (NCHW fp32), g = grad*(1-recon^2) */
+} vae_head_args;
+
+/* Loss kinds (vanilla_vae.py:124-146, beta_vae.py:129-152, iwae.py:129-160) */
+enum vae_loss_kind { VAE_LOSS_VANILLA = 0, VAE_LOSS_BETA_H = 1, VAE_LOSS_BETA_B = 2, VAE_LOSS_IWAE = 3 };
+
+typedef struct vae_elbo_args {
+  int32_t kind;            /* vae_loss_kind */
+  int32_t batch, samples, latent;
+  int32_t img_elems;       /* C*H*W of one image */
+  float kld_weight;        /* M_N */
+  float beta, gamma, c_max, c_stop_iter;
+  const float* iter;       /* BetaVAE-B: device num_iter (after the reference's +=1) */
+  const float* mulv;       /* [batch][2*latent] */
+  const float* sse;        /* [batch*samples] */
+  float* out;              /* [4]: loss, Reconstruction_Loss, KLD (as the reference reports it), kld_raw */
+  float* per_img;          /* [batch*samples] per-image MSE (experiment.py:60-62) */
+  float* head_coef;        /* [batch*samples] dL/d(sse_i) for vae_head_bwd_* */
+  float* kl_coef;          /* [batch*samples] per-row KL gradient coefficient */
+} vae_elbo_args;
+
+int vae_abi_version(void);
+const char* vae_last_error(void);
+
+/* --- Conv2d (encoder block, vanilla_vae.py:28-29 run at :84) ----------------------- */
+int vae_conv2d_fwd(const vae_conv_args* a, void* stream);
+int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream);
+int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream);
+/* --- ConvTranspose2d (decoder block, vanilla_vae.py:50-55, :65-70) ------------------ */
+int vae_convT2d_fwd(const vae_conv_args* a, void* stream);
+int vae_convT2d_bwd_data(const vae_conv_args* a, void* stream);
+int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream);
+/* --- Linear (fc_mu/fc_var vanilla_vae.py:36-37,89-90; decoder_input :43,101) -------- */
+int vae_linear_fwd(const vae_linear_args* a, void* stream);
+int vae_linear_bwd_data(const vae_linear_args* a, void* stream);
+int vae_linear_bwd_filter(const vae_linear_args* a, void* stream);
+/* --- final Conv2d + Tanh + reconstruction SSE (vanilla_vae.py:73-75, :140) ---------- */
+int vae_head_fwd(const vae_head_args* a, void* stream);
+int vae_head_bwd_data(const vae_head_args* a, void* stream);
+int vae_head_bwd_filter(const vae_head_args* a, void* stream);
+/* --- reparameterization (vanilla_vae.py:107-117): z = eps*exp(.5*logvar) + mu,
+ *     row r uses mu row r/samples.  z is written in `dtype`. */
+int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int32_t latent,
+                    const float* mulv, const float* eps, void* z, void* stream);
+/* --- ELBO terms + backward seeds (vanilla_vae.py:124-146 and variants) -------------- */
+int vae_elbo_fwd(const vae_elbo_args* a, void* stream);
+/* --- Adam (experiment.py:308-311; torch.optim.Adam semantics), flat fp32 buffers.
+ *     step/lr are device scalars so the call can be replayed from a graph.  When
+ *     p_lowp != NULL the updated parameters are also written as bf16 (weight copies). --- */
+int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v,
+                  const int32_t* step, const float* lr, float beta1, float beta2, float eps,
+                  float weight_decay, void* p_lowp, void* stream);
+/* --- fp32 -> bf16 copy (weight copies when the optimizer is not vae_adam_step) -------- */
+int vae_cast_bf16(int64_t n, const float* src, void* dst, void* stream);
+/* --- start of a training step: zero `bytes` at `zero` and ++*step ------------------ */
+int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAEHIP_H */

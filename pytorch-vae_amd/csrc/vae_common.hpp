@@ -1,0 +1,120 @@
+// Shared device/host helpers for libvaehip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "vaehip.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+namespace vae {
+
+// ---------------------------------------------------------------- error state (host)
+void set_error(const char* fmt, ...);
+int fail(int code, const char* fmt, ...);
+int check_launch(const char* what);
+
+// ---------------------------------------------------------------- scalar conversion
+__device__ __forceinline__ float ld_f(const float* p) { return *p; }
+__device__ __forceinline__ float ld_f(const __bf16* p) { return (float)(*p); }
+template <class T> __device__ __forceinline__ T cvt(float v);
+template <> __device__ __forceinline__ float cvt<float>(float v) { return v; }
+template <> __device__ __forceinline__ __bf16 cvt<__bf16>(float v) { return (__bf16)v; }
+
+// 8 consecutive elements -> floats (16-B aligned for bf16, 32-B for fp32)
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+  v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+__device__ __forceinline__ void ld8(const __bf16* p, float (&v)[8]) {
+  bf16x8 a = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+}
+__device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
+  f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+}
+__device__ __forceinline__ void ld4(const __bf16* p, float (&v)[4]) {
+  bf16x4 a = *reinterpret_cast<const bf16x4*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (float)a[j];
+}
+
+// LDS stores: 8 contiguous (16-B / 32-B aligned) and 2 contiguous elements
+__device__ __forceinline__ void st8(float* d, const float (&v)[8]) {
+  *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+  *reinterpret_cast<f32x4*>(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+}
+__device__ __forceinline__ void st8(__bf16* d, const float (&v)[8]) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)v[j];
+  *reinterpret_cast<bf16x8*>(d) = o;
+}
+__device__ __forceinline__ void st2(float* d, float a, float b) { *reinterpret_cast<f32x2*>(d) = f32x2{a, b}; }
+__device__ __forceinline__ void st2(__bf16* d, float a, float b) {
+  bf16x2 o; o[0] = (__bf16)a; o[1] = (__bf16)b;
+  *reinterpret_cast<bf16x2*>(d) = o;
+}
+
+__device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.f ? v : v * slope; }
+
+// ---------------------------------------------------------------- BN statistics
+// mean/invstd/var of channel c from the producer's Σ(y-shift), Σ(y-shift)^2.
+__device__ __forceinline__ void bn_moments(const vae_xform& x, int c, float& mean, float& invstd, float& var) {
+  const float inv_m = 1.0f / x.count;
+  const float s = x.sum[c] * inv_m;
+  var = fmaxf(x.sumsq[c] * inv_m - s * s, 0.0f);
+  mean = s + (x.shift ? x.shift[c] : 0.0f);
+  invstd = 1.0f / sqrtf(var + x.eps);
+}
+
+// Per-channel coefficient table in LDS for one transform.
+//   BN_ACT: v = lrelu(t*a + b)         ACT: v = lrelu(t)        NONE: v = t
+//   BN_DY : v = a*t + b*aux + c
+//   epilogue use (BN_ACT): also p,q with xhat = y*p + q
+template <int MAXC, bool EPI>
+struct XfTable {
+  float a[MAXC], b[MAXC], c[MAXC];
+  float p[EPI ? MAXC : 1], q[EPI ? MAXC : 1];
+
+  // Fill for channels [0, C); optionally update BN running stats (one block only).
+  __device__ __forceinline__ void fill(const vae_xform& x, bool update_running) {
+    if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return;
+    for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
+      float mean, invstd, var;
+      bn_moments(x, ch, mean, invstd, var);
+      const float g = x.gamma[ch];
+      if (x.kind == VAE_X_BN_ACT) {
+        const float sc = g * invstd;
+        a[ch] = sc;
+        b[ch] = x.beta[ch] - mean * sc;
+        if (EPI) { p[EPI ? ch : 0] = invstd; q[EPI ? ch : 0] = -mean * invstd; }
+        if (update_running && x.running_mean) {
+          const float m = x.momentum;
+          const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
+          x.running_mean[ch] = (1.f - m) * x.running_mean[ch] + m * mean;
+          x.running_var[ch] = (1.f - m) * x.running_var[ch] + m * unb;
+        }
+      } else {
+        const float inv_m = 1.0f / x.count;
+        const float A = g * invstd;
+        const float mg = x.dbeta[ch] * inv_m;         // mean of g
+        const float mgx = x.dgamma[ch] * inv_m;       // mean of g*xhat
+        a[ch] = A;
+        b[ch] = -A * invstd * mgx;
+        c[ch] = -A * (mg - mean * invstd * mgx);
+      }
+    }
+  }
+};
+
+}  // namespace vae

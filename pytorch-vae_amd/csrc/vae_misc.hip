@@ -1,0 +1,564 @@
+// Non-GEMM kernels of the VAE step: the decoder head (final Conv2d(C->3)+Tanh+SSE, a thin-N
+// layer that would waste 13/16 of an MFMA tile, so it runs on the VALU with its input tile
+// staged once in LDS), the reparameterization, the ELBO reductions, Adam, and utilities.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "vae_common.hpp"
+
+namespace vae {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, "%s: %s", what, hipGetErrorString(e));
+  return VAE_OK;
+}
+
+namespace {
+
+constexpr int HEAD_MAXC = 64;      // channels entering the head
+constexpr int HEAD_T = 256;        // threads = pixels per tile
+constexpr int CO = 3;              // RGB
+constexpr int HEAD_GS = 774;       // max (rows+2)*(w+2) with rows*w == 256
+
+struct HeadP {
+  int n, h, w, c, rows, samples, tiles;
+  const void* x; vae_xform xf;
+  const float* wt; const float* bias; const float* target;
+  float* recon; float* sse; const float* coef;
+  void* dx; vae_xform epi; float* dgamma; float* dbeta;
+  float* dw; float* db;
+  const float* grad_recon;
+};
+
+__device__ __forceinline__ float act_of(const vae_xform& xf, const float* ta, const float* tb, float v, int ch) {
+  if (xf.kind == VAE_X_BN_ACT) return lrelu(fmaf(v, ta[ch], tb[ch]), xf.slope);
+  if (xf.kind == VAE_X_ACT) return lrelu(v, xf.slope);
+  return v;
+}
+
+// BN forward coefficients of the head input (and x̂ = y*p + q for the backward epilogue);
+// `update_running`: this block also applies the BatchNorm running-stat update (once per call)
+__device__ void head_coefs(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq,
+                           bool update_running = false) {
+  if (xf.kind != VAE_X_BN_ACT) return;
+  for (int ch = threadIdx.x; ch < xf.channels; ch += blockDim.x) {
+    float mean, invstd, var;
+    bn_moments(xf, ch, mean, invstd, var);
+    ta[ch] = xf.gamma[ch] * invstd;
+    tb[ch] = xf.beta[ch] - mean * ta[ch];
+    if (tp) { tp[ch] = invstd; tq[ch] = -mean * invstd; }
+    if (update_running && xf.running_mean) {
+      const float m = xf.momentum;
+      const float unb = xf.count > 1.f ? var * xf.count / (xf.count - 1.f) : var;
+      xf.running_mean[ch] = (1.f - m) * xf.running_mean[ch] + m * mean;
+      xf.running_var[ch] = (1.f - m) * xf.running_var[ch] + m * unb;
+    }
+  }
+}
+
+// Stage act(x) rows [h0-1, h0+rows] x cols [-1, w] into LDS as [(rows+2)][(w+2)][c+4] floats
+template <class T>
+__device__ void stage_input(const HeadP& p, int n, int h0, float* xs, const float* ta, const float* tb) {
+  const int CP = p.c + 4, WP = p.w + 2;
+  const int oct_per_pix = p.c / 8;
+  const int total = (p.rows + 2) * WP * oct_per_pix;
+  const T* X = static_cast<const T*>(p.x);
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int o = e % oct_per_pix;
+    const int pix = e / oct_per_pix;
+    const int cc = pix % WP, rr = pix / WP;
+    const int hi = h0 + rr - 1, wi = cc - 1;
+    float v[8];
+    if (hi >= 0 && hi < p.h && wi >= 0 && wi < p.w) {
+      ld8(X + (((long)n * p.h + hi) * p.w + wi) * p.c + o * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = act_of(p.xf, ta, tb, v[j], o * 8 + j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    }
+    float* d = xs + (rr * WP + cc) * CP + o * 8;
+    *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+// recon = tanh(conv3x3(act(x)) + b) -> NCHW; sse[n] += Σ (recon - target)^2
+template <class T>
+__global__ void __launch_bounds__(HEAD_T) head_fwd_kernel(HeadP p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float ta[HEAD_MAXC], tb[HEAD_MAXC], ws[CO * 9 * HEAD_MAXC], red[HEAD_T / 64];
+  const int tiles_per_img = p.h / p.rows;
+  const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x % tiles_per_img) * p.rows;
+  head_coefs(p.xf, ta, tb, nullptr, nullptr, blockIdx.x == 0);
+  for (int i = threadIdx.x; i < CO * 9 * p.c; i += blockDim.x) ws[i] = p.wt[i];
+  __syncthreads();
+  stage_input<T>(p, n, h0, smem, ta, tb);
+  __syncthreads();
+  const int CP = p.c + 4, WP = p.w + 2;
+  const int tr = threadIdx.x / p.w, tc = threadIdx.x % p.w;
+  float o[CO] = {p.bias[0], p.bias[1], p.bias[2]};
+  for (int r = 0; r < 3; ++r)
+    for (int s = 0; s < 3; ++s) {
+      const float* xp = smem + ((tr + r) * WP + tc + s) * CP;
+      const float* wp = ws + (r * 3 + s) * p.c;
+      for (int c = 0; c < p.c; c += 4) {
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(xp + c);
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+          const float* wq = wp + co * 9 * p.c + c;
+          o[co] = fmaf(xv[0], wq[0], fmaf(xv[1], wq[1], fmaf(xv[2], wq[2], fmaf(xv[3], wq[3], o[co]))));
+        }
+      }
+    }
+  const int hh = h0 + tr;
+  const int img_t = n / p.samples;
+  float sq = 0.f;
+#pragma unroll
+  for (int co = 0; co < CO; ++co) {
+    const float y = tanhf(o[co]);
+    const long oi = (((long)n * CO + co) * p.h + hh) * p.w + tc;
+    p.recon[oi] = y;
+    const float d = y - p.target[(((long)img_t * CO + co) * p.h + hh) * p.w + tc];
+    sq = fmaf(d, d, sq);
+  }
+  for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < HEAD_T / 64; ++i) t += red[i];
+    atomicAdd(p.sse + n, t);
+  }
+}
+
+// gseed = coef[img] * (recon - target) * (1 - recon^2)   (d loss / d pre-tanh)
+__device__ __forceinline__ float gseed_at(const HeadP& p, int n, int co, int h, int w) {
+  const long oi = (((long)n * CO + co) * p.h + h) * p.w + w;
+  const float y = p.recon[oi];
+  if (p.grad_recon) return p.grad_recon[oi] * (1.f - y * y);
+  const float t = p.target[(((long)(n / p.samples) * CO + co) * p.h + h) * p.w + w];
+  return p.coef[n] * (y - t) * (1.f - y * y);
+}
+
+// dx[h,w,c] = Σ_{r,s,co} gseed[h+1-r, w+1-s, co] · W[co][r][s][c], then the BN/LReLU backward
+template <class T, int C>
+__global__ void __launch_bounds__(HEAD_T) head_bwd_data_kernel(HeadP p) {
+  __shared__ float ta[C], tb[C], tp[C], tq[C];
+  __shared__ float ws[CO * 9 * C];
+  __shared__ float gs[HEAD_GS * CO];                         // (rows+2) x (w+2) x 3
+  __shared__ float r1[4][C], r2[4][C];
+  const int tiles_per_img = p.h / p.rows;
+  const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x % tiles_per_img) * p.rows;
+  head_coefs(p.epi, ta, tb, tp, tq);
+  for (int i = threadIdx.x; i < CO * 9 * C; i += blockDim.x) ws[i] = p.wt[i];
+  const int WP = p.w + 2;
+  for (int e = threadIdx.x; e < (p.rows + 2) * WP; e += blockDim.x) {
+    const int cc = e % WP, rr = e / WP;
+    const int hi = h0 + rr - 1, wi = cc - 1;
+    const bool in = hi >= 0 && hi < p.h && wi >= 0 && wi < p.w;
+#pragma unroll
+    for (int co = 0; co < CO; ++co) gs[e * CO + co] = in ? gseed_at(p, n, co, hi, wi) : 0.f;
+  }
+  __syncthreads();
+  const int tr = threadIdx.x / p.w, tc = threadIdx.x % p.w;
+  float da[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) da[c] = 0.f;
+#pragma unroll 1
+  for (int r = 0; r < 3; ++r)
+#pragma unroll 1
+    for (int s = 0; s < 3; ++s) {
+      const float* g = gs + ((tr + 2 - r) * WP + (tc + 2 - s)) * CO;
+#pragma unroll
+      for (int co = 0; co < CO; ++co) {
+        const float gv = g[co];
+        const float* wq = ws + co * 9 * C + (r * 3 + s) * C;
+#pragma unroll
+        for (int c = 0; c < C; ++c) da[c] = fmaf(gv, wq[c], da[c]);
+      }
+    }
+  // BN + LeakyReLU backward of the head input
+  const long base = (((long)n * p.h + h0 + tr) * p.w + tc) * C;
+  const T* Y = static_cast<const T*>(p.epi.aux);
+  T* DX = static_cast<T*>(p.dx);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c0 = 0; c0 < C; c0 += 8) {
+    float y[8];
+    if (p.epi.kind != VAE_X_NONE) ld8(Y + base + c0, y);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      float gv = da[c], s1 = 0.f, s2 = 0.f;
+      if (p.epi.kind == VAE_X_BN_ACT) {
+        const float z = fmaf(y[j], ta[c], tb[c]);
+        gv = z > 0.f ? gv : gv * p.epi.slope;
+        s1 = gv;
+        s2 = gv * fmaf(y[j], tp[c], tq[c]);
+      } else if (p.epi.kind == VAE_X_ACT) {
+        gv = y[j] > 0.f ? gv : gv * p.epi.slope;
+      }
+      DX[base + c] = cvt<T>(gv);
+      if (p.epi.kind == VAE_X_BN_ACT) {
+        for (int off = 32; off > 0; off >>= 1) { s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off); }
+        if (lane == 0) { r1[wv][c] = s1; r2[wv][c] = s2; }
+      }
+    }
+  }
+  if (p.epi.kind == VAE_X_BN_ACT) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      atomicAdd(p.dbeta + c, r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c]);
+      atomicAdd(p.dgamma + c, r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c]);
+    }
+  }
+}
+
+// dW[co][r][s][c] += Σ_pix gseed[pix][co] · act(x)[pix + (r-1, s-1)][c];  db[co] += Σ gseed
+template <class T>
+__global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float ta[HEAD_MAXC], tb[HEAD_MAXC], gs[HEAD_T * CO], red[CO][HEAD_T / 64];
+  constexpr int NI = 3;                              // (9*C)/256 rounded up, C <= 85
+  const int nidx = 9 * p.c;
+  float acc[NI][CO];
+  float dbacc[CO] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[i][co] = 0.f;
+  head_coefs(p.xf, ta, tb, nullptr, nullptr);
+  const int tiles_per_img = p.h / p.rows;
+  const int CP = p.c + 4, WP = p.w + 2;
+  for (int tile = blockIdx.x; tile < p.tiles; tile += gridDim.x) {
+    const int n = tile / tiles_per_img, h0 = (tile % tiles_per_img) * p.rows;
+    __syncthreads();
+    stage_input<T>(p, n, h0, smem, ta, tb);
+    {
+      const int tr = threadIdx.x / p.w, tc = threadIdx.x % p.w;
+#pragma unroll
+      for (int co = 0; co < CO; ++co) {
+        const float g = gseed_at(p, n, co, h0 + tr, tc);
+        gs[threadIdx.x * CO + co] = g;
+        dbacc[co] += g;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = threadIdx.x + i * HEAD_T;
+      if (idx >= nidx) break;
+      const int tap = idx / p.c, c = idx - tap * p.c;
+      const int r = tap / 3, s = tap - r * 3;
+      for (int pix = 0; pix < HEAD_T; ++pix) {
+        const int tr = pix / p.w, tc = pix - tr * p.w;
+        const float xv = smem[((tr + r) * WP + tc + s) * CP + c];
+#pragma unroll
+        for (int co = 0; co < CO; ++co) acc[i][co] = fmaf(gs[pix * CO + co], xv, acc[i][co]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int idx = threadIdx.x + i * HEAD_T;
+    if (idx >= nidx) break;
+#pragma unroll
+    for (int co = 0; co < CO; ++co) atomicAdd(p.dw + co * nidx + idx, acc[i][co]);
+  }
+  if (p.db) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int co = 0; co < CO; ++co) {
+      float s = dbacc[co];
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+      if (lane == 0) red[co][wv] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < CO) {
+      float t = 0.f;
+      for (int i = 0; i < HEAD_T / 64; ++i) t += red[threadIdx.x][i];
+      atomicAdd(p.db + threadIdx.x, t);
+    }
+  }
+}
+
+int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
+  if (!a || !a->x || !a->wt || !a->bias || !a->target || !a->recon) return fail(VAE_E_BADARG, "%s: null tensor", what);
+  if (a->c % 8 || a->c > HEAD_MAXC || a->c <= 0) return fail(VAE_E_UNSUPPORTED, "%s: channels %d", what, a->c);
+  if (a->w <= 0 || a->w > 256 || HEAD_T % a->w || a->h % (HEAD_T / a->w))
+    return fail(VAE_E_UNSUPPORTED, "%s: spatial %dx%d (need w | 256 and (256/w) | h)", what, a->h, a->w);
+  if (a->dtype != VAE_F32 && a->dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "%s: dtype", what);
+  memset(&p, 0, sizeof(p));
+  p.n = a->n; p.h = a->h; p.w = a->w; p.c = a->c; p.rows = HEAD_T / a->w;
+  p.samples = a->samples > 0 ? a->samples : 1;
+  p.tiles = a->n * (a->h / p.rows);
+  p.x = a->x; p.xf = a->x_xf; p.wt = a->wt; p.bias = a->bias; p.target = a->target;
+  p.recon = a->recon; p.sse = a->sse; p.coef = a->coef;
+  p.dx = a->dx; p.epi = a->dx_epi; p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+  p.dw = a->dw; p.db = a->db; p.grad_recon = a->grad_recon;
+  if (p.xf.channels <= 0) p.xf.channels = a->c;
+  if (p.epi.channels <= 0) p.epi.channels = a->c;
+  return VAE_OK;
+}
+
+// ------------------------------------------------------------------ reparameterization
+template <class T>
+__global__ void reparam_kernel(int rows, int samples, int D, const float* mulv, const float* eps, T* z) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)rows * D) return;
+  const int r = (int)(i / D), d = (int)(i - (long)r * D);
+  const int b = r / samples;
+  const float mu = mulv[(long)b * 2 * D + d], lv = mulv[(long)b * 2 * D + D + d];
+  z[i] = cvt<T>(fmaf(eps[i], expf(0.5f * lv), mu));
+}
+
+// ---------------------------------------------------------------------------- ELBO
+__global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
+  __shared__ float kld_row[1024];
+  __shared__ float red[4][4];
+  const int B = a.batch, S = a.samples > 0 ? a.samples : 1, D = a.latent;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // kld_b = -0.5 Σ_d (1 + lv - mu^2 - exp(lv))  (one wave per row)
+  for (int b = wv; b < B; b += 4) {
+    float s = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      const float mu = a.mulv[(long)b * 2 * D + d], lv = a.mulv[(long)b * 2 * D + D + d];
+      s += 1.f + lv - mu * mu - expf(lv);
+    }
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) kld_row[b] = -0.5f * s;
+  }
+  __syncthreads();
+  const float inv_img = 1.f / (float)a.img_elems;
+  // totals: Σ sse, Σ kld_b
+  float ts = 0.f, tk = 0.f;
+  for (int i = threadIdx.x; i < B * S; i += 256) ts += a.sse[i];
+  for (int b = threadIdx.x; b < B; b += 256) tk += kld_row[b];
+  for (int off = 32; off > 0; off >>= 1) { ts += __shfl_xor(ts, off); tk += __shfl_xor(tk, off); }
+  if (lane == 0) { red[0][wv] = ts; red[1][wv] = tk; }
+  __syncthreads();
+  const float sse_tot = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const float kld_mean = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)B;
+  for (int i = threadIdx.x; i < B * S; i += 256) a.per_img[i] = a.sse[i] * inv_img;
+
+  if (a.kind != VAE_LOSS_IWAE) {
+    const float recon = sse_tot / ((float)B * (float)a.img_elems);
+    float loss, klc, kld_report;
+    if (a.kind == VAE_LOSS_VANILLA) {
+      loss = recon + a.kld_weight * kld_mean; klc = a.kld_weight; kld_report = -kld_mean;
+    } else if (a.kind == VAE_LOSS_BETA_H) {
+      loss = recon + a.beta * a.kld_weight * kld_mean; klc = a.beta * a.kld_weight; kld_report = kld_mean;
+    } else {
+      const float it = a.iter ? *a.iter : 1.f;
+      const float C = fminf(fmaxf(a.c_max / a.c_stop_iter * it, 0.f), a.c_max);
+      const float dlt = kld_mean - C;
+      loss = recon + a.gamma * a.kld_weight * fabsf(dlt);
+      klc = a.gamma * a.kld_weight * (dlt > 0.f ? 1.f : (dlt < 0.f ? -1.f : 0.f));
+      kld_report = kld_mean;
+    }
+    const float hc = 2.f / ((float)B * (float)a.img_elems);
+    for (int i = threadIdx.x; i < B; i += 256) { a.head_coef[i] = hc; a.kl_coef[i] = klc / (float)B; }
+    if (threadIdx.x == 0) { a.out[0] = loss; a.out[1] = recon; a.out[2] = kld_report; a.out[3] = kld_mean; }
+    return;
+  }
+  // IWAE: lw[b,s] = sse/img + M_N*kld_b ; w = softmax_s(lw) ; loss = mean_b Σ_s w lw
+  float lsum = 0.f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    float mx = -INFINITY;
+    for (int s = 0; s < S; ++s) mx = fmaxf(mx, a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b]);
+    float den = 0.f;
+    for (int s = 0; s < S; ++s) den += expf(a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b] - mx);
+    float wl = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const float lw = a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b];
+      wl += expf(lw - mx) / den * lw;
+    }
+    for (int s = 0; s < S; ++s) {
+      const float lw = a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b];
+      const float w = expf(lw - mx) / den;
+      const float g = w * (1.f + lw - wl) / (float)B;          // dL/dlw
+      a.head_coef[b * S + s] = g * 2.f * inv_img;
+      a.kl_coef[b * S + s] = g * a.kld_weight;
+    }
+    lsum += wl;
+  }
+  for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
+  __syncthreads();
+  if (lane == 0) red[2][wv] = lsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.out[0] = (red[2][0] + red[2][1] + red[2][2] + red[2][3]) / (float)B;
+    a.out[1] = sse_tot * inv_img / (float)(B * S);
+    a.out[2] = -kld_mean;
+    a.out[3] = kld_mean;
+  }
+}
+
+// ---------------------------------------------------------------------------- Adam
+template <bool LOWP>
+__global__ void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, const int* step, const float* lr, float b1, float b2, float eps,
+                            float wd, __bf16* __restrict__ lowp) {
+  const float t = (float)(*step);
+  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
+  const float step_size = *lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i];
+    float pi = p[i];
+    if (wd != 0.f) gi = fmaf(wd, pi, gi);
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);                 // lerp (torch Adam)
+    const float vi = fmaf(v[i], b2, (1.f - b2) * gi * gi);
+    const float den = sqrtf(vi) / bc2s + eps;
+    pi = pi - step_size * (mi / den);
+    m[i] = mi; v[i] = vi; p[i] = pi;
+    if (LOWP) lowp[i] = (__bf16)pi;
+  }
+}
+
+__global__ void cast_bf16_kernel(long n, const float* src, __bf16* dst) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    dst[i] = (__bf16)src[i];
+}
+
+__global__ void step_begin_kernel(f32x4* z, long n16, unsigned char* tail, int ntail, int* step) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x)
+    z[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (blockIdx.x == 0 && threadIdx.x < ntail) tail[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && step) *step += 1;
+}
+
+int grid_for(long n, int per_block = 256, int max_blocks = 2048) {
+  long b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return (int)(b > max_blocks ? max_blocks : b);
+}
+
+}  // namespace
+}  // namespace vae
+
+using namespace vae;
+
+extern "C" int vae_abi_version(void) { return VAE_ABI_VERSION; }
+extern "C" const char* vae_last_error(void) { return g_err; }
+
+extern "C" int vae_head_fwd(const vae_head_args* a, void* stream) {
+  HeadP p;
+  int rc = head_setup(a, p, "head_fwd");
+  if (rc) return rc;
+  if (!a->sse) return fail(VAE_E_BADARG, "head_fwd: sse");
+  const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
+  if (lds > 64 * 1024) return fail(VAE_E_UNSUPPORTED, "head_fwd: tile too large");
+  if (a->dtype == VAE_F32) hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(head_fwd_kernel<__bf16>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  return check_launch("head_fwd");
+}
+
+extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
+  HeadP p;
+  int rc = head_setup(a, p, "head_bwd_data");
+  if (rc) return rc;
+  if ((!a->coef && !a->grad_recon) || !a->dx) return fail(VAE_E_BADARG, "head_bwd_data: coef/grad_recon/dx");
+  if (p.epi.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta || !p.epi.aux)) return fail(VAE_E_BADARG, "head_bwd_data: BN epilogue");
+  if (p.epi.kind != VAE_X_NONE && !p.epi.aux) return fail(VAE_E_BADARG, "head_bwd_data: epilogue aux");
+  const hipStream_t st = (hipStream_t)stream;
+  const bool f = a->dtype == VAE_F32;
+  switch (a->c) {
+    case 32:
+      if (f) hipLaunchKernelGGL((head_bwd_data_kernel<float, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      else hipLaunchKernelGGL((head_bwd_data_kernel<__bf16, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      break;
+    case 64:
+      if (f) hipLaunchKernelGGL((head_bwd_data_kernel<float, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      else hipLaunchKernelGGL((head_bwd_data_kernel<__bf16, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      break;
+    default:
+      return fail(VAE_E_UNSUPPORTED, "head_bwd_data: channels %d (32 or 64)", a->c);
+  }
+  return check_launch("head_bwd_data");
+}
+
+extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
+  HeadP p;
+  int rc = head_setup(a, p, "head_bwd_filter");
+  if (rc) return rc;
+  if ((!a->coef && !a->grad_recon) || !a->dw) return fail(VAE_E_BADARG, "head_bwd_filter: coef/grad_recon/dw");
+  if (9 * a->c > 3 * HEAD_T) return fail(VAE_E_UNSUPPORTED, "head_bwd_filter: channels");
+  const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
+  const int grid = p.tiles < 256 ? p.tiles : 256;
+  if (a->dtype == VAE_F32) hipLaunchKernelGGL(head_bwd_filter_kernel<float>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(head_bwd_filter_kernel<__bf16>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  return check_launch("head_bwd_filter");
+}
+
+extern "C" int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int32_t latent, const float* mulv,
+                               const float* eps, void* z, void* stream) {
+  if (!mulv || !eps || !z || rows <= 0 || latent <= 0 || samples <= 0) return fail(VAE_E_BADARG, "reparam_fwd: args");
+  const long n = (long)rows * latent;
+  const int grid = (int)((n + 255) / 256);
+  if (dtype == VAE_F32) hipLaunchKernelGGL(reparam_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, samples, latent, mulv, eps, (float*)z);
+  else if (dtype == VAE_BF16) hipLaunchKernelGGL(reparam_kernel<__bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, samples, latent, mulv, eps, (__bf16*)z);
+  else return fail(VAE_E_BADDTYPE, "reparam_fwd: dtype");
+  return check_launch("reparam_fwd");
+}
+
+extern "C" int vae_elbo_fwd(const vae_elbo_args* a, void* stream) {
+  if (!a || !a->mulv || !a->sse || !a->out || !a->per_img || !a->head_coef || !a->kl_coef) return fail(VAE_E_BADARG, "elbo_fwd: args");
+  if (a->batch <= 0 || a->batch > 1024 || a->latent <= 0 || a->img_elems <= 0) return fail(VAE_E_BADSHAPE, "elbo_fwd: sizes");
+  if (a->kind < VAE_LOSS_VANILLA || a->kind > VAE_LOSS_IWAE) return fail(VAE_E_BADARG, "elbo_fwd: kind");
+  hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *a);
+  return check_launch("elbo_fwd");
+}
+
+extern "C" int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v, const int32_t* step,
+                             const float* lr, float beta1, float beta2, float eps, float weight_decay, void* p_lowp,
+                             void* stream) {
+  if (n <= 0) return VAE_OK;
+  if (!p || !g || !m || !v || !step || !lr) return fail(VAE_E_BADARG, "adam_step: null");
+  const int grid = grid_for(n);
+  if (p_lowp)
+    hipLaunchKernelGGL(adam_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)p_lowp);
+  else
+    hipLaunchKernelGGL(adam_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)nullptr);
+  return check_launch("adam_step");
+}
+
+extern "C" int vae_cast_bf16(int64_t n, const float* src, void* dst, void* stream) {
+  if (n <= 0) return VAE_OK;
+  if (!src || !dst) return fail(VAE_E_BADARG, "cast_bf16: null");
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (long)n, src, (__bf16*)dst);
+  return check_launch("cast_bf16");
+}
+
+extern "C" int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream) {
+  if (bytes < 0 || (bytes > 0 && !zero)) return fail(VAE_E_BADARG, "step_begin: args");
+  if (((uintptr_t)zero & 15) != 0) return fail(VAE_E_BADARG, "step_begin: zero region must be 16-B aligned");
+  const long n16 = bytes / 16;
+  const int ntail = (int)(bytes - n16 * 16);
+  hipLaunchKernelGGL(step_begin_kernel, dim3(grid_for(n16 > 0 ? n16 : 1)), dim3(256), 0, (hipStream_t)stream,
+                     (f32x4*)zero, n16, (unsigned char*)zero + n16 * 16, ntail, (int*)step);
+  return check_launch("step_begin");
+}

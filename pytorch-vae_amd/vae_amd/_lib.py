@@ -1,0 +1,145 @@
+"""ctypes binding of libvaehip.so (include/vaehip.h).
+
+The library is the product: there is no CPU or PyTorch fallback.  Loading fails loudly
+when the shared object is missing, and every call raises ``VaeHipError`` with the
+library's message when it returns non-zero.  torch is imported first so the process has a
+single HIP runtime (torch's bundled libamdhip64, which the library binds by soname).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_float, c_int32, c_int64, c_void_p
+
+import torch  # noqa: F401  (must precede the library: one HIP runtime per process)
+
+LIB_NAME = "libvaehip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+ABI_VERSION = 1
+
+F32, BF16 = 0, 1
+X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
+LOSS_VANILLA, LOSS_BETA_H, LOSS_BETA_B, LOSS_IWAE = 0, 1, 2, 3
+
+
+class VaeHipError(RuntimeError):
+    pass
+
+
+class Xform(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("channels", c_int32), ("slope", c_float), ("count", c_float),
+                ("eps", c_float), ("momentum", c_float),
+                ("sum", c_void_p), ("sumsq", c_void_p), ("shift", c_void_p), ("gamma", c_void_p),
+                ("beta", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("aux", c_void_p),
+                ("running_mean", c_void_p), ("running_var", c_void_p)]
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
+                ("k", c_int32), ("p", c_int32), ("q", c_int32), ("r", c_int32), ("stride", c_int32),
+                ("pad", c_int32), ("x_nchw_f32", c_int32),
+                ("x", c_void_p), ("x_xf", Xform), ("wt", c_void_p), ("bias", c_void_p), ("y", c_void_p),
+                ("y_sum", c_void_p), ("y_sumsq", c_void_p), ("residual", c_void_p), ("residual_xf", Xform),
+                ("dy", c_void_p), ("dy_xf", Xform), ("dx", c_void_p), ("dx_epi", Xform),
+                ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
+                ("split_k", c_int32)]
+
+
+class LinearArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("m", c_int32), ("n", c_int32), ("k", c_int32),
+                ("x", c_void_p), ("x_xf", Xform), ("wt", c_void_p), ("bias", c_void_p), ("y", c_void_p),
+                ("y_f32", c_int32), ("dy", c_void_p), ("dy_f32", c_int32), ("dx", c_void_p), ("dx_epi", Xform),
+                ("dx_dgamma", c_void_p),
+                ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
+                ("mulv", c_void_p), ("eps", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p),
+                ("samples", c_int32)]
+
+
+class HeadArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
+                ("x", c_void_p), ("x_xf", Xform), ("wt", c_void_p), ("bias", c_void_p),
+                ("target", c_void_p), ("samples", c_int32), ("recon", c_void_p), ("sse", c_void_p),
+                ("coef", c_void_p), ("dx", c_void_p), ("dx_epi", Xform), ("dx_dgamma", c_void_p),
+                ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p), ("grad_recon", c_void_p)]
+
+
+class ElboArgs(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("batch", c_int32), ("samples", c_int32), ("latent", c_int32),
+                ("img_elems", c_int32), ("kld_weight", c_float), ("beta", c_float), ("gamma", c_float),
+                ("c_max", c_float), ("c_stop_iter", c_float), ("iter", c_void_p), ("mulv", c_void_p),
+                ("sse", c_void_p), ("out", c_void_p), ("per_img", c_void_p), ("head_coef", c_void_p),
+                ("kl_coef", c_void_p)]
+
+
+# name -> (argtypes)
+_SIGS = {
+    "vae_abi_version": [],
+    "vae_last_error": [],
+    "vae_conv2d_fwd": [POINTER(ConvArgs), c_void_p],
+    "vae_conv2d_bwd_data": [POINTER(ConvArgs), c_void_p],
+    "vae_conv2d_bwd_filter": [POINTER(ConvArgs), c_void_p],
+    "vae_convT2d_fwd": [POINTER(ConvArgs), c_void_p],
+    "vae_convT2d_bwd_data": [POINTER(ConvArgs), c_void_p],
+    "vae_convT2d_bwd_filter": [POINTER(ConvArgs), c_void_p],
+    "vae_linear_fwd": [POINTER(LinearArgs), c_void_p],
+    "vae_linear_bwd_data": [POINTER(LinearArgs), c_void_p],
+    "vae_linear_bwd_filter": [POINTER(LinearArgs), c_void_p],
+    "vae_head_fwd": [POINTER(HeadArgs), c_void_p],
+    "vae_head_bwd_data": [POINTER(HeadArgs), c_void_p],
+    "vae_head_bwd_filter": [POINTER(HeadArgs), c_void_p],
+    "vae_reparam_fwd": [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p],
+    "vae_elbo_fwd": [POINTER(ElboArgs), c_void_p],
+    "vae_adam_step": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float,
+                      c_float, c_float, c_void_p, c_void_p],
+    "vae_cast_bf16": [c_int64, c_void_p, c_void_p, c_void_p],
+    "vae_step_begin": [c_void_p, c_int64, c_void_p, c_void_p],
+}
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library (no GPU work).  Raises if it is missing or the ABI differs."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise VaeHipError(f"{path} not found — build it with `make -C pytorch-vae_amd/csrc` "
+                          f"(or __graft_entry__.build()); there is no fallback path")
+    lib = ctypes.CDLL(path)
+    for name, argtypes in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_char_p if name == "vae_last_error" else c_int32
+    if lib.vae_abi_version() != ABI_VERSION:
+        raise VaeHipError(f"libvaehip ABI {lib.vae_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.vae_last_error().decode(errors="replace")
+        raise VaeHipError(f"{name} failed (rc={rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise VaeHipError(f"unsupported dtype {dt}")

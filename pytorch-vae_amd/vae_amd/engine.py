@@ -1,0 +1,118 @@
+"""Fused training step: step_begin -> forward -> ELBO -> backward -> [grad all-reduce] -> Adam.
+
+Replaces Lightning's loop around experiment.VAEXperiment.training_step (experiment.py:45-86)
+plus torch.optim.Adam (experiment.py:308-311) for the hot path.  One step is a fixed launch
+sequence on one stream; `TrainStep(graph=True)` captures it into HIP graphs so a step costs
+one or two graph launches from the host.  Data parallelism (DDP semantics of run.py:86:
+per-rank BatchNorm statistics, gradient mean over ranks) all-reduces the flat gradient
+buffer with RCCL between the backward graph and the optimizer graph.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from .net import StepPlan, VAENet
+
+
+class FusedAdam:
+    """torch.optim.Adam semantics (lerp first moment, bias-corrected) over the flat buffer;
+    also refreshes the bf16 weight copy in the same pass.  step and lr are device scalars."""
+
+    def __init__(self, net: VAENet, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+        self.net = net
+        self.m = torch.zeros_like(net.params)
+        self.v = torch.zeros_like(net.params)
+        self.step = torch.zeros(1, dtype=torch.int32, device=net.device)
+        self.lr = torch.full((1,), float(lr), dtype=torch.float32, device=net.device)
+        self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
+
+    def set_lr(self, lr: float):
+        self.lr.fill_(float(lr))
+
+    def apply(self, grads: torch.Tensor, stream=None):
+        net = self.net
+        L.call("vae_adam_step", net.params.numel(), net.params.data_ptr(), grads.data_ptr(), self.m.data_ptr(),
+               self.v.data_ptr(), self.step.data_ptr(), self.lr.data_ptr(), self.betas[0], self.betas[1], self.eps,
+               self.weight_decay, net.lowp.data_ptr() if net.lowp is not None else None,
+               stream if stream is not None else L.stream_ptr())
+
+
+class TrainStep:
+    """One full training step of the VanillaVAE family on fixed-shape device buffers.
+
+    Inputs live in `plan.x` (NCHW fp32 images) and `plan.eps` (N(0,1) noise, the reference's
+    torch.randn_like at vanilla_vae.py:116); write them before calling, or pass tensors."""
+
+    def __init__(self, net: VAENet, plan: StepPlan, opt: FusedAdam, *, graph: bool = True,
+                 process_group=None):
+        self.net, self.plan, self.opt = net, plan, opt
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.use_graph = graph
+        self.g_main: Optional[torch.cuda.CUDAGraph] = None
+        self.g_opt: Optional[torch.cuda.CUDAGraph] = None
+        self.stream = torch.cuda.Stream(device=net.device)
+
+    # -------------------------------------------------------------- eager pieces
+    def _main(self):
+        p = self.plan
+        st = L.stream_ptr()
+        L.call("vae_step_begin", p.zero.data_ptr(), p.zero.numel() * 4, self.opt.step.data_ptr(), st)
+        if p.loss_kind == L.LOSS_BETA_B:
+            p.num_iter.add_(1.0)
+        p.forward(st)
+        p.backward(st)
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.plan.grads, op=dist.ReduceOp.AVG, group=self.pg)
+            # BatchNorm running stats are per rank; DDP broadcasts rank 0's buffers each
+            # forward (broadcast_buffers=True), which we mirror after the update.
+            dist.broadcast(self.net.running, src=0, group=self.pg)
+
+    def _opt(self):
+        self.opt.apply(self.plan.grads, L.stream_ptr())
+
+    def _capture(self):
+        # warm up on a side stream (allocations, lazy init), then capture
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream())
+        state = (self.net.params.clone(), self.net.running.clone(), self.opt.m.clone(), self.opt.v.clone(),
+                 self.opt.step.clone(), self.plan.num_iter.clone())
+        with torch.cuda.stream(s):
+            self._main()
+            self._opt()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        # restore what the warm-up step changed
+        self.net.params.copy_(state[0]); self.net.running.copy_(state[1]); self.opt.m.copy_(state[2])
+        self.opt.v.copy_(state[3]); self.opt.step.copy_(state[4]); self.plan.num_iter.copy_(state[5])
+        self.net.sync_lowp()
+        self.g_main = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_main, stream=s):
+            self._main()
+        self.g_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_opt, stream=s):
+            self._opt()
+        torch.cuda.synchronize()
+
+    def __call__(self, x: Optional[torch.Tensor] = None, eps: Optional[torch.Tensor] = None):
+        if x is not None:
+            self.plan.x.copy_(x)
+        if eps is not None:
+            self.plan.eps.copy_(eps.reshape(self.plan.eps.shape))
+        if not self.use_graph:
+            self._main()
+            self._allreduce()
+            self._opt()
+        else:
+            if self.g_main is None:
+                self._capture()
+            self.g_main.replay()
+            self._allreduce()
+            self.g_opt.replay()
+        self.net.num_batches_tracked += 1

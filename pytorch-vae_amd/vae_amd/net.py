@@ -1,0 +1,436 @@
+"""The VanillaVAE-family network on libvaehip (VanillaVAE, BetaVAE, IWAE share it).
+
+Reference: models/vanilla_vae.py:11-146 (network, reparameterize, ELBO), beta_vae.py:129-152,
+iwae.py:95-160, experiment.py:45-86 (the step that calls it), experiment.py:308-311 (Adam).
+
+Design (MI355X-first):
+  * weights live in one flat fp32 buffer in native layouts (layout.py); in bf16 mode a bf16
+    copy of the GEMM weights is refreshed by the fused Adam kernel;
+  * activations are NHWC and stored *pre-BatchNorm*: every BatchNorm+LeakyReLU is applied by
+    the consuming kernel on load, the producing kernel accumulates Σ/Σ² per channel in its
+    epilogue, and backward folds BN-backward into the next kernel's load the same way;
+  * a `StepPlan` preallocates every buffer for one batch shape and prebuilds the ctypes
+    argument blocks of the ~40 launches of a training step, so a step is a fixed launch
+    sequence on one stream — capturable into a HIP graph (engine.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _lib as L
+from .layout import Layout, default_init, reference_key_order, vanilla_layout
+
+SLOPE = 0.01         # nn.LeakyReLU default
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+class VAENet:
+    """Parameters + BatchNorm state of the VanillaVAE conv stack on one device."""
+
+    def __init__(self, in_channels: int = 3, latent_dim: int = 128, hidden_dims: Optional[List[int]] = None,
+                 img_size: int = 64, dtype: torch.dtype = torch.float32, device=None,
+                 generator: Optional[torch.Generator] = None):
+        self.in_channels = in_channels
+        self.latent_dim = latent_dim
+        self.hidden_dims = list(hidden_dims or [32, 64, 128, 256, 512])
+        self.img_size = img_size
+        if img_size % (2 ** len(self.hidden_dims)) or img_size // (2 ** len(self.hidden_dims)) != 2:
+            raise ValueError("the reference's bottleneck is a [C,2,2] map (fc_mu = hidden_dims[-1]*4, "
+                             "models/vanilla_vae.py:36): need img_size == 2 * 2**len(hidden_dims)")
+        if in_channels != 3:
+            raise ValueError("the head reconstructs 3 channels (vanilla_vae.py:73); in_channels must be 3")
+        self.dtype = dtype
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.layout: Layout = vanilla_layout(in_channels, latent_dim, self.hidden_dims)
+        self.ref_order = reference_key_order(in_channels, latent_dim, self.hidden_dims)
+        self.params = torch.zeros(self.layout.total, dtype=torch.float32, device=self.device)
+        self.running = torch.zeros(self.layout.bn_total, dtype=torch.float32, device=self.device)
+        cpu_p = torch.zeros(self.layout.total)
+        cpu_r = torch.zeros(self.layout.bn_total)
+        default_init(self.layout, cpu_p, cpu_r, generator)
+        self.params.copy_(cpu_p)
+        self.running.copy_(cpu_r)
+        self.lowp = (torch.zeros(self.layout.total, dtype=torch.bfloat16, device=self.device)
+                     if dtype == torch.bfloat16 else None)
+        self.num_batches_tracked = 0
+        self.sync_lowp()
+
+    # ------------------------------------------------------------------ state
+    @property
+    def dcode(self) -> int:
+        return L.dtype_code(self.dtype)
+
+    def sync_lowp(self):
+        """Refresh the bf16 weight copy from the fp32 master (bf16 mode only)."""
+        if self.lowp is not None:
+            L.call("vae_cast_bf16", self.params.numel(), self.params.data_ptr(), self.lowp.data_ptr(), L.stream_ptr())
+
+    def load_reference_state_dict(self, sd: Dict[str, torch.Tensor]):
+        self.layout.load_reference(self.params, self.running, {k: v.to(self.device) for k, v in sd.items()})
+        nbt = sd.get(self.layout.bns[0].prefix + ".num_batches_tracked")
+        self.num_batches_tracked = int(nbt) if nbt is not None else 0
+        self.sync_lowp()
+
+    def reference_state_dict(self) -> Dict[str, torch.Tensor]:
+        return self.layout.export_reference(self.params, self.running, self.num_batches_tracked, self.ref_order)
+
+    # ------------------------------------------------------------------ pointers
+    def p(self, name: str) -> int:
+        """fp32 master pointer of a parameter."""
+        s = self.layout.by_name[name]
+        return self.params.data_ptr() + 4 * s.offset
+
+    def w(self, name: str) -> int:
+        """Pointer of the copy a GEMM reads (bf16 in bf16 mode)."""
+        s = self.layout.by_name[name]
+        if self.lowp is not None:
+            return self.lowp.data_ptr() + 2 * s.offset
+        return self.params.data_ptr() + 4 * s.offset
+
+    def run_mean(self, prefix: str) -> int:
+        b = self.layout.bn_by_prefix[prefix]
+        return self.running.data_ptr() + 4 * b.offset
+
+    def run_var(self, prefix: str) -> int:
+        b = self.layout.bn_by_prefix[prefix]
+        return self.running.data_ptr() + 4 * (b.offset + b.channels)
+
+
+class StepPlan:
+    """All buffers and prebuilt launches of one training step for a fixed batch shape.
+
+    loss: 'vanilla' | 'betaH' | 'betaB' | 'iwae';  samples: IWAE S (decoder batch B*S).
+    grads land in `self.grads` (same layout as net.params); `zero` (grads, BN sums, SSE,
+    d[mu|logvar]) is cleared by `vae_step_begin` at the start of every step."""
+
+    def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
+                 samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
+                 capacity_max_iter: float = 1e5):
+        self.net = net
+        self.B = batch
+        self.S = samples if loss == "iwae" else 1
+        self.loss_kind = {"vanilla": L.LOSS_VANILLA, "betaH": L.LOSS_BETA_H, "betaB": L.LOSS_BETA_B,
+                          "iwae": L.LOSS_IWAE}[loss]
+        self.kld_weight, self.beta, self.gamma = kld_weight, beta, gamma
+        self.c_max, self.c_stop = max_capacity, capacity_max_iter
+        dev, T = net.device, net.dtype
+        D, h, img = net.latent_dim, net.hidden_dims, net.img_size
+        B, BS = self.B, self.B * self.S
+        self._keep = []            # ctypes structs referenced by the call lists
+
+        # -------- buffers
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.x = torch.zeros(B, 3, img, img, **f32)                     # NCHW input (reference layout)
+        self.eps = torch.zeros(BS, D, **f32)
+        self.enc = []
+        sp = img
+        for c in h:
+            sp //= 2
+            self.enc.append(torch.empty(B, sp, sp, c, dtype=T, device=dev))
+        self.mulv = torch.empty(B, 2 * D, **f32)
+        self.z = torch.empty(BS, D, dtype=T, device=dev)
+        r = h[::-1]
+        self.h0 = torch.empty(BS, 2, 2, r[0], dtype=T, device=dev)
+        self.dec = []
+        sp = 2
+        for i in range(len(r) - 1):
+            sp *= 2
+            self.dec.append(torch.empty(BS, sp, sp, r[i + 1], dtype=T, device=dev))
+        self.fin = torch.empty(BS, img, img, r[-1], dtype=T, device=dev)
+        self.recon = torch.empty(BS, 3, img, img, **f32)
+        self.out = torch.zeros(4, **f32)                                  # loss, recon, KLD(report), kld
+        self.per_img = torch.zeros(BS, **f32)
+        self.head_coef = torch.zeros(BS, **f32)
+        self.kl_coef = torch.zeros(BS, **f32)
+        self.num_iter = torch.zeros(1, **f32)                             # BetaVAE-B counter (beta_vae.py:132)
+        # backward buffers (gradients w.r.t. pre-activation of each stored tensor)
+        self.g_enc = [torch.empty_like(t) for t in self.enc]
+        self.g_h0 = torch.empty_like(self.h0)
+        self.g_dec = [torch.empty_like(t) for t in self.dec]
+        self.g_fin = torch.empty_like(self.fin)
+        # zero region: grads | BN sums | sse | dmulv   (16-B aligned pieces)
+        nbn = sum(b.channels for b in net.layout.bns)
+        nz = net.layout.total + 2 * nbn + _pad4(BS) + _pad4(B * 2 * D)
+        self.zero = torch.zeros(nz, **f32)
+        o = 0
+        self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
+        self.bnsum: Dict[str, torch.Tensor] = {}
+        for b in net.layout.bns:
+            self.bnsum[b.prefix] = self.zero[o:o + 2 * b.channels]; o += 2 * b.channels
+        self.sse = self.zero[o:o + BS]; o += _pad4(BS)
+        self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
+        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.fwd_calls: List = []
+        self.bwd_calls: List = []
+        self._build()
+
+    # ------------------------------------------------------------------ helpers
+    def g(self, name: str) -> int:
+        s = self.net.layout.by_name[name]
+        return self.grads.data_ptr() + 4 * s.offset
+
+    def _bn_prod_bias(self, prefix: str) -> str:
+        return prefix[:-2] + ".0.bias"          # "encoder.3.1" -> "encoder.3.0.bias"
+
+    def bn_xf(self, prefix: str, kind: int, count: int, aux=None, running: bool = False) -> L.Xform:
+        net = self.net
+        C = net.layout.bn_by_prefix[prefix].channels
+        s = self.bnsum[prefix]
+        xf = L.Xform(kind=kind, channels=C, slope=SLOPE, count=float(count), eps=BN_EPS, momentum=BN_MOMENTUM)
+        xf.sum = s.data_ptr()
+        xf.sumsq = s.data_ptr() + 4 * C
+        xf.shift = net.p(self._bn_prod_bias(prefix))
+        xf.gamma = net.p(prefix + ".weight")
+        xf.beta = net.p(prefix + ".bias")
+        if kind == L.X_BN_DY:
+            xf.dgamma = self.g(prefix + ".weight")
+            xf.dbeta = self.g(prefix + ".bias")
+        if aux is not None:
+            xf.aux = aux.data_ptr()
+        if running:
+            xf.running_mean = net.run_mean(prefix)
+            xf.running_var = net.run_var(prefix)
+        return xf
+
+    def _add(self, lst, fn, arg):
+        self._keep.append(arg)
+        lst.append((fn, ctypes.byref(arg)))
+
+    # ------------------------------------------------------------------ plan
+    def _build(self):
+        net, T = self.net, self.net.dcode
+        h = net.hidden_dims
+        r = h[::-1]
+        D = net.latent_dim
+        B, BS = self.B, self.B * self.S
+        img = net.img_size
+        nenc = len(h)
+        enc_pre = [f"encoder.{i}.1" for i in range(nenc)]
+        dec_pre = [f"decoder.{i}.1" for i in range(len(r) - 1)] + ["final_layer.1"]
+        dec_w = [f"decoder.{i}.0" for i in range(len(r) - 1)] + ["final_layer.0"]
+        dec_out = self.dec + [self.fin]
+        g_dec_out = self.g_dec + [self.g_fin]
+
+        def cnt(t):   # BN reduction size of a stored NHWC map
+            return t.shape[0] * t.shape[1] * t.shape[2]
+
+        F = self.fwd_calls
+        # ---------------------------------------------------------------- encoder
+        sp = img
+        for i in range(nenc):
+            a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=(3 if i == 0 else h[i - 1]), k=h[i], p=sp // 2, q=sp // 2,
+                           r=3, stride=2, pad=1)
+            if i == 0:
+                a.x_nchw_f32 = 1
+                a.x = self.x.data_ptr()
+            else:
+                a.x = self.enc[i - 1].data_ptr()
+                a.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]), running=True)
+            a.wt = net.w(f"encoder.{i}.0.weight")
+            a.bias = net.p(f"encoder.{i}.0.bias")
+            a.y = self.enc[i].data_ptr()
+            a.y_sum = self.bnsum[enc_pre[i]].data_ptr()
+            a.y_sumsq = a.y_sum + 4 * h[i]
+            self._add(F, "vae_conv2d_fwd", a)
+            sp //= 2
+        # ---------------------------------------------------------------- fc_mu | fc_var
+        a = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
+        a.x = self.enc[-1].data_ptr()
+        a.x_xf = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), running=True)
+        a.wt = net.w("fc_mu.weight")
+        a.bias = net.p("fc_mu.bias")
+        a.y = self.mulv.data_ptr()
+        a.y_f32 = 1
+        self._add(F, "vae_linear_fwd", a)
+        self._reparam = (T, BS, self.S, D, self.mulv.data_ptr(), self.eps.data_ptr(), self.z.data_ptr())
+        F.append(("vae_reparam_fwd", None))
+        # ---------------------------------------------------------------- decoder_input
+        a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
+        a.x = self.z.data_ptr()
+        a.wt = net.w("decoder_input.weight")
+        a.bias = net.p("decoder_input.bias")
+        a.y = self.h0.data_ptr()
+        self._add(F, "vae_linear_fwd", a)
+        # ---------------------------------------------------------------- decoder (ConvT)
+        sp = 2
+        prev, prev_pre = self.h0, None
+        for i in range(len(r)):
+            cin = r[i] if i < len(r) - 1 else r[-1]
+            cout = r[i + 1] if i < len(r) - 1 else r[-1]
+            a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
+            a.x = prev.data_ptr()
+            if prev_pre is not None:
+                a.x_xf = self.bn_xf(prev_pre, L.X_BN_ACT, cnt(prev), running=True)
+            a.wt = net.w(dec_w[i] + ".weight")
+            a.bias = net.p(dec_w[i] + ".bias")
+            a.y = dec_out[i].data_ptr()
+            a.y_sum = self.bnsum[dec_pre[i]].data_ptr()
+            a.y_sumsq = a.y_sum + 4 * cout
+            self._add(F, "vae_convT2d_fwd", a)
+            prev, prev_pre = dec_out[i], dec_pre[i]
+            sp *= 2
+        # ---------------------------------------------------------------- head + SSE
+        hd = L.HeadArgs(dtype=T, n=BS, h=img, w=img, c=r[-1], samples=self.S)
+        hd.x = self.fin.data_ptr()
+        hd.x_xf = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin), running=True)
+        hd.wt = net.p("final_layer.3.weight")
+        hd.bias = net.p("final_layer.3.bias")
+        hd.target = self.x.data_ptr()
+        hd.recon = self.recon.data_ptr()
+        hd.sse = self.sse.data_ptr()
+        self._add(F, "vae_head_fwd", hd)
+        # ---------------------------------------------------------------- ELBO
+        e = L.ElboArgs(kind=self.loss_kind, batch=B, samples=self.S, latent=D, img_elems=3 * img * img,
+                       kld_weight=self.kld_weight, beta=self.beta, gamma=self.gamma, c_max=self.c_max,
+                       c_stop_iter=self.c_stop)
+        e.iter = self.num_iter.data_ptr()
+        e.mulv = self.mulv.data_ptr()
+        e.sse = self.sse.data_ptr()
+        e.out = self.out.data_ptr()
+        e.per_img = self.per_img.data_ptr()
+        e.head_coef = self.head_coef.data_ptr()
+        e.kl_coef = self.kl_coef.data_ptr()
+        self._add(F, "vae_elbo_fwd", e)
+
+        # ================================================================ backward
+        Bw = self.bwd_calls
+        hb = L.HeadArgs(dtype=T, n=BS, h=img, w=img, c=r[-1], samples=self.S)
+        hb.x = self.fin.data_ptr()
+        hb.x_xf = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin))
+        hb.wt = net.p("final_layer.3.weight")
+        hb.bias = net.p("final_layer.3.bias")
+        hb.target = self.x.data_ptr()
+        hb.recon = self.recon.data_ptr()
+        hb.coef = self.head_coef.data_ptr()
+        hb.dx = self.g_fin.data_ptr()
+        hb.dx_epi = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin))
+        hb.dx_epi.aux = self.fin.data_ptr()
+        hb.dx_dgamma = self.g("final_layer.1.weight")
+        hb.dx_dbeta = self.g("final_layer.1.bias")
+        hb.dw = self.g("final_layer.3.weight")
+        hb.db = self.g("final_layer.3.bias")
+        self._add(Bw, "vae_head_bwd_data", hb)
+        self._add(Bw, "vae_head_bwd_filter", hb)
+        # decoder, last block first
+        sps = [2 * 2 ** i for i in range(len(r))]          # input spatial of each ConvT
+        for i in reversed(range(len(r))):
+            sp = sps[i]
+            cin = r[i] if i < len(r) - 1 else r[-1]
+            cout = r[i + 1] if i < len(r) - 1 else r[-1]
+            x_t = self.h0 if i == 0 else dec_out[i - 1]
+            gx_t = self.g_h0 if i == 0 else g_dec_out[i - 1]
+            dy_xf = self.bn_xf(dec_pre[i], L.X_BN_DY, cnt(dec_out[i]), aux=dec_out[i])
+            a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
+            a.dy = g_dec_out[i].data_ptr()
+            a.dy_xf = dy_xf
+            a.wt = net.w(dec_w[i] + ".weight")
+            a.dx = gx_t.data_ptr()
+            if i > 0:
+                a.dx_epi = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t), aux=x_t)
+                a.dx_dgamma = self.g(dec_pre[i - 1] + ".weight")
+                a.dx_dbeta = self.g(dec_pre[i - 1] + ".bias")
+            self._add(Bw, "vae_convT2d_bwd_data", a)
+            f = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
+            f.x = x_t.data_ptr()
+            if i > 0:
+                f.x_xf = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t))
+            f.dy = g_dec_out[i].data_ptr()
+            f.dy_xf = dy_xf
+            f.dw = self.g(dec_w[i] + ".weight")
+            f.db = self.g(dec_w[i] + ".bias")
+            self._add(Bw, "vae_convT2d_bwd_filter", f)
+        # decoder_input: dz -> d[mu|logvar] (reparameterization + KL), and its weight grads
+        a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
+        a.dy = self.g_h0.data_ptr()
+        a.wt = net.w("decoder_input.weight")
+        a.mulv = self.mulv.data_ptr()
+        a.eps = self.eps.data_ptr()
+        a.kl_coef = self.kl_coef.data_ptr()
+        a.dmulv = self.dmulv.data_ptr()
+        a.samples = self.S
+        self._add(Bw, "vae_linear_bwd_data", a)
+        f = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
+        f.dy = self.g_h0.data_ptr()
+        f.x = self.z.data_ptr()
+        f.dw = self.g("decoder_input.weight")
+        f.db = self.g("decoder_input.bias")
+        self._add(Bw, "vae_linear_bwd_filter", f)
+        # fc_mu | fc_var
+        a = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
+        a.dy = self.dmulv.data_ptr()
+        a.dy_f32 = 1
+        a.wt = net.w("fc_mu.weight")
+        a.dx = self.g_enc[-1].data_ptr()
+        a.dx_epi = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), aux=self.enc[-1])
+        a.dx_dgamma = self.g(enc_pre[-1] + ".weight")
+        a.dx_dbeta = self.g(enc_pre[-1] + ".bias")
+        self._add(Bw, "vae_linear_bwd_data", a)
+        f = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
+        f.dy = self.dmulv.data_ptr()
+        f.dy_f32 = 1
+        f.x = self.enc[-1].data_ptr()
+        f.x_xf = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]))
+        f.dw = self.g("fc_mu.weight")
+        f.db = self.g("fc_mu.bias")
+        self._add(Bw, "vae_linear_bwd_filter", f)
+        # encoder, last block first
+        sps = [img // 2 ** i for i in range(nenc)]
+        for i in reversed(range(nenc)):
+            sp = sps[i]
+            cin = 3 if i == 0 else h[i - 1]
+            dy_xf = self.bn_xf(enc_pre[i], L.X_BN_DY, cnt(self.enc[i]), aux=self.enc[i])
+            f = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
+            f.dy = self.g_enc[i].data_ptr()
+            f.dy_xf = dy_xf
+            if i == 0:
+                f.x_nchw_f32 = 1
+                f.x = self.x.data_ptr()
+            else:
+                f.x = self.enc[i - 1].data_ptr()
+                f.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]))
+            f.dw = self.g(f"encoder.{i}.0.weight")
+            f.db = self.g(f"encoder.{i}.0.bias")
+            self._add(Bw, "vae_conv2d_bwd_filter", f)
+            if i > 0:
+                a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
+                a.dy = self.g_enc[i].data_ptr()
+                a.dy_xf = dy_xf
+                a.wt = net.w(f"encoder.{i}.0.weight")
+                a.dx = self.g_enc[i - 1].data_ptr()
+                a.dx_epi = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]), aux=self.enc[i - 1])
+                a.dx_dgamma = self.g(enc_pre[i - 1] + ".weight")
+                a.dx_dbeta = self.g(enc_pre[i - 1] + ".bias")
+                self._add(Bw, "vae_conv2d_bwd_data", a)
+
+    # ------------------------------------------------------------------ execution
+    def _run(self, calls, stream):
+        for fn, arg in calls:
+            if fn == "vae_reparam_fwd":
+                L.call(fn, *self._reparam, stream)
+            else:
+                L.call(fn, arg, stream)
+
+    def begin(self, stream=None):
+        stream = stream if stream is not None else L.stream_ptr()
+        L.call("vae_step_begin", self.zero.data_ptr(), self.zero.numel() * 4, self.step.data_ptr(), stream)
+        if self.loss_kind == L.LOSS_BETA_B:
+            self.num_iter.add_(1.0)
+
+    def forward(self, stream=None):
+        self._run(self.fwd_calls, stream if stream is not None else L.stream_ptr())
+
+    def backward(self, stream=None):
+        self._run(self.bwd_calls, stream if stream is not None else L.stream_ptr())
+
+    def loss_dict(self) -> Dict[str, float]:
+        o = self.out.tolist()
+        third = "KLD"
+        return {"loss": o[0], "Reconstruction_Loss": o[1], third: o[2]}
+
+
+def _pad4(n: int) -> int:
+    return (n + 3) // 4 * 4

@@ -1,0 +1,123 @@
+"""Teacher-forced one-step parity of the fused MI355X training step against the reference's
+golden vectors (tests/golden, produced by the reference's own modules) and the CPU oracle.
+
+Bar (north_star): ELBO terms within 1e-4 relative in fp32 mode.  Also checked: mu/logvar,
+reconstructions, per-image MSE, every parameter gradient (norm within 1e-3, the measured
+CPU-vs-CPU spread of 1.1e-4 x 10), BN running statistics, and the params after Adam."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import case_inputs, load_case, summary
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["vanilla_b16", "vanilla_b8_kl", "betaH_b16", "betaB_b8", "iwae_b4"]
+
+
+def _plan_for(meta, dtype=torch.float32):
+    from vae_amd.engine import FusedAdam
+    from vae_amd.net import StepPlan, VAENet
+    kw = meta["ctor"]
+    net = VAENet(latent_dim=kw["latent_dim"], dtype=dtype, device="cuda")
+    arch = meta["arch"]
+    if arch == "VanillaVAE":
+        loss = "vanilla"
+    elif arch == "BetaVAE":
+        loss = "betaH" if kw.get("loss_type", "B") == "H" else "betaB"
+    else:
+        loss = "iwae"
+    plan = StepPlan(net, meta["batch"], loss=loss, kld_weight=meta["M_N"], samples=meta["samples"] or 1,
+                    beta=kw.get("beta", 4), gamma=kw.get("gamma", 1000.0), max_capacity=kw.get("max_capacity", 25),
+                    capacity_max_iter=kw.get("Capacity_max_iter", 1e5))
+    opt = FusedAdam(net, lr=meta["lr"])
+    return net, plan, opt
+
+
+def _run_step(meta, dtype=torch.float32):
+    sd, x, eps = case_inputs(meta)
+    net, plan, opt = _plan_for(meta, dtype)
+    net.load_reference_state_dict(sd)
+    plan.x.copy_(x)
+    plan.eps.copy_(eps.reshape(plan.eps.shape))
+    from vae_amd import _lib as L
+    st = L.stream_ptr()
+    L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
+    if plan.loss_kind == L.LOSS_BETA_B:
+        plan.num_iter.add_(1.0)
+    plan.forward(st)
+    plan.backward(st)
+    torch.cuda.synchronize()
+    return net, plan, opt
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_step_matches_reference(case):
+    meta, ref = load_case(case)
+    net, plan, opt = _run_step(meta)
+    out = plan.out.cpu().tolist()
+    got = {"loss": out[0], "Reconstruction_Loss": out[1]}
+    got["KLD"] = out[2]
+    for k in ("loss", "Reconstruction_Loss", "KLD"):
+        v = meta["loss"][k]
+        assert abs(got[k] - v) <= 1e-4 * abs(v), (k, got[k], v)
+    B = meta["batch"]
+    S = meta["samples"] or 1
+    recon = plan.recon.cpu()
+    if meta["arch"] == "IWAE":
+        recon = recon.view(B, S, 3, 64, 64)
+        per_img = plan.per_img.cpu().view(B, S).numpy()
+    else:
+        per_img = plan.per_img.cpu().numpy()
+    n_head = ref["recon_head"].shape[0]
+    np.testing.assert_allclose(recon[:n_head].numpy(), ref["recon_head"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(per_img, ref["per_img_mse"], rtol=1e-4)
+    mu = plan.mulv[:, :128].cpu().numpy()
+    lv = plan.mulv[:, 128:].cpu().numpy()
+    np.testing.assert_allclose(mu, ref["mu"], rtol=0, atol=1e-4 * np.abs(ref["mu"]).max())
+    np.testing.assert_allclose(lv, ref["log_var"], rtol=0, atol=1e-4 * np.abs(ref["log_var"]).max())
+    grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
+    worst = []
+    for name in meta["param_names"]:
+        g = grads[name]
+        st = summary(g)
+        rs = ref[f"grad_stats/{name}"]
+        if name.endswith(".0.bias") and not name.startswith("final_layer.3"):
+            # conv bias before train-mode BN: analytically zero gradient (rounding noise on
+            # both sides); bound it by the weight-gradient scale of the same layer
+            wref = ref[f"grad_stats/{name[:-4]}weight"]
+            assert st[2] <= 1e-4 * wref[2] + 1e-7, (name, st, rs)
+            continue
+        err = abs(st[1] - rs[1]) / max(rs[1], 1e-12)
+        worst.append((err, name))
+        assert err < 1e-3, (name, st, rs)
+        # element-wise: 1% of the tensor's largest entry (sums over 1e4-1e6 products with
+        # cancellation; the norm bar above is the 1e-3 parity criterion)
+        np.testing.assert_allclose(g.flatten()[:64].numpy(), ref[f"grad_head/{name}"], rtol=0,
+                                   atol=1e-2 * rs[2] + 1e-10, err_msg=name)
+    run = {k: v.cpu() for k, v in net.reference_state_dict().items()}
+    for k in ref:
+        if k.startswith("running/"):
+            np.testing.assert_allclose(run[k[8:]].numpy(), ref[k], rtol=1e-4, atol=1e-6, err_msg=k)
+    # Adam (one step from zero state) on the same gradients
+    opt.apply(plan.grads)
+    torch.cuda.synchronize()
+    newp = {k: v.cpu() for k, v in net.reference_state_dict().items()}
+    for name in meta["param_names"]:
+        if name.endswith(".0.bias") and not name.startswith("final_layer.3"):
+            continue
+        # first Adam step moves each weight by ~lr*sign(g); near-zero g makes that ratio
+        # sensitive, so compare to 1e-3 of the step size
+        np.testing.assert_allclose(newp[name].flatten()[:64].numpy(), ref[f"new_head/{name}"], rtol=0,
+                                   atol=1e-3 * meta["lr"] + 1e-7, err_msg=name)
+
+
+@pytest.mark.parametrize("case", ["vanilla_b16", "iwae_b4"])
+def test_step_bf16_close(case):
+    """bf16 throughput mode: ELBO terms within 2e-3 relative of the reference."""
+    meta, ref = load_case(case)
+    net, plan, opt = _run_step(meta, torch.bfloat16)
+    out = plan.out.cpu().tolist()
+    assert abs(out[0] - meta["loss"]["loss"]) <= 2e-3 * abs(meta["loss"]["loss"])
+    assert abs(out[1] - meta["loss"]["Reconstruction_Loss"]) <= 2e-3 * abs(meta["loss"]["Reconstruction_Loss"])
+    assert abs(out[2] - meta["loss"]["KLD"]) <= 2e-2 * abs(meta["loss"]["KLD"])
