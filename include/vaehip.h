@@ -111,7 +111,10 @@ typedef struct vae_conv_args {
   float* dx_dbeta;
   float* dw;               /* bwd_filter: fp32 weight gradient, native layout (accumulated) */
   float* db;               /* bwd_filter: fp32 bias gradient (accumulated) or NULL */
-  int32_t split_k;         /* bwd_filter: 0 = choose automatically */
+  int32_t split_k;         /* 0 = choose automatically, 1 = no split-K */
+  void* workspace;         /* fp32 scratch for split-K partial slabs (may be NULL: no split
+                              of fwd / bwd_data); reused by every call on the stream */
+  int64_t workspace_bytes;
 } vae_conv_args;
 
 /* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,
@@ -134,6 +137,8 @@ typedef struct vae_linear_args {
   const float* kl_coef;    /* [m] per-row coefficient of dKL (see vae_elbo_fwd) or NULL */
   float* dmulv;            /* [rows_mu][2*k], accumulated */
   int32_t samples;         /* rows per mu row (IWAE S; 1 otherwise) */
+  void* workspace;         /* as vae_conv_args.workspace */
+  int64_t workspace_bytes;
 } vae_linear_args;
 
 /* Final layer of the decoder: Conv2d(C->3, k3, s1, p1) + Tanh (vanilla_vae.py:73-75) and the

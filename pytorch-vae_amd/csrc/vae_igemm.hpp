@@ -4,11 +4,11 @@
 //
 // A and B are "operands": views of NHWC tensors / weight matrices with a per-channel
 // transform (BatchNorm+LeakyReLU forward, or BatchNorm backward) applied on load.  Tiles are
-// staged global -> registers -> LDS as [rows][BK] (k contiguous, padded), and read as MFMA
-// fragments: lane l owns row (l&15) and the 8 consecutive k of group (l>>4).  fp32 runs
-// v_mfma_f32_16x16x4_f32 eight times over those 8 k (k permuted inside the tile — the sum is
-// order-free); bf16 runs one v_mfma_f32_16x16x32_bf16.  The next tile's global loads are
-// issued before the MFMAs of the current one (register prefetch).
+// staged global -> registers -> LDS (double-buffered, one barrier per K-tile; the next tile's
+// global loads are in flight during the current tile's MFMAs) as [rows][BK] (k contiguous,
+// padded), and read as MFMA fragments: lane l owns row (l&15) and 8 consecutive k of group
+// (l>>4).  fp32 (BK=32) runs v_mfma_f32_16x16x4_f32 eight times over those 8 k (k permuted
+// inside the tile — the sum is order-free); bf16 (BK=64) runs v_mfma_f32_16x16x32_bf16 twice.
 //
 // Operand modes (vector direction V_K = 8 contiguous k per load, V_M = 4 contiguous rows):
 //   A_CONV   im2col gather of a strided conv (NHWC dtype, or the NCHW fp32 image)    V_K
@@ -18,10 +18,15 @@
 //   B_NK     weights [N][K]                                                        V_K
 //   B_KN     weights [K'][N] addressed through the phase tap tables (or dense)     V_M
 //   B_GATHER conv gather with n = (r,s,c), k = pixel (weight gradient)             V_M
+// Per-thread row state (pixel coordinates, base offsets) is computed once before the K loop;
+// index decompositions inside it use magic-number division (FastDiv).
+//
 // Epilogues: E_STORE (bias, residual, per-channel Σ/Σ² for the next BatchNorm),
 //            E_BNBWD (g = da·act'(z) of the producing layer, Σg -> dβ, Σg·x̂ -> dγ),
 //            E_ACC   (split-K fp32 atomic accumulation of weight gradients),
 //            E_REPARAM (dz -> d[mu|logvar] incl. the analytic KL gradient).
+// Split-K for the non-accumulating epilogues: each K-slice writes an fp32 slab and
+// igemm_finalize sums the slabs in a fixed order (deterministic) and runs the epilogue.
 #pragma once
 #include "vae_common.hpp"
 
@@ -32,11 +37,30 @@ enum BMode { B_NK = 0, B_KN = 1, B_GATHER = 2 };
 enum EMode { E_STORE = 0, E_BNBWD = 1, E_ACC = 2, E_REPARAM = 3 };
 
 constexpr int MAXC = 512;   // max channels of a per-channel transform table
-constexpr int BK = 32;
 constexpr int NTHREADS = 256;
 
+template <class T> constexpr int bk_of() { return sizeof(T) == 2 ? 64 : 32; }
+
+// Magic-number division for 0 <= n < 2^31 (round-up method; exact for every n in range).
+struct FastDiv {
+  uint32_t d, mul, shr;
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return d == 1 ? n : (__umulhi(n, mul) >> shr); }
+};
+
+inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d < 1 ? 1 : d;
+  if (f.d == 1) { f.mul = 0; f.shr = 0; return f; }
+  uint32_t l = 0;
+  while ((1u << l) < f.d) ++l;
+  const uint32_t p = 31 + l;
+  f.mul = (uint32_t)(((1ull << p) + f.d - 1) / f.d);
+  f.shr = p - 32;
+  return f;
+}
+
 struct GemmParams {
-  int M, N, K;               // K of phase 0 for A_CONVT (per-phase K from the tap tables)
+  int M, N, K;               // K unused for A_CONVT (per-phase K from the tap tables)
   int ksplit, nphase;
   // ---- A operand
   const void* a_ptr; int a_ld; vae_xform a_xf;
@@ -49,7 +73,8 @@ struct GemmParams {
   //   A_CONV/B_GATHER: tensor [gn][gh][gw][gc], output grid gp x gq, kernel gr, stride gs, pad gpad
   //   A_CONVT: input tensor [gn][gh][gw][gc] -> output gho x gwo, phase grid gp x gq
   int gn, gh, gw, gc, gp, gq, gr, gs, gpad, gho, gwo;
-  int ntap_h[2], ntap_w[2], tap_h[2][4], tap_w[2][4];
+  int ntap_h[2], ntap_w[2], tap0[2];   // phase ph: taps r = tap0[ph] + gs*t, t < ntap
+  FastDiv fd_gq, fd_gp, fd_gc, fd_gr, fd_ntw[2];
   // ---- epilogue
   void* out; int out_ld; int out_phase;      // out_phase: rows are phase-grid pixels
   int out_f32;               // E_STORE: write fp32 instead of T
@@ -57,248 +82,457 @@ struct GemmParams {
   const void* residual; vae_xform res_xf;
   vae_xform epi_xf; float* dgamma; float* dbeta;
   float* bias_grad;
+  float* dbc; int dbc_from_b;  // closed-form BN-followed bias gradient (wgrad, first block)
   const float* mulv; const float* eps; const float* kl_coef; float* dmulv; int samples, latent;
+  float* slab;               // split-K partials [nphase][ksplit][M][N] (non-ACC epilogues)
 };
 
-// ------------------------------------------------------------------ per-element transform
-template <class TIn, int MAXCT>
-__device__ __forceinline__ float xf_apply(const vae_xform& x, const XfTable<MAXCT, false>& t, float v,
-                                          int ch, const TIn* aux, long idx) {
-  switch (x.kind) {
-    case VAE_X_ACT: return lrelu(v, x.slope);
-    case VAE_X_BN_ACT: return lrelu(fmaf(v, t.a[ch], t.b[ch]), x.slope);
-    case VAE_X_BN_DY: return fmaf(t.a[ch], v, fmaf(t.b[ch], ld_f(aux + idx), t.c[ch]));
-    default: return v;
+// Phase-specific constants of a transposed-conv problem, resolved once per block with selects
+// (runtime indexing of kernarg arrays makes the compiler copy the whole struct to scratch).
+struct PhaseInfo {
+  int ph, pw, t0h, t0w, nth, ntw;
+  FastDiv fdw;
+};
+
+__device__ __forceinline__ PhaseInfo make_phase(const GemmParams& p, int phase) {
+  PhaseInfo q;
+  q.ph = phase >= p.gs ? 1 : 0;
+  q.pw = phase - q.ph * p.gs;
+  q.t0h = q.ph ? p.tap0[1] : p.tap0[0];
+  q.t0w = q.pw ? p.tap0[1] : p.tap0[0];
+  q.nth = q.ph ? p.ntap_h[1] : p.ntap_h[0];
+  q.ntw = q.pw ? p.ntap_w[1] : p.ntap_w[0];
+  q.fdw = q.pw ? p.fd_ntw[1] : p.fd_ntw[0];
+  return q;
+}
+
+// ------------------------------------------------------------------ per-channel tables
+// Views into dynamic LDS, sized by the real channel count of each transform:
+//   BN_ACT: v = lrelu(t*a + b)   BN_DY: v = a*t + b*aux + c   epilogue BN_ACT: x̂ = y*p + q
+struct Tab {
+  float *a, *b, *c, *p, *q;
+};
+
+__device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bool update_running) {
+  if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return;
+  for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
+    float mean, invstd, var;
+    bn_moments(x, ch, mean, invstd, var);
+    const float g = x.gamma[ch];
+    if (x.kind == VAE_X_BN_ACT) {
+      const float sc = g * invstd;
+      t.a[ch] = sc;
+      t.b[ch] = x.beta[ch] - mean * sc;
+      if (epi) { t.p[ch] = invstd; t.q[ch] = -mean * invstd; }
+      if (update_running && x.running_mean) {
+        const float m = x.momentum;
+        const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
+        x.running_mean[ch] = (1.f - m) * x.running_mean[ch] + m * mean;
+        x.running_var[ch] = (1.f - m) * x.running_var[ch] + m * unb;
+      }
+    } else {
+      const float inv_m = 1.0f / x.count;
+      const float A = g * invstd;
+      const float mg = x.dbeta[ch] * inv_m;         // mean of g
+      const float mgx = x.dgamma[ch] * inv_m;       // mean of g*xhat
+      t.a[ch] = A;
+      t.b[ch] = -A * invstd * mgx;
+      t.c[ch] = -A * (mg - mean * invstd * mgx);
+    }
   }
 }
 
-// --------------------------------------------------------------------- operand loading
-// Each thread loads "octets" of 8 elements: V_K = one row × 8 k, V_M = 4 rows × 2 k.
-template <class T, class TIn, int AM, int MAXCT>
-struct AOperand {
-  // V_K: rows [row], k0..k0+7
-  __device__ __forceinline__ static void load_vk(const GemmParams& p, const XfTable<MAXCT, false>& xt, int phase,
-                                 int row, int k0, int Kp, float (&v)[8]) {
+__host__ __device__ inline int tab_floats(const vae_xform& x, bool epi) {
+  if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return 0;
+  return (epi ? 4 : 3) * x.channels;
+}
+
+// ------------------------------------------------------------------ pending loads
+// A staged group of 8 elements: raw values, the BN-backward aux values, and masks.  The
+// transform is applied by finish() when the group is written to LDS, so nothing consumes a
+// global load before the MFMAs of the previous K-tile have been issued.
+struct Pend {
+  float v[8];
+  float y[8];
+  uint32_t mx;     // bit e: element e was loaded -> apply the transform
+  uint32_t keep;   // bit e: keep v[e] as is (the bias-gradient ones column)
+  int chb;         // transform channel of the group's first row / k
+};
+
+// element e -> row/k offset within the group: V_K: e (8 k), V_M: e >> 1 (4 rows x 2 k)
+template <bool VM>
+__device__ __forceinline__ void finish(const vae_xform& x, const Tab& t, Pend& g) {
+  const int C = x.channels;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.f;
-    if (row >= p.M || k0 >= Kp) return;
-    const TIn* X = static_cast<const TIn*>(p.a_ptr);
-    const TIn* aux = static_cast<const TIn*>(p.a_xf.aux);
-    if constexpr (AM == A_DENSE) {
-      const long base = (long)row * p.a_ld + k0;
-      if (k0 + 8 <= Kp && (p.a_ld & 7) == 0) {
-        ld8(X + base, v);
+  for (int e = 0; e < 8; ++e) {
+    const int off = VM ? (e >> 1) : e;
+    int ch = g.chb + off;
+    if (C >= 8) ch = ch >= C ? ch - C : ch;
+    else ch = ch % C;
+    float v = g.v[e];
+    if ((g.mx >> e) & 1u) {
+      switch (x.kind) {
+        case VAE_X_ACT: v = lrelu(v, x.slope); break;
+        case VAE_X_BN_ACT: v = lrelu(fmaf(v, t.a[ch], t.b[ch]), x.slope); break;
+        case VAE_X_BN_DY: v = fmaf(t.a[ch], v, fmaf(t.b[ch], g.y[e], t.c[ch])); break;
+        default: break;
+      }
+    } else if (!((g.keep >> e) & 1u)) {
+      v = 0.f;
+    }
+    g.v[e] = v;
+  }
+}
+
+// ------------------------------------------------------------------ V_K operand (row x 8 k)
+// Row state is computed once per thread slot; load() is called once per K-tile.
+template <class TIn, int MODE>
+struct RowOperand {
+  int valid;       // row in range
+  int vecok;       // A_DENSE / B_NK: 8-element vector loads are aligned
+  int n, hb, wb;   // A_CONV: image, top-left input coordinate; A_CONVT: image, ho, wo
+  long base;       // A_DENSE / B_NK: row offset
+
+  __device__ __forceinline__ void init(const GemmParams& p, int row, int rows, int phase, int ld) {
+    valid = row < rows;
+    if constexpr (MODE == A_DENSE || MODE == 100 + B_NK) {
+      base = (long)row * ld;
+      vecok = (ld & 7) == 0;
+    } else if constexpr (MODE == A_CONV) {
+      const uint32_t t = p.fd_gq.div(row), oq = row - t * p.gq;
+      const uint32_t nn = p.fd_gp.div(t), op = t - nn * p.gp;
+      n = nn; hb = op * p.gs - p.gpad; wb = oq * p.gs - p.gpad;
+    } else if constexpr (MODE == A_CONVT) {
+      const PhaseInfo q = make_phase(p, phase);
+      const uint32_t t = p.fd_gq.div(row), ww = row - t * p.gq;
+      const uint32_t nn = p.fd_gp.div(t), hh = t - nn * p.gp;
+      n = nn; hb = hh * p.gs + q.ph; wb = ww * p.gs + q.pw;
+    }
+  }
+
+  __device__ __forceinline__ void load8(const TIn* X, const TIn* aux, bool dy, long idx, Pend& g) const {
+    ld8(X + idx, g.v);
+    if (dy) ld8(aux + idx, g.y);
+    g.mx = 0xffu;
+  }
+
+  __device__ __forceinline__ void load(const GemmParams& p, const vae_xform& xf, const TIn* X, int phase, int k0,
+                                       int Kp, Pend& g) const {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, v[j], (k0 + j) % p.a_xf.channels, aux, base + j);
+    for (int j = 0; j < 8; ++j) g.v[j] = 0.f;
+    g.mx = 0u; g.keep = 0u; g.chb = 0;
+    if (!valid || k0 >= Kp) return;
+    const TIn* aux = static_cast<const TIn*>(xf.aux);
+    const bool dy = xf.kind == VAE_X_BN_DY;
+    if constexpr (MODE == A_DENSE || MODE == 100 + B_NK) {
+      const long idx = base + k0;
+      if constexpr (MODE == A_DENSE) g.chb = k0 % xf.channels;
+      if (vecok && k0 + 8 <= Kp) {
+        load8(X, aux, dy, idx, g);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (k0 + j < Kp) v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, ld_f(X + base + j), (k0 + j) % p.a_xf.channels, aux, base + j);
+          if (k0 + j < Kp) {
+            g.v[j] = ld_f(X + idx + j);
+            if (dy) g.y[j] = ld_f(aux + idx + j);
+            g.mx |= 1u << j;
+          }
       }
-    } else if constexpr (AM == A_CONV) {
-      // row -> (n, op, oq) of the output grid
-      const int oq = row % p.gq;
-      const int t = row / p.gq;
-      const int op = t % p.gp;
-      const int n = t / p.gp;
-      const int hb = op * p.gs - p.gpad, wb = oq * p.gs - p.gpad;
+    } else if constexpr (MODE == A_CONV) {
       const int C = p.gc;
       if (!p.g_nchw && (C & 7) == 0) {
-        const int tap = k0 / C, c = k0 - tap * C;
-        const int r = tap / p.gr, s = tap - r * p.gr;
+        const uint32_t tap = p.fd_gc.div(k0);
+        const int c = k0 - tap * C;
+        const uint32_t r = p.fd_gr.div(tap);
+        const int s = tap - r * p.gr;
         const int hi = hb + r, wi = wb + s;
+        g.chb = c;
         if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) return;
-        const long base = (((long)n * p.gh + hi) * p.gw + wi) * C + c;
-        ld8(X + base, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, v[j], c + j, aux, base + j);
+        load8(X, aux, dy, (((long)n * p.gh + hi) * p.gw + wi) * C + c, g);
       } else {
+        g.chb = k0 - p.fd_gc.div(k0) * C;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = k0 + j;
-          const int tap = k / C, c = k - tap * C;
-          const int r = tap / p.gr, s = tap - r * p.gr;
+          const uint32_t tap = p.fd_gc.div(k);
+          const int c = k - tap * C;
+          const uint32_t r = p.fd_gr.div(tap);
+          const int s = tap - r * p.gr;
           const int hi = hb + r, wi = wb + s;
           if (k >= Kp || hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) continue;
           const long idx = p.g_nchw ? (((long)n * C + c) * p.gh + hi) * p.gw + wi
                                     : (((long)n * p.gh + hi) * p.gw + wi) * C + c;
-          v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, ld_f(X + idx), c, aux, idx);
+          g.v[j] = ld_f(X + idx);
+          if (dy) g.y[j] = ld_f(aux + idx);
+          g.mx |= 1u << j;
         }
       }
-    } else if constexpr (AM == A_CONVT) {
-      const int ph = phase / p.gs, pw = phase - (phase / p.gs) * p.gs;
-      const int ww = row % p.gq;
-      const int t = row / p.gq;
-      const int hh = t % p.gp;
-      const int n = t / p.gp;
-      const int ho = hh * p.gs + ph, wo = ww * p.gs + pw;
+    } else if constexpr (MODE == A_CONVT) {
+      const PhaseInfo q = make_phase(p, phase);
       const int C = p.gc;
-      const int ntw = p.ntap_w[pw];
+      const int ntw = q.ntw;
       if ((C & 7) == 0) {
-        const int c = k0 % C, tt = k0 / C;
-        const int tw = tt % ntw, th = tt / ntw;
-        const int r = p.tap_h[ph][th], s = p.tap_w[pw][tw];
-        const int hi = (ho + p.gpad - r) / p.gs, wi = (wo + p.gpad - s) / p.gs;
+        const uint32_t tt = p.fd_gc.div(k0);
+        const int c = k0 - tt * C;
+        const uint32_t th = q.fdw.div(tt);
+        const int tw = tt - th * ntw;
+        const int r = q.t0h + p.gs * (int)th, s = q.t0w + p.gs * (int)tw;
+        const int hi = (hb + p.gpad - r) / p.gs, wi = (wb + p.gpad - s) / p.gs;
+        g.chb = c;
         if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) return;
-        const long base = (((long)n * p.gh + hi) * p.gw + wi) * C + c;
-        ld8(X + base, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, v[j], c + j, aux, base + j);
+        load8(X, aux, dy, (((long)n * p.gh + hi) * p.gw + wi) * C + c, g);
       } else {
+        g.chb = k0 - p.fd_gc.div(k0) * C;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int k = k0 + j;
           if (k >= Kp) continue;
-          const int c = k % C, tt = k / C;
-          const int tw = tt % ntw, th = tt / ntw;
-          const int r = p.tap_h[ph][th], s = p.tap_w[pw][tw];
-          const int hi = (ho + p.gpad - r) / p.gs, wi = (wo + p.gpad - s) / p.gs;
+          const uint32_t tt = p.fd_gc.div(k);
+          const int c = k - tt * C;
+          const uint32_t th = q.fdw.div(tt);
+          const int tw = tt - th * ntw;
+          const int r = q.t0h + p.gs * (int)th, s = q.t0w + p.gs * (int)tw;
+          const int hi = (hb + p.gpad - r) / p.gs, wi = (wb + p.gpad - s) / p.gs;
           if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) continue;
           const long idx = (((long)n * p.gh + hi) * p.gw + wi) * C + c;
-          v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, ld_f(X + idx), c, aux, idx);
+          g.v[j] = ld_f(X + idx);
+          if (dy) g.y[j] = ld_f(aux + idx);
+          g.mx |= 1u << j;
         }
-      }
-    }
-  }
-  // V_M: rows row0..row0+3 at k (A_KM: element (m,k) at k*lda + m)
-  __device__ __forceinline__ static void load_vm(const GemmParams& p, const XfTable<MAXCT, false>& xt, int row0, int k, float (&v)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = 0.f;
-    if constexpr (AM == A_KM) {
-      if (k >= p.K || row0 >= p.M) return;
-      const TIn* X = static_cast<const TIn*>(p.a_ptr);
-      const TIn* aux = static_cast<const TIn*>(p.a_xf.aux);
-      const long base = (long)k * p.a_ld + row0;
-      if (row0 + 4 <= p.M && (p.a_ld & 3) == 0) {
-        ld4(X + base, v);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, v[j], (row0 + j) % p.a_xf.channels, aux, base + j);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (row0 + j < p.M) v[j] = xf_apply<TIn, MAXCT>(p.a_xf, xt, ld_f(X + base + j), (row0 + j) % p.a_xf.channels, aux, base + j);
       }
     }
   }
 };
 
-template <class T, class TIn, int BMD, int MAXCT>
-struct BOperand {
-  __device__ __forceinline__ static void load_vk(const GemmParams& p, int phase, int row, int k0, int Kp, float (&v)[8]) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.f;
-    if constexpr (BMD == B_NK) {
-      if (row >= p.N || k0 >= Kp) return;
-      const TIn* W = static_cast<const TIn*>(p.b_ptr);
-      const long base = (long)row * p.b_ld + k0;
-      if (k0 + 8 <= Kp && (p.b_ld & 7) == 0) {
-        ld8(W + base, v);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (k0 + j < Kp) v[j] = ld_f(W + base + j);
-      }
+// ------------------------------------------------------------------ V_M operand (4 rows x 2 k)
+// element e of the group = row (e >> 1), k (e & 1)
+template <class TIn, int MODE>
+struct ColOperand {
+  int r0;          // first of the 4 rows (m for A_KM, n for B_KN/B_GATHER)
+  int nvalid;      // rows in range (0..4)
+  int vec;         // the 4 rows can be read as one vector
+  int r, s, c;     // B_GATHER: tap and channel of row r0
+  int ch0;         // transform channel of r0
+
+  __device__ __forceinline__ void init(const GemmParams& p, int row0, int rows, int ld, const vae_xform& xf) {
+    r0 = row0;
+    nvalid = rows - row0 < 0 ? 0 : (rows - row0 > 4 ? 4 : rows - row0);
+    vec = nvalid == 4 && (ld & 3) == 0;
+    if constexpr (MODE >= 100) vec = vec && (p.ones_col < 0 || row0 + 4 <= p.ones_col);
+    ch0 = row0 % xf.channels;
+    if constexpr (MODE == 100 + B_GATHER) {
+      const uint32_t tap = p.fd_gc.div(row0);
+      c = row0 - tap * p.gc;
+      const uint32_t rr = p.fd_gr.div(tap);
+      r = rr; s = tap - rr * p.gr;
+      vec = vec && !p.g_nchw && (p.gc & 3) == 0;
+      ch0 = c;
     }
   }
-  // V_M: 4 consecutive n at one k
-  __device__ __forceinline__ static void load_vm(const GemmParams& p, const XfTable<MAXCT, false>& xt, int phase, int n0, int k,
-                                 int Kp, float (&v)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = 0.f;
-    if (k >= Kp || n0 >= p.N) return;
-    if constexpr (BMD == B_KN) {
-      // row of the [K'][N] matrix: dense (nphase==0 tables unused) or via phase taps
-      long kr;
-      if (p.b_taps) {
-        const int ph = phase / p.gs, pw = phase - (phase / p.gs) * p.gs;
-        const int C = p.gc, ntw = p.ntap_w[pw];
-        const int c = k % C, tt = k / C;
-        const int tw = tt % ntw, th = tt / ntw;
-        const int r = p.tap_h[ph][th], s = p.tap_w[pw][tw];
-        kr = ((long)c * p.gr + r) * p.gr + s;
-      } else {
-        kr = k;
-      }
-      const TIn* W = static_cast<const TIn*>(p.b_ptr);
-      const TIn* aux = static_cast<const TIn*>(p.b_xf.aux);
-      const long base = kr * p.b_ld + n0;
-      if (n0 + 4 <= p.N && (p.b_ld & 3) == 0 && (p.ones_col < 0 || n0 + 4 <= p.ones_col)) {
-        ld4(W + base, v);
-        if (p.b_xf.kind != VAE_X_NONE) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = xf_apply<TIn, MAXCT>(p.b_xf, xt, v[j], (n0 + j) % p.b_xf.channels, aux, base + j);
+
+  // one k (t = 0 or 1 selects the element slots)
+  __device__ __forceinline__ void load1(const GemmParams& p, const vae_xform& xf, const TIn* X, int phase, int k,
+                                        int Kp, int t, Pend& g) const {
+    if (k >= Kp || nvalid == 0) return;
+    const TIn* aux = static_cast<const TIn*>(xf.aux);
+    const bool dy = xf.kind == VAE_X_BN_DY;
+    float v4[4], y4[4];
+    if constexpr (MODE == A_KM || MODE == 100 + B_KN) {
+      long kr = k;
+      if constexpr (MODE == 100 + B_KN) {
+        if (p.b_taps) {
+          const PhaseInfo q = make_phase(p, phase);
+          const uint32_t tt = p.fd_gc.div(k);
+          const int cc = k - tt * p.gc;
+          const uint32_t th = q.fdw.div(tt);
+          const int tw = tt - th * q.ntw;
+          kr = ((long)cc * p.gr + (q.t0h + p.gs * (int)th)) * p.gr + (q.t0w + p.gs * (int)tw);
         }
+      }
+      const int ld = (MODE == A_KM) ? p.a_ld : p.b_ld;
+      const long idx = kr * ld + r0;
+      if (vec) {
+        ld4(X + idx, v4);
+        if (dy) ld4(aux + idx, y4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { g.v[2 * j + t] = v4[j]; if (dy) g.y[2 * j + t] = y4[j]; }
+        g.mx |= 0x55u << t;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int n = n0 + j;
-          if (n >= p.N) continue;
-          if (n == p.ones_col) { v[j] = 1.f; continue; }
-          v[j] = xf_apply<TIn, MAXCT>(p.b_xf, xt, ld_f(W + base + j), n % p.b_xf.channels, aux, base + j);
+          if (j >= nvalid) continue;
+          if constexpr (MODE >= 100) {
+            if (r0 + j == p.ones_col) { g.v[2 * j + t] = 1.f; g.keep |= 1u << (2 * j + t); continue; }
+          }
+          g.v[2 * j + t] = ld_f(X + idx + j);
+          if (dy) g.y[2 * j + t] = ld_f(aux + idx + j);
+          g.mx |= 1u << (2 * j + t);
         }
       }
-    } else if constexpr (BMD == B_GATHER) {
-      // k = pixel (n_img, op, oq) of the gp x gq grid; n = (r, s, c) of the gathered tensor
-      const int oq = k % p.gq;
-      const int t = k / p.gq;
-      const int op = t % p.gp;
-      const int nimg = t / p.gp;
-      const TIn* X = static_cast<const TIn*>(p.b_ptr);
-      const TIn* aux = static_cast<const TIn*>(p.b_xf.aux);
-      const int C = p.gc;
-      if (!p.g_nchw && (C & 3) == 0 && (p.ones_col < 0 || n0 + 4 <= p.ones_col) && n0 + 4 <= p.N) {
-        const int tap = n0 / C, c = n0 - tap * C;
-        const int r = tap / p.gr, s = tap - r * p.gr;
+    } else if constexpr (MODE == 100 + B_GATHER) {
+      // k = pixel (n_img, op, oq) of the gp x gq grid
+      const uint32_t tq = p.fd_gq.div(k), oq = k - tq * p.gq;
+      const uint32_t nimg = p.fd_gp.div(tq), op = tq - nimg * p.gp;
+      if (vec) {
         const int hi = op * p.gs - p.gpad + r, wi = oq * p.gs - p.gpad + s;
         if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) return;
-        const long base = (((long)nimg * p.gh + hi) * p.gw + wi) * C + c;
-        ld4(X + base, v);
+        const long idx = (((long)nimg * p.gh + hi) * p.gw + wi) * p.gc + c;
+        ld4(X + idx, v4);
+        if (dy) ld4(aux + idx, y4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = xf_apply<TIn, MAXCT>(p.b_xf, xt, v[j], c + j, aux, base + j);
+        for (int j = 0; j < 4; ++j) { g.v[2 * j + t] = v4[j]; if (dy) g.y[2 * j + t] = y4[j]; }
+        g.mx |= 0x55u << t;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int n = n0 + j;
-          if (n >= p.N) continue;
-          if (n == p.ones_col) { v[j] = 1.f; continue; }
-          const int tap = n / C, c = n - tap * C;
-          const int r = tap / p.gr, s = tap - r * p.gr;
-          const int hi = op * p.gs - p.gpad + r, wi = oq * p.gs - p.gpad + s;
+          const int nn = r0 + j;
+          if (j >= nvalid) continue;
+          if (nn == p.ones_col) { g.v[2 * j + t] = 1.f; g.keep |= 1u << (2 * j + t); continue; }
+          const uint32_t tap = p.fd_gc.div(nn);
+          const int cc = nn - tap * p.gc;
+          const uint32_t rr = p.fd_gr.div(tap);
+          const int ss = tap - rr * p.gr;
+          const int hi = op * p.gs - p.gpad + rr, wi = oq * p.gs - p.gpad + ss;
           if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) continue;
-          // B_GATHER's tensor may be the fp32 NCHW image (first-layer weight gradient)
-          const long idx = p.g_nchw ? (((long)nimg * C + c) * p.gh + hi) * p.gw + wi
-                                    : (((long)nimg * p.gh + hi) * p.gw + wi) * C + c;
-          v[j] = xf_apply<TIn, MAXCT>(p.b_xf, xt, ld_f(X + idx), c, aux, idx);
+          const long idx = p.g_nchw ? (((long)nimg * p.gc + cc) * p.gh + hi) * p.gw + wi
+                                    : (((long)nimg * p.gh + hi) * p.gw + wi) * p.gc + cc;
+          g.v[2 * j + t] = ld_f(X + idx);
+          if (dy) g.y[2 * j + t] = ld_f(aux + idx);
+          g.mx |= 1u << (2 * j + t);
         }
       }
     }
   }
+
+  __device__ __forceinline__ void load(const GemmParams& p, const vae_xform& xf, const TIn* X, int phase, int k,
+                                       int Kp, Pend& g) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g.v[j] = 0.f;
+    g.mx = 0u; g.keep = 0u; g.chb = ch0;
+    load1(p, xf, X, phase, k, Kp, 0, g);
+    load1(p, xf, X, phase, k + 1, Kp, 1, g);
+  }
 };
+
+// ------------------------------------------------------------------ epilogue helpers
+__device__ __forceinline__ long out_index(const GemmParams& p, int phase, int row, int col) {
+  if (p.out_phase) {
+    const int ph = phase >= p.gs ? 1 : 0, pw = phase - ph * p.gs;
+    const uint32_t t = p.fd_gq.div(row), ww = row - t * p.gq;
+    const uint32_t n = p.fd_gp.div(t), hh = t - n * p.gp;
+    const int ho = hh * p.gs + ph, wo = ww * p.gs + pw;
+    return (((long)n * p.gho + ho) * p.gwo + wo) * p.out_ld + col;
+  }
+  return (long)row * p.out_ld + col;
+}
+
+// One output element of a non-accumulating epilogue.  s1/s2 collect the per-column sums.
+template <class T, int EM>
+__device__ __forceinline__ void epi_elem(const GemmParams& p, const Tab& xe, int phase, int row,
+                                         int col, float v, float& s1, float& s2) {
+  if constexpr (EM == E_REPARAM) {
+    const int b = row / p.samples;
+    const float mu = p.mulv[(long)b * 2 * p.latent + col];
+    const float lv = p.mulv[(long)b * 2 * p.latent + p.latent + col];
+    const float ep = p.eps[(long)row * p.latent + col];
+    const float c = p.kl_coef ? p.kl_coef[row] : 0.f;
+    const float sd = expf(0.5f * lv);
+    atomicAdd(p.dmulv + (long)b * 2 * p.latent + col, v + c * mu);
+    atomicAdd(p.dmulv + (long)b * 2 * p.latent + p.latent + col, v * ep * 0.5f * sd + c * 0.5f * (expf(lv) - 1.f));
+  } else {
+    const long idx = out_index(p, phase, row, col);
+    if constexpr (EM == E_STORE) {
+      float y = v + (p.bias ? p.bias[col] : 0.f);
+      if (p.residual) {
+        float rv = ld_f(static_cast<const T*>(p.residual) + idx);
+        if (p.res_xf.kind == VAE_X_ACT) rv = lrelu(rv, p.res_xf.slope);
+        y += rv;
+      }
+      if (p.out_f32) static_cast<float*>(p.out)[idx] = y;
+      else static_cast<T*>(p.out)[idx] = cvt<T>(y);
+      s1 += v;
+      s2 += v * v;
+    } else {  // E_BNBWD
+      float g = v;
+      if (p.epi_xf.kind == VAE_X_BN_ACT) {
+        const int ch = col % p.epi_xf.channels;
+        const float yv = ld_f(static_cast<const T*>(p.epi_xf.aux) + idx);
+        const float z = fmaf(yv, xe.a[ch], xe.b[ch]);
+        g = z > 0.f ? v : v * p.epi_xf.slope;
+        s1 += g;
+        s2 += g * fmaf(yv, xe.p[ch], xe.q[ch]);
+      } else if (p.epi_xf.kind == VAE_X_ACT) {
+        const float yv = ld_f(static_cast<const T*>(p.epi_xf.aux) + idx);
+        g = yv > 0.f ? v : v * p.epi_xf.slope;
+      }
+      static_cast<T*>(p.out)[idx] = cvt<T>(g);
+    }
+  }
+}
+
+template <int EM>
+__device__ __forceinline__ bool epi_wants_sums(const GemmParams& p) {
+  if constexpr (EM == E_STORE) return p.sum != nullptr;
+  if constexpr (EM == E_BNBWD) return p.epi_xf.kind == VAE_X_BN_ACT;
+  return false;
+}
+
+template <int EM>
+__device__ __forceinline__ void epi_flush_sums(const GemmParams& p, int col, float s1, float s2) {
+  float* g1 = (EM == E_STORE) ? p.sum : p.dbeta;
+  float* g2 = (EM == E_STORE) ? p.sumsq : p.dgamma;
+  const int ch = (EM == E_STORE) ? col : col % p.epi_xf.channels;
+  atomicAdd(g1 + ch, s1);
+  atomicAdd(g2 + ch, s2);
+}
+
+// Closed-form bias gradient of a conv followed by train-mode BatchNorm:
+//   db = Σ dy = A·Σg + B·Σy + C·M per channel (A,B,C the BN-backward coefficients)
+__device__ __forceinline__ void closed_form_db(const vae_xform& x, float* db) {
+  for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
+    float mean, invstd, var;
+    bn_moments(x, ch, mean, invstd, var);
+    const float inv_m = 1.0f / x.count;
+    const float A = x.gamma[ch] * invstd;
+    const float mgx = x.dgamma[ch] * inv_m;
+    const float mg = x.dbeta[ch] * inv_m;
+    const float B = -A * invstd * mgx;
+    const float C = -A * (mg - mean * invstd * mgx);
+    const float sum_y = x.sum[ch] + x.count * (x.shift ? x.shift[ch] : 0.f);
+    db[ch] += A * x.dbeta[ch] + B * sum_y + C * x.count;
+  }
+}
 
 template <int AM> constexpr bool a_is_vm() { return AM == A_KM; }
 template <int BMD> constexpr bool b_is_vm() { return BMD != B_NK; }
 
+// dynamic LDS: per-channel tables of the A, B and epilogue transforms (floats)
+__host__ __device__ inline int table_floats(const GemmParams& p, bool epi_tbl) {
+  return tab_floats(p.a_xf, false) + tab_floats(p.b_xf, false) + (epi_tbl ? tab_floats(p.epi_xf, true) : 0);
+}
+
 // ------------------------------------------------------------------------------ kernel
-// T: LDS/MFMA type; TA: storage type of the A tensor (fp32 for the NCHW image);
+// T: LDS/MFMA type; TA: storage type of the A tensor (fp32 for the NCHW image / d[mu|logvar]);
 // TB: storage type of B (the gathered activation for B_GATHER, weights otherwise).
 template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM>
 __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
+  constexpr int BK = bk_of<T>();
   constexpr int LDK = BK + (sizeof(T) == 4 ? 4 : 8);        // padded LDS row (elements)
   constexpr int WTM = BM / 2, WTN = BN / 2;                 // 2x2 waves
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr bool A_VM = a_is_vm<AM>();
   constexpr bool B_VM = b_is_vm<BMD>();
+  constexpr int KO = BK / 8;                                // V_K octets per row
   constexpr int A_OCT = BM * BK / 8, B_OCT = BN * BK / 8;   // octets per tile
   constexpr int A_PER = (A_OCT + NTHREADS - 1) / NTHREADS, B_PER = (B_OCT + NTHREADS - 1) / NTHREADS;
-  constexpr bool B_XF = (BMD != B_NK);
   constexpr bool EPI_TBL = (EM == E_BNBWD);
+  constexpr int A_MODE = AM;
+  constexpr int B_MODE = 100 + BMD;
 
-  __shared__ __attribute__((aligned(16))) T As[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LDK];
-  __shared__ XfTable<MAXC, false> xa;
-  __shared__ XfTable<B_XF ? MAXC : 1, false> xb;
-  __shared__ XfTable<EPI_TBL ? MAXC : 1, true> xe;
+  __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
   __shared__ float red1[BN], red2[BN];
+  extern __shared__ float tabs[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -308,22 +542,48 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   const int ks = blockIdx.z - phase * p.ksplit;
   const bool first_block = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
 
-  // per-phase K
   int Kp = p.K;
   if constexpr (AM == A_CONVT) {
-    const int ph = phase / p.gs, pw = phase - ph * p.gs;
-    Kp = p.ntap_h[ph] * p.ntap_w[pw] * p.gc;
+    const PhaseInfo q = make_phase(p, phase);
+    Kp = q.nth * q.ntw * p.gc;
   }
   const int ktiles = (Kp + BK - 1) / BK;
   const int kper = (ktiles + p.ksplit - 1) / p.ksplit;
   const int kt0 = ks * kper;
   const int kt1 = min(ktiles, kt0 + kper);
 
-  // per-channel tables (BN coefficients) and the reduction scratch
-  xa.fill(p.a_xf, first_block);
-  if constexpr (B_XF) xb.fill(p.b_xf, false);
-  if constexpr (EPI_TBL) xe.fill(p.epi_xf, false);
-  for (int i = tid; i < BN; i += NTHREADS) { red1[i] = 0.f; red2[i] = 0.f; }
+  // table views (carved in the order A, B, epilogue)
+  Tab ta, tb, te;
+  {
+    float* q = tabs;
+    const int ca = p.a_xf.channels, cb = p.b_xf.channels, ce = p.epi_xf.channels;
+    const bool ha = tab_floats(p.a_xf, false) > 0, hb = tab_floats(p.b_xf, false) > 0;
+    ta = Tab{q, q + ca, q + 2 * ca, nullptr, nullptr};
+    if (ha) q += 3 * ca;
+    tb = Tab{q, q + cb, q + 2 * cb, nullptr, nullptr};
+    if (hb) q += 3 * cb;
+    te = Tab{q, q + ce, nullptr, q + 2 * ce, q + 3 * ce};
+  }
+
+  // ---- per-thread operand row state (computed once)
+  const TA* Ap = static_cast<const TA*>(p.a_ptr);
+  const TB* Bp = static_cast<const TB*>(p.b_ptr);
+  RowOperand<TA, A_MODE> ars[A_VM ? 1 : A_PER];
+  ColOperand<TA, A_MODE> acs[A_VM ? A_PER : 1];
+  RowOperand<TB, B_MODE> brs[B_VM ? 1 : B_PER];
+  ColOperand<TB, B_MODE> bcs[B_VM ? B_PER : 1];
+#pragma unroll
+  for (int i = 0; i < A_PER; ++i) {
+    const int o = tid + i * NTHREADS;
+    if constexpr (!A_VM) ars[i].init(p, m0 + o / KO, p.M, phase, p.a_ld);
+    else acs[i].init(p, m0 + (o % (BM / 4)) * 4, p.M, p.a_ld, p.a_xf);
+  }
+#pragma unroll
+  for (int i = 0; i < B_PER; ++i) {
+    const int o = tid + i * NTHREADS;
+    if constexpr (!B_VM) brs[i].init(p, n0 + o / KO, p.N, phase, p.b_ld);
+    else bcs[i].init(p, n0 + (o % (BN / 4)) * 4, p.N, p.b_ld, p.b_xf);
+  }
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -331,7 +591,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float ra[A_PER][8], rb[B_PER][8];
+  Pend pa[A_PER], pb[B_PER];
 
   auto load_tiles = [&](int kt) {
     const int kb = kt * BK;
@@ -339,48 +599,31 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (o < A_OCT) {
-        if constexpr (!A_VM) {
-          AOperand<T, TA, AM, MAXC>::load_vk(p, xa, phase, m0 + o / (BK / 8), kb + (o % (BK / 8)) * 8, Kp, ra[i]);
-        } else {
-          const int rq = o % (BM / 4), kp = o / (BM / 4);
-          float v0[4], v1[4];
-          AOperand<T, TA, AM, MAXC>::load_vm(p, xa, m0 + rq * 4, kb + 2 * kp, v0);
-          AOperand<T, TA, AM, MAXC>::load_vm(p, xa, m0 + rq * 4, kb + 2 * kp + 1, v1);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { ra[i][2 * j] = v0[j]; ra[i][2 * j + 1] = v1[j]; }
-        }
+        if constexpr (!A_VM) ars[i].load(p, p.a_xf, Ap, phase, kb + (o % KO) * 8, Kp, pa[i]);
+        else acs[i].load(p, p.a_xf, Ap, phase, kb + 2 * (o / (BM / 4)), Kp, pa[i]);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (o < B_OCT) {
-        if constexpr (!B_VM) {
-          BOperand<T, TB, BMD, MAXC>::load_vk(p, phase, n0 + o / (BK / 8), kb + (o % (BK / 8)) * 8, Kp, rb[i]);
-        } else {
-          const int rq = o % (BN / 4), kp = o / (BN / 4);
-          float v0[4], v1[4];
-          BOperand<T, TB, BMD, (B_XF ? MAXC : 1)>::load_vm(p, xb, phase, n0 + rq * 4, kb + 2 * kp, Kp, v0);
-          BOperand<T, TB, BMD, (B_XF ? MAXC : 1)>::load_vm(p, xb, phase, n0 + rq * 4, kb + 2 * kp + 1, Kp, v1);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { rb[i][2 * j] = v0[j]; rb[i][2 * j + 1] = v1[j]; }
-        }
+        if constexpr (!B_VM) brs[i].load(p, p.b_xf, Bp, phase, kb + (o % KO) * 8, Kp, pb[i]);
+        else bcs[i].load(p, p.b_xf, Bp, phase, kb + 2 * (o / (BN / 4)), Kp, pb[i]);
       }
     }
   };
-  auto store_tiles = [&]() {
+  auto store_tiles = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (o < A_OCT) {
+        finish<A_VM>(p.a_xf, ta, pa[i]);
         if constexpr (!A_VM) {
-          st8(As + (o / (BK / 8)) * LDK + (o % (BK / 8)) * 8, ra[i]);
+          st8(As[buf] + (o / KO) * LDK + (o % KO) * 8, pa[i].v);
         } else {
           const int rq = o % (BM / 4), kp = o / (BM / 4);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            st2(As + (rq * 4 + j) * LDK + 2 * kp, ra[i][2 * j], ra[i][2 * j + 1]);
-          }
+          for (int j = 0; j < 4; ++j) st2(As[buf] + (rq * 4 + j) * LDK + 2 * kp, pa[i].v[2 * j], pa[i].v[2 * j + 1]);
         }
       }
     }
@@ -388,39 +631,31 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     for (int i = 0; i < B_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (o < B_OCT) {
+        finish<B_VM>(p.b_xf, tb, pb[i]);
         if constexpr (!B_VM) {
-          st8(Bs + (o / (BK / 8)) * LDK + (o % (BK / 8)) * 8, rb[i]);
+          st8(Bs[buf] + (o / KO) * LDK + (o % KO) * 8, pb[i].v);
         } else {
           const int rq = o % (BN / 4), kp = o / (BN / 4);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            st2(Bs + (rq * 4 + j) * LDK + 2 * kp, rb[i][2 * j], rb[i][2 * j + 1]);
-          }
+          for (int j = 0; j < 4; ++j) st2(Bs[buf] + (rq * 4 + j) * LDK + 2 * kp, pb[i].v[2 * j], pb[i].v[2 * j + 1]);
         }
       }
     }
   };
-
-  __syncthreads();   // tables ready
-  if (kt0 < kt1) load_tiles(kt0);
-  for (int kt = kt0; kt < kt1; ++kt) {
-    __syncthreads();
-    store_tiles();
-    __syncthreads();
-    if (kt + 1 < kt1) load_tiles(kt + 1);
+  auto compute = [&](int buf) {
     const int koff = 8 * (lane >> 4);
     if constexpr (sizeof(T) == 4) {
       float af[TM][8], bfr[TN][8];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const float* src = reinterpret_cast<const float*>(As) + (wm * WTM + i * 16 + (lane & 15)) * LDK + koff;
+        const float* src = reinterpret_cast<const float*>(As[buf]) + (wm * WTM + i * 16 + (lane & 15)) * LDK + koff;
         f32x4 x0 = *reinterpret_cast<const f32x4*>(src), x1 = *reinterpret_cast<const f32x4*>(src + 4);
         af[i][0] = x0[0]; af[i][1] = x0[1]; af[i][2] = x0[2]; af[i][3] = x0[3];
         af[i][4] = x1[0]; af[i][5] = x1[1]; af[i][6] = x1[2]; af[i][7] = x1[3];
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const float* src = reinterpret_cast<const float*>(Bs) + (wn * WTN + j * 16 + (lane & 15)) * LDK + koff;
+        const float* src = reinterpret_cast<const float*>(Bs[buf]) + (wn * WTN + j * 16 + (lane & 15)) * LDK + koff;
         f32x4 x0 = *reinterpret_cast<const f32x4*>(src), x1 = *reinterpret_cast<const f32x4*>(src + 4);
         bfr[j][0] = x0[0]; bfr[j][1] = x0[1]; bfr[j][2] = x0[2]; bfr[j][3] = x0[3];
         bfr[j][4] = x1[0]; bfr[j][5] = x1[1]; bfr[j][6] = x1[2]; bfr[j][7] = x1[3];
@@ -433,36 +668,50 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[j][s], acc[i][j], 0, 0, 0);
     } else {
-      bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (wm * WTM + i * 16 + (lane & 15)) * LDK + koff);
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + (lane & 15)) * LDK + koff);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(As[buf] + (wm * WTM + i * 16 + (lane & 15)) * LDK + koff + 32 * kk);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs[buf] + (wn * WTN + j * 16 + (lane & 15)) * LDK + koff + 32 * kk);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // prologue: first tile's global loads go out before the table fill (they overlap it)
+  if (kt0 < kt1) load_tiles(kt0);
+  tab_fill(p.a_xf, ta, false, first_block);
+  tab_fill(p.b_xf, tb, false, false);
+  if constexpr (EPI_TBL) tab_fill(p.epi_xf, te, true, false);
+  for (int i = tid; i < BN; i += NTHREADS) { red1[i] = 0.f; red2[i] = 0.f; }
+  if constexpr (EM == E_ACC) {
+    if (first_block && p.dbc) closed_form_db(p.dbc_from_b ? p.b_xf : p.a_xf, p.dbc);
+  }
+  __syncthreads();   // tables ready
+  if (kt0 < kt1) {
+    store_tiles(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) load_tiles(kt + 1);       // raw loads in flight during the MFMAs below
+      compute(buf);
+      if (more) store_tiles(buf ^ 1);     // transform + LDS write; other buffer, read 1 iter ago
+      __syncthreads();
+      buf ^= 1;
     }
   }
 
   // ------------------------------------------------------------------------ epilogue
   // lane holds rows 4*(lane>>4)+e, column lane&15 of each 16x16 tile
-  const int ph = phase / (p.gs > 0 ? p.gs : 1), pw = phase - ph * (p.gs > 0 ? p.gs : 1);
-  auto out_index = [&](int row, int col) -> long {
-    if (p.out_phase) {
-      const int ww = row % p.gq;
-      const int t = row / p.gq;
-      const int hh = t % p.gp;
-      const int n = t / p.gp;
-      const int ho = hh * p.gs + ph, wo = ww * p.gs + pw;
-      return (((long)n * p.gho + ho) * p.gwo + wo) * p.out_ld + col;
-    }
-    return (long)row * p.out_ld + col;
-  };
-
   if constexpr (EM == E_ACC) {
     float* out = static_cast<float*>(p.out);
 #pragma unroll
@@ -482,31 +731,24 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
         }
       }
     return;
-  } else if constexpr (EM == E_REPARAM) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int d = n0 + wn * WTN + j * 16 + (lane & 15);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
-          if (row >= p.M || d >= p.N) continue;
-          const int b = row / p.samples;
-          const float mu = p.mulv[(long)b * 2 * p.latent + d];
-          const float lv = p.mulv[(long)b * 2 * p.latent + p.latent + d];
-          const float ep = p.eps[(long)row * p.latent + d];
-          const float c = p.kl_coef ? p.kl_coef[row] : 0.f;
-          const float dz = acc[i][j][e];
-          const float sd = expf(0.5f * lv);
-          atomicAdd(p.dmulv + (long)b * 2 * p.latent + d, dz + c * mu);
-          atomicAdd(p.dmulv + (long)b * 2 * p.latent + p.latent + d, dz * ep * 0.5f * sd + c * 0.5f * (expf(lv) - 1.f));
-        }
-      }
-    return;
   } else {
-    T* out = static_cast<T*>(p.out);
-    const bool want_sums = (EM == E_STORE) ? (p.sum != nullptr) : (p.epi_xf.kind == VAE_X_BN_ACT);
+    if (p.slab) {
+      // split-K: raw partial sums to this slice's slab; igemm_finalize runs the epilogue
+      float* sl = p.slab + ((long)(phase * p.ksplit + ks) * p.M) * p.N;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WTN + j * 16 + (lane & 15);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
+            if (row < p.M && col < p.N) sl[(long)row * p.N + col] = acc[i][j][e];
+          }
+        }
+      return;
+    }
+    const bool want_sums = epi_wants_sums<EM>(p);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = n0 + wn * WTN + j * 16 + (lane & 15);
@@ -518,36 +760,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
         for (int e = 0; e < 4; ++e) {
           const int row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
           if (row >= p.M || !col_ok) continue;
-          const float v = acc[i][j][e];
-          const long idx = out_index(row, col);
-          if constexpr (EM == E_STORE) {
-            float y = v + (p.bias ? p.bias[col] : 0.f);
-            if (p.residual) {
-              const T* res = static_cast<const T*>(p.residual);
-              float rv = ld_f(res + idx);
-              if (p.res_xf.kind == VAE_X_ACT) rv = lrelu(rv, p.res_xf.slope);
-              y += rv;
-            }
-            if (p.out_f32) static_cast<float*>(p.out)[idx] = y;
-            else out[idx] = cvt<T>(y);
-            s1 += v;
-            s2 += v * v;
-          } else {  // E_BNBWD
-            float g = v;
-            if (p.epi_xf.kind == VAE_X_BN_ACT) {
-              const int ch = col % p.epi_xf.channels;
-              const float yv = ld_f(static_cast<const T*>(p.epi_xf.aux) + idx);
-              const float z = fmaf(yv, xe.a[ch], xe.b[ch]);
-              g = z > 0.f ? v : v * p.epi_xf.slope;
-              const float xh = fmaf(yv, xe.p[ch], xe.q[ch]);
-              s1 += g;
-              s2 += g * xh;
-            } else if (p.epi_xf.kind == VAE_X_ACT) {
-              const float yv = ld_f(static_cast<const T*>(p.epi_xf.aux) + idx);
-              g = yv > 0.f ? v : v * p.epi_xf.slope;
-            }
-            out[idx] = cvt<T>(g);
-          }
+          epi_elem<T, EM>(p, te, phase, row, col, acc[i][j][e], s1, s2);
         }
       if (want_sums) {
         s1 += __shfl_xor(s1, 16);
@@ -562,15 +775,46 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     }
     if (want_sums) {
       __syncthreads();
-      float* g1 = (EM == E_STORE) ? p.sum : p.dbeta;
-      float* g2 = (EM == E_STORE) ? p.sumsq : p.dgamma;
-      const int nch = (EM == E_STORE) ? p.N : p.epi_xf.channels;
       for (int c = tid; c < BN; c += NTHREADS)
-        if (n0 + c < p.N) {
-          atomicAdd(g1 + (n0 + c) % nch, red1[c]);
-          atomicAdd(g2 + (n0 + c) % nch, red2[c]);
-        }
+        if (n0 + c < p.N) epi_flush_sums<EM>(p, n0 + c, red1[c], red2[c]);
     }
+  }
+}
+
+// Split-K finalize: sums the K-slices' slabs in slice order and runs the epilogue.
+// grid: (ceil(M*nphase / 64), ceil(N / 64)); block 256 = 4 row groups x 64 columns.
+template <class T, int EM>
+__global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
+  constexpr bool EPI_TBL = (EM == E_BNBWD);
+  __shared__ float r1[4][64], r2[4][64];
+  extern __shared__ float tabs[];
+  const int ce = p.epi_xf.channels;
+  const Tab te{tabs, tabs + ce, nullptr, tabs + 2 * ce, tabs + 3 * ce};
+  if constexpr (EPI_TBL) tab_fill(p.epi_xf, te, true, false);
+  __syncthreads();
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.y * 64 + cl;
+  const long rows_total = (long)p.M * p.nphase;
+  float s1 = 0.f, s2 = 0.f;
+  if (col < p.N) {
+    for (int rr = rg; rr < 64; rr += 4) {
+      const long grow = (long)blockIdx.x * 64 + rr;
+      if (grow >= rows_total) break;
+      const int phase = (int)(grow / p.M);
+      const int row = (int)(grow - (long)phase * p.M);
+      const float* sl = p.slab + ((long)phase * p.ksplit * p.M + row) * p.N + col;
+      float v = 0.f;
+      for (int s = 0; s < p.ksplit; ++s) v += sl[(long)s * p.M * p.N];
+      epi_elem<T, EM>(p, te, phase, row, col, v, s1, s2);
+    }
+  }
+  if (epi_wants_sums<EM>(p)) {
+    r1[rg][cl] = s1;
+    r2[rg][cl] = s2;
+    __syncthreads();
+    if (rg == 0 && col < p.N)
+      epi_flush_sums<EM>(p, col, r1[0][cl] + r1[1][cl] + r1[2][cl] + r1[3][cl],
+                         r2[0][cl] + r2[1][cl] + r2[2][cl] + r2[3][cl]);
   }
 }
 

@@ -1,0 +1,202 @@
+// Host-side planning and launching of the implicit-GEMM kernels: tile shape, split-K, FastDiv
+// setup, slab workspace and the finalize pass.  Included by the entry-point translation units.
+#pragma once
+#include "vae_igemm.hpp"
+
+namespace vae {
+namespace {
+
+constexpr int kCUs = 256;
+constexpr int kTargetBlocks = 512;   // 2 resident workgroups per CU
+
+inline vae_xform sanitize(vae_xform x) {
+  if (x.channels <= 0) x.channels = 1;
+  return x;
+}
+
+inline bool xf_ok(const vae_xform& x, const char* what) {
+  if (x.kind < VAE_X_NONE || x.kind > VAE_X_BN_DY) { fail(VAE_E_BADARG, "%s: bad xform kind %d", what, x.kind); return false; }
+  if (x.kind == VAE_X_BN_ACT || x.kind == VAE_X_BN_DY) {
+    if (x.channels > MAXC) { fail(VAE_E_UNSUPPORTED, "%s: %d channels > %d", what, x.channels, MAXC); return false; }
+    if (!x.sum || !x.sumsq || !x.gamma || !x.beta || x.count <= 0.f) {
+      fail(VAE_E_BADARG, "%s: BatchNorm transform needs sum/sumsq/gamma/beta/count", what); return false;
+    }
+    if (x.kind == VAE_X_BN_DY && (!x.dgamma || !x.dbeta || !x.aux)) {
+      fail(VAE_E_BADARG, "%s: BN_DY transform needs dgamma/dbeta/aux", what); return false;
+    }
+  }
+  if (x.kind == VAE_X_ACT && !(x.slope >= 0.f)) { fail(VAE_E_BADARG, "%s: bad slope", what); return false; }
+  return true;
+}
+
+// A backward epilogue that differentiates an activation must be given the stored
+// pre-activation tensor (aux); a NULL there would be a device fault, so reject it here.
+inline bool epi_ok(const vae_xform& x, const char* what) {
+  if (!xf_ok(x, what)) return false;
+  if ((x.kind == VAE_X_BN_ACT || x.kind == VAE_X_ACT) && !x.aux) {
+    fail(VAE_E_BADARG, "%s: activation-backward epilogue needs aux (the stored pre-activation)", what);
+    return false;
+  }
+  if (x.kind == VAE_X_BN_DY) { fail(VAE_E_BADARG, "%s: BN_DY is not an epilogue transform", what); return false; }
+  return true;
+}
+
+// Phase tap tables of a transposed conv (or conv dgrad) with stride S, kernel R, padding P:
+// output coordinate o of phase ph = o % S receives taps r with (ph + P - r) % S == 0.
+inline bool make_taps(GemmParams& p, int S, int R, int P) {
+  if (S < 1 || S > 2) return false;
+  for (int ph = 0; ph < S; ++ph) {
+    const int first = ((ph + P) % S + S) % S;       // smallest r with (ph + P - r) % S == 0
+    const int n = first < R ? (R - 1 - first) / S + 1 : 0;
+    if (n < 1 || n > 4) return false;
+    p.tap0[ph] = first;
+    p.ntap_h[ph] = n; p.ntap_w[ph] = n;
+  }
+  return true;
+}
+
+inline GemmParams base_params() {
+  GemmParams p;
+  memset(&p, 0, sizeof(p));
+  p.ksplit = 1; p.nphase = 1; p.ones_col = -1; p.gs = 1; p.samples = 1; p.gr = 1;
+  p.a_xf.channels = 1; p.b_xf.channels = 1; p.epi_xf.channels = 1; p.res_xf.channels = 1;
+  p.ntap_h[0] = p.ntap_h[1] = p.ntap_w[0] = p.ntap_w[1] = 1;
+  return p;
+}
+
+inline void finish_divs(GemmParams& p) {
+  p.fd_gq = make_fastdiv(p.gq > 0 ? p.gq : 1);
+  p.fd_gp = make_fastdiv(p.gp > 0 ? p.gp : 1);
+  p.fd_gc = make_fastdiv(p.gc > 0 ? p.gc : 1);
+  p.fd_gr = make_fastdiv(p.gr > 0 ? p.gr : 1);
+  p.fd_ntw[0] = make_fastdiv(p.ntap_w[0] > 0 ? p.ntap_w[0] : 1);
+  p.fd_ntw[1] = make_fastdiv(p.ntap_w[1] > 0 ? p.ntap_w[1] : 1);
+}
+
+struct Tile { int bm, bn; };
+
+// Largest tile that still fills the CUs; thin N prefers the 128x32 tile.
+inline Tile pick_tile(long M, long N, int nphase) {
+  const Tile cands_thin[] = {{128, 32}, {64, 64}, {32, 64}, {32, 32}};
+  const Tile cands[] = {{64, 64}, {32, 64}, {32, 32}};
+  const Tile* c = N <= 32 ? cands_thin : cands;
+  const int nc = N <= 32 ? 4 : 3;
+  for (int i = 0; i < nc; ++i) {
+    const long blocks = ((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn) * nphase;
+    if (blocks >= kCUs) return c[i];
+  }
+  return {32, 32};
+}
+
+// K-slices: enough blocks to cover the CUs twice, >= 4 K-tiles per slice, and (for slab
+// epilogues) the partial slabs must fit the caller's workspace.
+inline int pick_split(long blocks, int ktiles, bool slab, long slab_elems_per_split, long ws_bytes) {
+  if (blocks >= kTargetBlocks || ktiles < 8) return 1;
+  int s = (int)((kTargetBlocks + blocks - 1) / blocks);
+  const int maxs = ktiles / 4;
+  if (s > maxs) s = maxs;
+  if (slab) {
+    const long fit = slab_elems_per_split > 0 ? ws_bytes / (slab_elems_per_split * 4) : 0;
+    if (s > fit) s = (int)fit;
+  }
+  return s < 2 ? 1 : s;
+}
+
+template <class T, int EM>
+inline int launch_finalize(const GemmParams& p, hipStream_t st) {
+  const long rows = (long)p.M * p.nphase;
+  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((p.N + 63) / 64));
+  const size_t lds = EM == E_BNBWD ? (size_t)tab_floats(p.epi_xf, true) * 4 : 0;
+  hipLaunchKernelGGL((igemm_finalize<T, EM>), grid, dim3(NTHREADS), lds, st, p);
+  return check_launch("igemm_finalize");
+}
+
+template <class T, class TA, class TB, int AM, int BMD, int EM>
+inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
+  const dim3 block(NTHREADS);
+  const dim3 grid((p.M + t.bm - 1) / t.bm, (p.N + t.bn - 1) / t.bn, p.nphase * p.ksplit);
+  const size_t lds = (size_t)table_floats(p, EM == E_BNBWD) * 4;
+  if (t.bm == 64 && t.bn == 64)
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 64, 64, AM, BMD, EM>), grid, block, lds, st, p);
+  else if (t.bm == 128 && t.bn == 32)
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 128, 32, AM, BMD, EM>), grid, block, lds, st, p);
+  else if (t.bm == 32 && t.bn == 64)
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 64, AM, BMD, EM>), grid, block, lds, st, p);
+  else
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 32, AM, BMD, EM>), grid, block, lds, st, p);
+  int rc = check_launch("igemm");
+  if (rc) return rc;
+  if (EM != E_ACC && p.slab) return launch_finalize<T, EM>(p, st);
+  return VAE_OK;
+}
+
+// Plan tile + split-K, then launch.  A_F32 / B_F32: instantiate the bf16 variant whose A / B
+// tensor is fp32 (the NCHW image, d[mu|logvar]).
+template <int AM, int BMD, int EM, bool A_F32 = false, bool B_F32 = false>
+inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req, void* ws, long ws_bytes,
+                  hipStream_t st) {
+  if (p.M <= 0 || p.N <= 0) return VAE_OK;
+  finish_divs(p);
+  const Tile t = pick_tile(p.M, p.N, p.nphase);
+  const int bk = dtype == VAE_F32 ? 32 : 64;
+  int kmax = p.K;
+  if (AM == A_CONVT) {
+    kmax = 0;
+    for (int ph = 0; ph < p.nphase; ++ph) {
+      const int k = p.ntap_h[ph / p.gs] * p.ntap_w[ph % p.gs] * p.gc;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  const int ktiles = (kmax + bk - 1) / bk;
+  const long blocks = (long)((p.M + t.bm - 1) / t.bm) * ((p.N + t.bn - 1) / t.bn) * p.nphase;
+  const bool slab = EM != E_ACC;
+  int split = split_req > 0 ? split_req : pick_split(blocks, ktiles, slab, (long)p.M * p.N * p.nphase, ws ? ws_bytes : 0);
+  if (slab && split > 1) {
+    if (!ws || (long)split * p.M * p.N * p.nphase * 4 > ws_bytes) split = 1;
+    else p.slab = static_cast<float*>(ws);
+  }
+  p.ksplit = split < 1 ? 1 : split;
+  if (dtype == VAE_F32) return launch_tiled<float, float, float, AM, BMD, EM>(p, t, st);
+  if (dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "dtype %d", dtype);
+  if constexpr (A_F32) {
+    if (a_f32) return launch_tiled<__bf16, float, __bf16, AM, BMD, EM>(p, t, st);
+  }
+  if constexpr (B_F32) {
+    if (b_f32) return launch_tiled<__bf16, __bf16, float, AM, BMD, EM>(p, t, st);
+  }
+  if (a_f32 || b_f32) return fail(VAE_E_UNSUPPORTED, "fp32 operand not instantiated for this op");
+  return launch_tiled<__bf16, __bf16, __bf16, AM, BMD, EM>(p, t, st);
+}
+
+// Column sums of a plain [rows][C] tensor (bias gradient of a layer whose dy is stored as is)
+template <class T>
+__global__ void column_sum(const T* x, long rows, int C, float* out) {
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  if (c >= C) return;
+  float s = 0.f;
+  for (long r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (long)gridDim.x * 4) s += ld_f(x + r * C + c);
+  atomicAdd(out + c, s);
+}
+
+inline int column_sum_launch(int dtype, const void* dy, long rows, int C, float* db, hipStream_t st) {
+  const dim3 grid(64, (C + 63) / 64);
+  if (dtype == VAE_F32) hipLaunchKernelGGL(column_sum<float>, grid, dim3(256), 0, st, (const float*)dy, rows, C, db);
+  else hipLaunchKernelGGL(column_sum<__bf16>, grid, dim3(256), 0, st, (const __bf16*)dy, rows, C, db);
+  return check_launch("column_sum");
+}
+
+}  // namespace
+}  // namespace vae
+
+namespace vae {
+namespace {
+inline bool geom_ok(const vae_conv_args* a, const char* what) {
+  if (!a) { fail(VAE_E_BADARG, "%s: null args", what); return false; }
+  if (a->n <= 0 || a->h <= 0 || a->w <= 0 || a->c <= 0 || a->k <= 0 || a->p <= 0 || a->q <= 0 || a->r <= 0 ||
+      a->stride <= 0 || a->pad < 0) {
+    fail(VAE_E_BADSHAPE, "%s: bad geometry", what); return false;
+  }
+  return true;
+}
+}  // namespace
+}  // namespace vae

@@ -1,0 +1,54 @@
+// C-ABI entry points of the Linear layers: fc_mu|fc_var fused as one N=2D layer
+// (models/vanilla_vae.py:36-37, :89-90) and decoder_input (:43, :101).
+#include "vae_launch.hpp"
+
+using namespace vae;
+
+extern "C" int vae_linear_fwd(const vae_linear_args* a, void* stream) {
+  if (!a || !a->x || !a->wt || !a->y || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_fwd: args");
+  if (!xf_ok(a->x_xf, "linear_fwd.x")) return VAE_E_BADARG;
+  GemmParams p = base_params();
+  p.M = a->m; p.N = a->n; p.K = a->k;
+  p.a_ptr = a->x; p.a_ld = a->k; p.a_xf = sanitize(a->x_xf);
+  p.b_ptr = a->wt; p.b_ld = a->k;
+  p.out = a->y; p.out_ld = a->n; p.bias = a->bias; p.out_f32 = a->y_f32;
+  return launch<A_DENSE, B_NK, E_STORE>(a->dtype, false, false, p, 0, a->workspace, a->workspace_bytes,
+                                        (hipStream_t)stream);
+}
+
+// dx[m][k] = Σ_n dy[m][n] · W[n][k];  epilogue: activation backward (dx_epi) or, when
+// mulv is set, the reparameterization + KL backward into dmulv
+extern "C" int vae_linear_bwd_data(const vae_linear_args* a, void* stream) {
+  if (!a || !a->dy || !a->wt || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_bwd_data: args");
+  if (!a->mulv && !epi_ok(a->dx_epi, "linear_bwd_data.epi")) return VAE_E_BADARG;
+  GemmParams p = base_params();
+  p.M = a->m; p.N = a->k; p.K = a->n;
+  p.a_ptr = a->dy; p.a_ld = a->n;
+  p.b_ptr = a->wt; p.b_ld = a->k;
+  p.out = a->dx; p.out_ld = a->k;
+  if (a->mulv) {
+    if (!a->eps || !a->dmulv || a->samples <= 0) return fail(VAE_E_BADARG, "linear_bwd_data: reparam args");
+    p.mulv = a->mulv; p.eps = a->eps; p.kl_coef = a->kl_coef; p.dmulv = a->dmulv;
+    p.samples = a->samples; p.latent = a->k;
+    return launch<A_DENSE, B_KN, E_REPARAM, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace,
+                                                  a->workspace_bytes, (hipStream_t)stream);
+  }
+  if (!a->dx) return fail(VAE_E_BADARG, "linear_bwd_data: dx");
+  p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+  if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "linear_bwd_data: dgamma/dbeta");
+  return launch<A_DENSE, B_KN, E_BNBWD, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace, a->workspace_bytes,
+                                              (hipStream_t)stream);
+}
+
+// dW[n][k] += Σ_m dy[m][n] · xf(x)[m][k];  db[n] += Σ_m dy[m][n]  (ones column)
+extern "C" int vae_linear_bwd_filter(const vae_linear_args* a, void* stream) {
+  if (!a || !a->dy || !a->x || !a->dw || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_bwd_filter: args");
+  if (!xf_ok(a->x_xf, "linear_bwd_filter.x")) return VAE_E_BADARG;
+  GemmParams p = base_params();
+  p.M = a->n; p.N = a->k + (a->db ? 1 : 0); p.K = a->m;
+  p.ones_col = a->db ? a->k : -1; p.bias_grad = a->db;
+  p.a_ptr = a->dy; p.a_ld = a->n;
+  p.b_ptr = a->x; p.b_ld = a->k; p.b_xf = sanitize(a->x_xf);
+  p.out = a->dw; p.out_ld = a->k;
+  return launch<A_KM, B_KN, E_ACC, true>(a->dtype, a->dy_f32 != 0, false, p, 0, nullptr, 0, (hipStream_t)stream);
+}

@@ -42,7 +42,7 @@ class ConvArgs(ctypes.Structure):
                 ("y_sum", c_void_p), ("y_sumsq", c_void_p), ("residual", c_void_p), ("residual_xf", Xform),
                 ("dy", c_void_p), ("dy_xf", Xform), ("dx", c_void_p), ("dx_epi", Xform),
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
-                ("split_k", c_int32)]
+                ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -52,7 +52,7 @@ class LinearArgs(ctypes.Structure):
                 ("dx_dgamma", c_void_p),
                 ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
                 ("mulv", c_void_p), ("eps", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p),
-                ("samples", c_int32)]
+                ("samples", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
 
 
 class HeadArgs(ctypes.Structure):

@@ -26,6 +26,7 @@ from .layout import Layout, default_init, reference_key_order, vanilla_layout
 SLOPE = 0.01         # nn.LeakyReLU default
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+WORKSPACE_BYTES = 32 << 20
 
 
 class VAENet:
@@ -164,6 +165,8 @@ class StepPlan:
         self.sse = self.zero[o:o + BS]; o += _pad4(BS)
         self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        # split-K partial slabs (fp32), reused by every launch of the step on the stream
+        self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
         self._build()
@@ -197,6 +200,9 @@ class StepPlan:
         return xf
 
     def _add(self, lst, fn, arg):
+        if isinstance(arg, (L.ConvArgs, L.LinearArgs)):
+            arg.workspace = self.workspace.data_ptr()
+            arg.workspace_bytes = self.workspace.numel() * 4
         self._keep.append(arg)
         lst.append((fn, ctypes.byref(arg)))
 

@@ -25,9 +25,10 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+@pytest.mark.parametrize("split", [0, 3])
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("cin,cout,hw", [(32, 64, 16), (64, 32, 8), (16, 48, 12)])
-def test_conv2d_fwd_bnact_and_stats(dtype, cin, cout, hw):
+def test_conv2d_fwd_bnact_and_stats(dtype, cin, cout, hw, split):
     L = _L()
     torch.manual_seed(0)
     N = 4
@@ -43,6 +44,8 @@ def test_conv2d_fwd_bnact_and_stats(dtype, cin, cout, hw):
     a = L.ConvArgs(dtype=L.dtype_code(dtype), n=N, h=hw, w=hw, c=cin, k=cout, p=hw // 2, q=hw // 2, r=3, stride=2, pad=1)
     a.x = bn.y_dev.data_ptr(); a.x_xf = bn.xf(); a.wt = wd.data_ptr(); a.bias = bd.data_ptr(); a.y = out.data_ptr()
     a.y_sum = s.data_ptr(); a.y_sumsq = s.data_ptr() + 4 * cout
+    ws = torch.empty(1 << 20, device="cuda")
+    a.split_k = split; a.workspace = ws.data_ptr(); a.workspace_bytes = ws.numel() * 4
     L.call("vae_conv2d_fwd", ctypes.byref(a), _stream())
     torch.cuda.synchronize()
     assert rel(to_nchw(out), ref) < tol(dtype)
@@ -130,8 +133,9 @@ def test_conv_backward_plain(dtype, transposed):
     assert rel(db.cpu(), b.grad) < tol(dtype)
 
 
+@pytest.mark.parametrize("split", [0, 2])
 @pytest.mark.parametrize("dtype", DTYPES)
-def test_conv2d_backward_bn(dtype):
+def test_conv2d_backward_bn(dtype, split):
     """dy through BN_DY (BN-backward on load) and dx through the BN_ACT epilogue, vs autograd
     of conv(lrelu(bn(y_prev))) -> bn -> (upstream grad)."""
     L = _L()
@@ -173,6 +177,8 @@ def test_conv2d_backward_bn(dtype):
     a.dx_dgamma = dgp.data_ptr(); a.dx_dbeta = dbp.data_ptr()
     a.x = bnp.y_dev.data_ptr(); a.x_xf = bnp.xf(L.X_BN_ACT)
     a.dw = dw.data_ptr(); a.db = db.data_ptr()
+    ws = torch.empty(1 << 20, device="cuda")
+    a.split_k = split; a.workspace = ws.data_ptr(); a.workspace_bytes = ws.numel() * 4
     L.call("vae_conv2d_bwd_data", ctypes.byref(a), _stream())
     L.call("vae_conv2d_bwd_filter", ctypes.byref(a), _stream())
     torch.cuda.synchronize()
