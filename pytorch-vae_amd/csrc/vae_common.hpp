@@ -65,7 +65,8 @@ __device__ __forceinline__ void st2(__bf16* d, float a, float b) {
   *reinterpret_cast<bf16x2*>(d) = o;
 }
 
-__device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.f ? v : v * slope; }
+// LeakyReLU for 0 <= slope <= 1 (checked on the host): max(v, slope*v) — two VALU ops, no compare
+__device__ __forceinline__ float lrelu(float v, float slope) { return fmaxf(v, v * slope); }
 
 // ---------------------------------------------------------------- BN statistics
 // mean/invstd/var of channel c from the producer's Σ(y-shift), Σ(y-shift)^2.

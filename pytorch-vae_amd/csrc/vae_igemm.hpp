@@ -85,7 +85,31 @@ struct GemmParams {
   float* dbc; int dbc_from_b;  // closed-form BN-followed bias gradient (wgrad, first block)
   const float* mulv; const float* eps; const float* kl_coef; float* dmulv; int samples, latent;
   float* slab;               // split-K partials [nphase][ksplit][M][N] (non-ACC epilogues)
+  // ---- operand access (host-derived, see vae_launch.hpp)
+  uint32_t a_bytes, b_bytes; // buffer-resource extents of the A / B tensors (and their aux)
+  FastDiv fd_ach, fd_bch;    // transform channel counts of A / B
+  unsigned long long* probe; // VAE_PROBE builds: per-block phase timestamps (diagnostics only)
 };
+
+// Phase timestamps of one block (VAE_PROBE builds): record = {block id, wall0, wall3, clk0..clk3,
+// hw id}; probe[0] is the record counter, probe[1] the capacity.
+#ifdef VAE_PROBE
+#define PROBE_MARK(i) do { if (threadIdx.x == 0) clk[i] = __builtin_readcyclecounter(); } while (0)
+__device__ __forceinline__ void probe_write(unsigned long long* pr, const unsigned long long* clk,
+                                           unsigned long long w0) {
+  if (!pr || threadIdx.x != 0) return;
+  const unsigned long long slot = atomicAdd(pr, 1ull);
+  if (slot >= pr[1]) return;                 // pr[1]: capacity in records
+  unsigned long long* r = pr + 8 + slot * 8;
+  r[0] = blockIdx.x | ((unsigned long long)blockIdx.y << 21) | ((unsigned long long)blockIdx.z << 42);
+  r[1] = w0;
+  r[2] = wall_clock64();
+  r[3] = clk[0]; r[4] = clk[1]; r[5] = clk[2]; r[6] = clk[3];
+  r[7] = __builtin_amdgcn_s_getreg((23 << 0) | (0 << 6) | (31 << 11));   // HW_ID
+}
+#else
+#define PROBE_MARK(i) do { } while (0)
+#endif
 
 // Phase-specific constants of a transposed-conv problem, resolved once per block with selects
 // (runtime indexing of kernarg arrays makes the compiler copy the whole struct to scratch).
@@ -107,14 +131,25 @@ __device__ __forceinline__ PhaseInfo make_phase(const GemmParams& p, int phase) 
 }
 
 // ------------------------------------------------------------------ per-channel tables
-// Views into dynamic LDS, sized by the real channel count of each transform:
+// Views into dynamic LDS, sized by the real channel count of each transform (rounded up to 4
+// so vector reads of 4 consecutive channels stay 16-byte aligned):
 //   BN_ACT: v = lrelu(t*a + b)   BN_DY: v = a*t + b*aux + c   epilogue BN_ACT: x̂ = y*p + q
 struct Tab {
   float *a, *b, *c, *p, *q;
 };
 
+__host__ __device__ inline int tab_pad(int c) { return (c + 3) & ~3; }
+// Each table row is followed by 8 zero entries (the "zero slot" at index tab_pad(C)): a packed
+// group that is out of range points its channel there, so any transform maps it to exactly 0.
+__host__ __device__ inline int tab_stride(int c) { return tab_pad(c) + 8; }
+
 __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bool update_running) {
   if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return;
+  if (threadIdx.x < 8) {
+    const int z = tab_pad(x.channels) + threadIdx.x;
+    t.a[z] = 0.f; t.b[z] = 0.f;
+    if (x.kind == VAE_X_BN_DY) t.c[z] = 0.f;
+  }
   for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
     float mean, invstd, var;
     bn_moments(x, ch, mean, invstd, var);
@@ -144,60 +179,101 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
 
 __host__ __device__ inline int tab_floats(const vae_xform& x, bool epi) {
   if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return 0;
-  return (epi ? 4 : 3) * x.channels;
+  return (epi ? 4 : 3) * tab_stride(x.channels);
 }
 
-// ------------------------------------------------------------------ pending loads
-// A staged group of 8 elements: raw values, the BN-backward aux values, and masks.  The
-// transform is applied by finish() when the group is written to LDS, so nothing consumes a
-// global load before the MFMAs of the previous K-tile have been issued.
-struct Pend {
-  float v[8];
-  float y[8];
-  uint32_t mx;     // bit e: element e was loaded -> apply the transform
-  uint32_t keep;   // bit e: keep v[e] as is (the bias-gradient ones column)
-  int chb;         // transform channel of the group's first row / k
+// ------------------------------------------------------------------ buffer loads
+// Operands are read through buffer resources: an offset at or past the resource size returns 0
+// without touching memory.  Every load of a K-tile is therefore issued unconditionally (no
+// branch, so no wait next to it); out-of-range elements are dropped by a validity mask when
+// the tile is written to LDS.  Offsets are 32-bit bytes (host checks tensors < 2 GiB).
+constexpr uint32_t kOOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* ptr, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int NB>
+__device__ __forceinline__ void bload(rsrc_t r, uint32_t off, uint32_t* d) {
+  if constexpr (NB == 16) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+  } else if constexpr (NB == 8) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    d[0] = v[0]; d[1] = v[1];
+  } else if constexpr (NB == 4) {
+    d[0] = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  } else {
+    d[0] = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+  }
+}
+
+// One operand as the kernel sees it: tensor (+ BN_DY aux) resources and its transform.
+// The packed-vs-per-element layout is the kernel template parameter VEC (host-decided, see
+// operand_vec in vae_launch.hpp): a runtime choice would put a branch between a load and the
+// point its value is consumed.
+template <class TIn>
+struct Src {
+  rsrc_t x, y;
+  int kind, C;
+  int zs;          // zero-slot channel index (tab_pad(C))
+  float slope;
+  int dy;
 };
 
-// element e -> row/k offset within the group: V_K: e (8 k), V_M: e >> 1 (4 rows x 2 k)
-template <bool VM>
-__device__ __forceinline__ void finish(const vae_xform& x, const Tab& t, Pend& g) {
-  const int C = x.channels;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int off = VM ? (e >> 1) : e;
-    int ch = g.chb + off;
-    if (C >= 8) ch = ch >= C ? ch - C : ch;
-    else ch = ch % C;
-    float v = g.v[e];
-    if ((g.mx >> e) & 1u) {
-      switch (x.kind) {
-        case VAE_X_ACT: v = lrelu(v, x.slope); break;
-        case VAE_X_BN_ACT: v = lrelu(fmaf(v, t.a[ch], t.b[ch]), x.slope); break;
-        case VAE_X_BN_DY: v = fmaf(t.a[ch], v, fmaf(t.b[ch], g.y[e], t.c[ch])); break;
-        default: break;
-      }
-    } else if (!((g.keep >> e) & 1u)) {
-      v = 0.f;
-    }
-    g.v[e] = v;
-  }
+template <class TIn>
+__device__ __forceinline__ Src<TIn> make_src(const void* ptr, uint32_t bytes, const vae_xform& xf) {
+  Src<TIn> s;
+  s.dy = xf.kind == VAE_X_BN_DY;
+  s.x = make_rsrc(ptr, bytes);
+  s.y = make_rsrc(s.dy ? xf.aux : ptr, bytes);
+  s.kind = xf.kind;
+  s.C = xf.channels;
+  s.zs = tab_pad(xf.channels);
+  s.slope = xf.slope;
+  return s;
+}
+
+// ------------------------------------------------------------------ raw staging
+// A group of 8 elements in flight between its global load and its LDS store.
+//   V_K (row x 8 k):    element e = k offset e
+//   V_M (4 rows x 2 k): element e = 4*t + j  (k offset t, row j)
+// Packed layout (vec): the raw vector(s) as loaded — bf16 pairs per dword, fp32 one per
+// dword.  Generic layout: element e in w[e] (bf16 in the low half).
+struct Pend {
+  uint32_t w[8], y[8];
+  uint32_t m;       // bit e: element e is in range (else it becomes 0)
+  uint32_t ones;    // bit e: element e is the bias-gradient ones column (becomes 1)
+  int chb;          // transform channel of element 0 (V_K) / row 0 (V_M); generic B_GATHER: row 0
+  int chb1;         // packed V_M: channel of row 0 for the second k (zero slot when out of range)
+};
+
+template <class TIn, bool VEC>
+__device__ __forceinline__ float raw_elem(const uint32_t* w, int e) {
+  if constexpr (sizeof(TIn) == 4) return __uint_as_float(w[e]);
+  else if constexpr (VEC) return __uint_as_float((e & 1) ? (w[e >> 1] & 0xffff0000u) : (w[e >> 1] << 16));
+  else return __uint_as_float(w[e] << 16);
+}
+
+template <class TIn, int NB>
+__device__ __forceinline__ void bload_pair(const Src<TIn>& s, uint32_t off, uint32_t* w, uint32_t* y) {
+  bload<NB>(s.x, off, w);
+  if (s.dy) bload<NB>(s.y, off, y);
 }
 
 // ------------------------------------------------------------------ V_K operand (row x 8 k)
 // Row state is computed once per thread slot; load() is called once per K-tile.
-template <class TIn, int MODE>
+template <class TIn, int MODE, bool VEC>
 struct RowOperand {
   int valid;       // row in range
-  int vecok;       // A_DENSE / B_NK: 8-element vector loads are aligned
   int n, hb, wb;   // A_CONV: image, top-left input coordinate; A_CONVT: image, ho, wo
-  long base;       // A_DENSE / B_NK: row offset
+  int base;        // A_DENSE / B_NK: row offset (elements)
 
   __device__ __forceinline__ void init(const GemmParams& p, int row, int rows, int phase, int ld) {
     valid = row < rows;
     if constexpr (MODE == A_DENSE || MODE == 100 + B_NK) {
-      base = (long)row * ld;
-      vecok = (ld & 7) == 0;
+      base = row * ld;
     } else if constexpr (MODE == A_CONV) {
       const uint32_t t = p.fd_gq.div(row), oq = row - t * p.gq;
       const uint32_t nn = p.fd_gp.div(t), op = t - nn * p.gp;
@@ -210,209 +286,305 @@ struct RowOperand {
     }
   }
 
-  __device__ __forceinline__ void load8(const TIn* X, const TIn* aux, bool dy, long idx, Pend& g) const {
-    ld8(X + idx, g.v);
-    if (dy) ld8(aux + idx, g.y);
-    g.mx = 0xffu;
-  }
-
-  __device__ __forceinline__ void load(const GemmParams& p, const vae_xform& xf, const TIn* X, int phase, int k0,
-                                       int Kp, Pend& g) const {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) g.v[j] = 0.f;
-    g.mx = 0u; g.keep = 0u; g.chb = 0;
-    if (!valid || k0 >= Kp) return;
-    const TIn* aux = static_cast<const TIn*>(xf.aux);
-    const bool dy = xf.kind == VAE_X_BN_DY;
+  // element offset + in-range flag of k (per-element path, and the group's k0 in the packed one)
+  __device__ __forceinline__ int offset(const GemmParams& p, const PhaseInfo& q, int k, bool& ok) const {
     if constexpr (MODE == A_DENSE || MODE == 100 + B_NK) {
-      const long idx = base + k0;
-      if constexpr (MODE == A_DENSE) g.chb = k0 % xf.channels;
-      if (vecok && k0 + 8 <= Kp) {
-        load8(X, aux, dy, idx, g);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (k0 + j < Kp) {
-            g.v[j] = ld_f(X + idx + j);
-            if (dy) g.y[j] = ld_f(aux + idx + j);
-            g.mx |= 1u << j;
-          }
-      }
+      ok = true;
+      return base + k;
     } else if constexpr (MODE == A_CONV) {
       const int C = p.gc;
-      if (!p.g_nchw && (C & 7) == 0) {
-        const uint32_t tap = p.fd_gc.div(k0);
-        const int c = k0 - tap * C;
-        const uint32_t r = p.fd_gr.div(tap);
-        const int s = tap - r * p.gr;
-        const int hi = hb + r, wi = wb + s;
-        g.chb = c;
-        if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) return;
-        load8(X, aux, dy, (((long)n * p.gh + hi) * p.gw + wi) * C + c, g);
-      } else {
-        g.chb = k0 - p.fd_gc.div(k0) * C;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = k0 + j;
-          const uint32_t tap = p.fd_gc.div(k);
-          const int c = k - tap * C;
-          const uint32_t r = p.fd_gr.div(tap);
-          const int s = tap - r * p.gr;
-          const int hi = hb + r, wi = wb + s;
-          if (k >= Kp || hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) continue;
-          const long idx = p.g_nchw ? (((long)n * C + c) * p.gh + hi) * p.gw + wi
-                                    : (((long)n * p.gh + hi) * p.gw + wi) * C + c;
-          g.v[j] = ld_f(X + idx);
-          if (dy) g.y[j] = ld_f(aux + idx);
-          g.mx |= 1u << j;
-        }
-      }
-    } else if constexpr (MODE == A_CONVT) {
-      const PhaseInfo q = make_phase(p, phase);
+      const uint32_t tap = p.fd_gc.div(k);
+      const int c = k - tap * C;
+      const uint32_t r = p.fd_gr.div(tap);
+      const int s = tap - r * p.gr;
+      const int hi = hb + r, wi = wb + s;
+      ok = hi >= 0 && hi < p.gh && wi >= 0 && wi < p.gw;
+      return p.g_nchw ? ((n * C + c) * p.gh + hi) * p.gw + wi : ((n * p.gh + hi) * p.gw + wi) * C + c;
+    } else {  // A_CONVT
       const int C = p.gc;
-      const int ntw = q.ntw;
-      if ((C & 7) == 0) {
-        const uint32_t tt = p.fd_gc.div(k0);
-        const int c = k0 - tt * C;
-        const uint32_t th = q.fdw.div(tt);
-        const int tw = tt - th * ntw;
-        const int r = q.t0h + p.gs * (int)th, s = q.t0w + p.gs * (int)tw;
-        const int hi = (hb + p.gpad - r) / p.gs, wi = (wb + p.gpad - s) / p.gs;
-        g.chb = c;
-        if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) return;
-        load8(X, aux, dy, (((long)n * p.gh + hi) * p.gw + wi) * C + c, g);
-      } else {
-        g.chb = k0 - p.fd_gc.div(k0) * C;
+      const uint32_t tt = p.fd_gc.div(k);
+      const int c = k - tt * C;
+      const uint32_t th = q.fdw.div(tt);
+      const int tw = tt - th * q.ntw;
+      const int r = q.t0h + p.gs * (int)th, s = q.t0w + p.gs * (int)tw;
+      const int hi = (hb + p.gpad - r) / p.gs, wi = (wb + p.gpad - s) / p.gs;
+      ok = hi >= 0 && hi < p.gh && wi >= 0 && wi < p.gw;
+      return ((n * p.gh + hi) * p.gw + wi) * C + c;
+    }
+  }
+
+  __device__ __forceinline__ void load(const GemmParams& p, const Src<TIn>& s, const PhaseInfo& q, const FastDiv& fdc,
+                                       int k0, int Kp, Pend& g) const {
+    constexpr int E = sizeof(TIn);
+    g.ones = 0u;
+    g.chb = s.kind >= VAE_X_BN_ACT ? (int)(k0 - fdc.div(k0) * s.C) : 0;
+    if constexpr (VEC) {
+      // whole group in or out (host: K % 8 == 0); out -> zeros and the zero-slot channel
+      bool ok;
+      const int idx = offset(p, q, k0, ok);
+      const bool gv = valid && ok && k0 < Kp;
+      g.chb = gv ? g.chb : s.zs;
+      const uint32_t off = gv ? (uint32_t)idx * E : kOOB;
+      bload_pair<TIn, 16>(s, off, g.w, g.y);
+      if constexpr (E == 4) bload_pair<TIn, 16>(s, off + 16, g.w + 4, g.y + 4);
+    } else {
+      uint32_t m = 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = k0 + j;
-          if (k >= Kp) continue;
-          const uint32_t tt = p.fd_gc.div(k);
-          const int c = k - tt * C;
-          const uint32_t th = q.fdw.div(tt);
-          const int tw = tt - th * ntw;
-          const int r = q.t0h + p.gs * (int)th, s = q.t0w + p.gs * (int)tw;
-          const int hi = (hb + p.gpad - r) / p.gs, wi = (wb + p.gpad - s) / p.gs;
-          if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) continue;
-          const long idx = (((long)n * p.gh + hi) * p.gw + wi) * C + c;
-          g.v[j] = ld_f(X + idx);
-          if (dy) g.y[j] = ld_f(aux + idx);
-          g.mx |= 1u << j;
-        }
+      for (int e = 0; e < 8; ++e) {
+        bool ok;
+        const int idx = offset(p, q, k0 + e, ok);
+        ok = ok && valid && k0 + e < Kp;
+        m |= (uint32_t)ok << e;
+        bload_pair<TIn, E>(s, ok ? (uint32_t)idx * E : kOOB, g.w + e, g.y + e);
       }
+      g.m = m;
     }
   }
 };
 
 // ------------------------------------------------------------------ V_M operand (4 rows x 2 k)
-// element e of the group = row (e >> 1), k (e & 1)
-template <class TIn, int MODE>
+template <class TIn, int MODE, bool VEC>
 struct ColOperand {
   int r0;          // first of the 4 rows (m for A_KM, n for B_KN/B_GATHER)
-  int nvalid;      // rows in range (0..4)
-  int vec;         // the 4 rows can be read as one vector
+  uint32_t rmask;  // rows in range, ones column excluded (4 bits)
+  uint32_t omask;  // the ones column (4 bits)
   int r, s, c;     // B_GATHER: tap and channel of row r0
-  int ch0;         // transform channel of r0
+  int ch0;         // transform channel of r0 (generic B_GATHER: r0 itself)
 
-  __device__ __forceinline__ void init(const GemmParams& p, int row0, int rows, int ld, const vae_xform& xf) {
+  __device__ __forceinline__ void init(const GemmParams& p, int row0, int rows, const vae_xform& xf) {
     r0 = row0;
-    nvalid = rows - row0 < 0 ? 0 : (rows - row0 > 4 ? 4 : rows - row0);
-    vec = nvalid == 4 && (ld & 3) == 0;
-    if constexpr (MODE >= 100) vec = vec && (p.ones_col < 0 || row0 + 4 <= p.ones_col);
-    ch0 = row0 % xf.channels;
+    rmask = 0u; omask = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool in = row0 + j < rows;
+      const bool one = MODE >= 100 && row0 + j == p.ones_col;
+      rmask |= (uint32_t)(in && !one) << j;
+      omask |= (uint32_t)(in && one) << j;
+    }
+    ch0 = xf.kind >= VAE_X_BN_ACT ? row0 % xf.channels : 0;
     if constexpr (MODE == 100 + B_GATHER) {
       const uint32_t tap = p.fd_gc.div(row0);
       c = row0 - tap * p.gc;
       const uint32_t rr = p.fd_gr.div(tap);
       r = rr; s = tap - rr * p.gr;
-      vec = vec && !p.g_nchw && (p.gc & 3) == 0;
-      ch0 = c;
+      ch0 = VEC ? c : row0;
     }
   }
 
-  // one k (t = 0 or 1 selects the element slots)
-  __device__ __forceinline__ void load1(const GemmParams& p, const vae_xform& xf, const TIn* X, int phase, int k,
-                                        int Kp, int t, Pend& g) const {
-    if (k >= Kp || nvalid == 0) return;
-    const TIn* aux = static_cast<const TIn*>(xf.aux);
-    const bool dy = xf.kind == VAE_X_BN_DY;
-    float v4[4], y4[4];
-    if constexpr (MODE == A_KM || MODE == 100 + B_KN) {
-      long kr = k;
-      if constexpr (MODE == 100 + B_KN) {
-        if (p.b_taps) {
-          const PhaseInfo q = make_phase(p, phase);
-          const uint32_t tt = p.fd_gc.div(k);
-          const int cc = k - tt * p.gc;
-          const uint32_t th = q.fdw.div(tt);
-          const int tw = tt - th * q.ntw;
-          kr = ((long)cc * p.gr + (q.t0h + p.gs * (int)th)) * p.gr + (q.t0w + p.gs * (int)tw);
-        }
+  // element offset of (row r0 + j, k) and whether the gathered position is in range
+  __device__ __forceinline__ int offset(const GemmParams& p, const PhaseInfo& q, int k, int j, bool& ok) const {
+    ok = true;
+    if constexpr (MODE == A_KM) {
+      return k * p.a_ld + r0 + j;
+    } else if constexpr (MODE == 100 + B_KN) {
+      int kr = k;
+      if (p.b_taps) {
+        const uint32_t tt = p.fd_gc.div(k);
+        const int cc = k - tt * p.gc;
+        const uint32_t th = q.fdw.div(tt);
+        const int tw = tt - th * q.ntw;
+        kr = (cc * p.gr + (q.t0h + p.gs * (int)th)) * p.gr + (q.t0w + p.gs * (int)tw);
       }
-      const int ld = (MODE == A_KM) ? p.a_ld : p.b_ld;
-      const long idx = kr * ld + r0;
-      if (vec) {
-        ld4(X + idx, v4);
-        if (dy) ld4(aux + idx, y4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { g.v[2 * j + t] = v4[j]; if (dy) g.y[2 * j + t] = y4[j]; }
-        g.mx |= 0x55u << t;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (j >= nvalid) continue;
-          if constexpr (MODE >= 100) {
-            if (r0 + j == p.ones_col) { g.v[2 * j + t] = 1.f; g.keep |= 1u << (2 * j + t); continue; }
-          }
-          g.v[2 * j + t] = ld_f(X + idx + j);
-          if (dy) g.y[2 * j + t] = ld_f(aux + idx + j);
-          g.mx |= 1u << (2 * j + t);
-        }
-      }
-    } else if constexpr (MODE == 100 + B_GATHER) {
-      // k = pixel (n_img, op, oq) of the gp x gq grid
+      return kr * p.b_ld + r0 + j;
+    } else {  // B_GATHER: k = pixel (n_img, op, oq) of the gp x gq grid, row = (r, s, c)
       const uint32_t tq = p.fd_gq.div(k), oq = k - tq * p.gq;
       const uint32_t nimg = p.fd_gp.div(tq), op = tq - nimg * p.gp;
-      if (vec) {
-        const int hi = op * p.gs - p.gpad + r, wi = oq * p.gs - p.gpad + s;
-        if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) return;
-        const long idx = (((long)nimg * p.gh + hi) * p.gw + wi) * p.gc + c;
-        ld4(X + idx, v4);
-        if (dy) ld4(aux + idx, y4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { g.v[2 * j + t] = v4[j]; if (dy) g.y[2 * j + t] = y4[j]; }
-        g.mx |= 0x55u << t;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int nn = r0 + j;
-          if (j >= nvalid) continue;
-          if (nn == p.ones_col) { g.v[2 * j + t] = 1.f; g.keep |= 1u << (2 * j + t); continue; }
-          const uint32_t tap = p.fd_gc.div(nn);
-          const int cc = nn - tap * p.gc;
-          const uint32_t rr = p.fd_gr.div(tap);
-          const int ss = tap - rr * p.gr;
-          const int hi = op * p.gs - p.gpad + rr, wi = oq * p.gs - p.gpad + ss;
-          if (hi < 0 || hi >= p.gh || wi < 0 || wi >= p.gw) continue;
-          const long idx = p.g_nchw ? (((long)nimg * p.gc + cc) * p.gh + hi) * p.gw + wi
-                                    : (((long)nimg * p.gh + hi) * p.gw + wi) * p.gc + cc;
-          g.v[2 * j + t] = ld_f(X + idx);
-          if (dy) g.y[2 * j + t] = ld_f(aux + idx);
-          g.mx |= 1u << (2 * j + t);
-        }
+      int rr = r, ss = s, cc = c;
+      if constexpr (!VEC) {
+        const int nn = r0 + j;
+        const uint32_t tap = p.fd_gc.div(nn);
+        cc = nn - tap * p.gc;
+        const uint32_t ru = p.fd_gr.div(tap);
+        rr = ru; ss = tap - ru * p.gr;
       }
+      const int hi = op * p.gs - p.gpad + rr, wi = oq * p.gs - p.gpad + ss;
+      ok = hi >= 0 && hi < p.gh && wi >= 0 && wi < p.gw;
+      return p.g_nchw ? ((nimg * p.gc + cc) * p.gh + hi) * p.gw + wi : ((nimg * p.gh + hi) * p.gw + wi) * p.gc + cc;
     }
   }
 
-  __device__ __forceinline__ void load(const GemmParams& p, const vae_xform& xf, const TIn* X, int phase, int k,
-                                       int Kp, Pend& g) const {
+  __device__ __forceinline__ void load(const GemmParams& p, const Src<TIn>& s, const PhaseInfo& q, int k, int Kp,
+                                       Pend& g) const {
+    constexpr int E = sizeof(TIn);
+    g.chb = ch0;
+    g.ones = omask | (omask << 4);
+    uint32_t m = 0u;
+    if constexpr (VEC) {
+      // rows beyond the operand feed output rows/columns that are never stored (host: row
+      // count % 4 == 0); a k out of range or a padding position reads zeros + zero slot
 #pragma unroll
-    for (int j = 0; j < 8; ++j) g.v[j] = 0.f;
-    g.mx = 0u; g.keep = 0u; g.chb = ch0;
-    load1(p, xf, X, phase, k, Kp, 0, g);
-    load1(p, xf, X, phase, k + 1, Kp, 1, g);
+      for (int t = 0; t < 2; ++t) {
+        bool ok;
+        const int idx = offset(p, q, k + t, 0, ok);
+        ok = ok && k + t < Kp;
+        if (t == 0) g.chb = ok ? ch0 : s.zs;
+        else g.chb1 = ok ? ch0 : s.zs;
+        const uint32_t off = ok ? (uint32_t)idx * E : kOOB;
+        if constexpr (E == 2) bload_pair<TIn, 8>(s, off, g.w + 2 * t, g.y + 2 * t);
+        else bload_pair<TIn, 16>(s, off, g.w + 4 * t, g.y + 4 * t);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bool ok;
+          const int idx = offset(p, q, k + t, j, ok);
+          ok = ok && k + t < Kp && ((rmask >> j) & 1u);
+          m |= (uint32_t)ok << (4 * t + j);
+          bload_pair<TIn, E>(s, ok ? (uint32_t)idx * E : kOOB, g.w + 4 * t + j, g.y + 4 * t + j);
+        }
+    }
+    g.m = m;
   }
 };
+
+// Transform of a staged group (after its loads have landed) -> 8 floats in element order.
+// Masked elements become 0 after the transform (the transform of a zero pad is not zero).
+template <class TIn, int MODE, bool VM, bool VEC>
+__device__ __forceinline__ void finish(const GemmParams& p, const Src<TIn>& s, const Tab& t, const Pend& g,
+                                       float (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = raw_elem<TIn, VEC>(g.w, e);
+  if (s.kind == VAE_X_BN_ACT || s.kind == VAE_X_BN_DY) {
+    const bool dy = s.kind == VAE_X_BN_DY;
+    float a[8], b[8], c[8];
+    if constexpr (VEC) {
+      // channels are consecutive: V_K chb..chb+7, V_M chb..chb+3 (16-byte aligned table reads)
+      if constexpr (VM) {
+        const f32x4 A = *reinterpret_cast<const f32x4*>(t.a + g.chb);
+        const f32x4 B = *reinterpret_cast<const f32x4*>(t.b + g.chb);
+        f32x4 Cc = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (dy) Cc = *reinterpret_cast<const f32x4*>(t.c + g.chb);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { a[e] = A[e & 3]; b[e] = B[e & 3]; c[e] = Cc[e & 3]; }
+      } else {
+        const f32x4 A0 = *reinterpret_cast<const f32x4*>(t.a + g.chb), A1 = *reinterpret_cast<const f32x4*>(t.a + g.chb + 4);
+        const f32x4 B0 = *reinterpret_cast<const f32x4*>(t.b + g.chb), B1 = *reinterpret_cast<const f32x4*>(t.b + g.chb + 4);
+        f32x4 C0 = f32x4{0.f, 0.f, 0.f, 0.f}, C1 = C0;
+        if (dy) { C0 = *reinterpret_cast<const f32x4*>(t.c + g.chb); C1 = *reinterpret_cast<const f32x4*>(t.c + g.chb + 4); }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = A0[e]; a[e + 4] = A1[e]; b[e] = B0[e]; b[e + 4] = B1[e]; c[e] = C0[e]; c[e + 4] = C1[e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        int ch;
+        if constexpr (VM && MODE == 100 + B_GATHER) {
+          const int nn = g.chb + (e & 3);
+          ch = nn - (int)p.fd_gc.div(nn) * p.gc;
+        } else {
+          ch = (g.chb + (VM ? (e & 3) : e)) % s.C;
+        }
+        a[e] = t.a[ch]; b[e] = t.b[ch]; c[e] = dy ? t.c[ch] : 0.f;
+      }
+    }
+    if (dy) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaf(a[e], v[e], fmaf(b[e], raw_elem<TIn, VEC>(g.y, e), c[e]));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = lrelu(fmaf(v[e], a[e], b[e]), s.slope);
+    }
+  } else if (s.kind == VAE_X_ACT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = lrelu(v[e], s.slope);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    v[e] = ((g.m >> e) & 1u) ? v[e] : 0.f;
+    if constexpr (VM && MODE >= 100) v[e] = ((g.ones >> e) & 1u) ? 1.f : v[e];
+  }
+}
+
+// ------------------------------------------------------------------ packed (VEC) groups -> LDS
+// No masks: out-of-range data is already 0 and its channel is the zero slot.  Untransformed
+// groups of the LDS type are copied as raw bits.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 tab4(const float* t, int ch) { return *reinterpret_cast<const f32x4*>(t + ch); }
+
+template <class T, class TIn>
+__device__ __forceinline__ void store_vk(const Src<TIn>& s, const Tab& t, const Pend& g, T* dst) {
+  if constexpr (sizeof(T) == sizeof(TIn)) {
+    if (s.kind == VAE_X_NONE) {
+      reinterpret_cast<u32x4*>(dst)[0] = u32x4{g.w[0], g.w[1], g.w[2], g.w[3]};
+      if constexpr (sizeof(T) == 4) reinterpret_cast<u32x4*>(dst)[1] = u32x4{g.w[4], g.w[5], g.w[6], g.w[7]};
+      return;
+    }
+  }
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = raw_elem<TIn, true>(g.w, e);
+  if (s.kind == VAE_X_ACT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = lrelu(v[e], s.slope);
+  } else if (s.kind == VAE_X_BN_ACT) {
+    const f32x4 a0 = tab4(t.a, g.chb), a1 = tab4(t.a, g.chb + 4), b0 = tab4(t.b, g.chb), b1 = tab4(t.b, g.chb + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = lrelu(fmaf(v[e], a0[e], b0[e]), s.slope);
+      v[e + 4] = lrelu(fmaf(v[e + 4], a1[e], b1[e]), s.slope);
+    }
+  } else if (s.kind == VAE_X_BN_DY) {
+    const f32x4 a0 = tab4(t.a, g.chb), a1 = tab4(t.a, g.chb + 4), b0 = tab4(t.b, g.chb), b1 = tab4(t.b, g.chb + 4);
+    const f32x4 c0 = tab4(t.c, g.chb), c1 = tab4(t.c, g.chb + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = fmaf(a0[e], v[e], fmaf(b0[e], raw_elem<TIn, true>(g.y, e), c0[e]));
+      v[e + 4] = fmaf(a1[e], v[e + 4], fmaf(b1[e], raw_elem<TIn, true>(g.y, e + 4), c1[e]));
+    }
+  }
+  st8(dst, v);
+}
+
+// rows j = 0..3 of the group go to dst + j*ldk as the pair (k, k+1)
+template <class T, class TIn, int MODE>
+__device__ __forceinline__ void store_vm(const Src<TIn>& s, const Tab& t, const Pend& g, T* dst, int ldk) {
+  if constexpr (sizeof(T) == 2 && sizeof(TIn) == 2) {
+    if (s.kind == VAE_X_NONE && (MODE < 100 || g.ones == 0u)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = g.w[j >> 1], hi = g.w[2 + (j >> 1)];
+        *reinterpret_cast<uint32_t*>(dst + j * ldk) =
+            (j & 1) ? ((lo >> 16) | (hi & 0xffff0000u)) : ((lo & 0xffffu) | (hi << 16));
+      }
+      return;
+    }
+  }
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = raw_elem<TIn, true>(g.w, e);
+  if (s.kind == VAE_X_ACT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = lrelu(v[e], s.slope);
+  } else if (s.kind == VAE_X_BN_ACT) {
+    const f32x4 a0 = tab4(t.a, g.chb), a1 = tab4(t.a, g.chb1), b0 = tab4(t.b, g.chb), b1 = tab4(t.b, g.chb1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = lrelu(fmaf(v[j], a0[j], b0[j]), s.slope);
+      v[4 + j] = lrelu(fmaf(v[4 + j], a1[j], b1[j]), s.slope);
+    }
+  } else if (s.kind == VAE_X_BN_DY) {
+    const f32x4 a0 = tab4(t.a, g.chb), a1 = tab4(t.a, g.chb1), b0 = tab4(t.b, g.chb), b1 = tab4(t.b, g.chb1);
+    const f32x4 c0 = tab4(t.c, g.chb), c1 = tab4(t.c, g.chb1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = fmaf(a0[j], v[j], fmaf(b0[j], raw_elem<TIn, true>(g.y, j), c0[j]));
+      v[4 + j] = fmaf(a1[j], v[4 + j], fmaf(b1[j], raw_elem<TIn, true>(g.y, 4 + j), c1[j]));
+    }
+  }
+  if constexpr (MODE >= 100) {
+    if (g.ones) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ((g.ones >> e) & 1u) ? 1.f : v[e];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) st2(dst + j * ldk, v[j], v[4 + j]);
+}
 
 // ------------------------------------------------------------------ epilogue helpers
 __device__ __forceinline__ long out_index(const GemmParams& p, int phase, int row, int col) {
@@ -514,7 +686,7 @@ __host__ __device__ inline int table_floats(const GemmParams& p, bool epi_tbl) {
 // ------------------------------------------------------------------------------ kernel
 // T: LDS/MFMA type; TA: storage type of the A tensor (fp32 for the NCHW image / d[mu|logvar]);
 // TB: storage type of B (the gathered activation for B_GATHER, weights otherwise).
-template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM>
+template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM, bool VEC>
 __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   constexpr int BK = bk_of<T>();
   constexpr int LDK = BK + (sizeof(T) == 4 ? 4 : 8);        // padded LDS row (elements)
@@ -534,6 +706,11 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   __shared__ float red1[BN], red2[BN];
   extern __shared__ float tabs[];
 
+#ifdef VAE_PROBE
+  unsigned long long clk[4] = {0, 0, 0, 0};
+  const unsigned long long wall0 = threadIdx.x == 0 ? wall_clock64() : 0;
+#endif
+  PROBE_MARK(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -556,7 +733,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   Tab ta, tb, te;
   {
     float* q = tabs;
-    const int ca = p.a_xf.channels, cb = p.b_xf.channels, ce = p.epi_xf.channels;
+    const int ca = tab_stride(p.a_xf.channels), cb = tab_stride(p.b_xf.channels), ce = tab_stride(p.epi_xf.channels);
     const bool ha = tab_floats(p.a_xf, false) > 0, hb = tab_floats(p.b_xf, false) > 0;
     ta = Tab{q, q + ca, q + 2 * ca, nullptr, nullptr};
     if (ha) q += 3 * ca;
@@ -565,24 +742,25 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     te = Tab{q, q + ce, nullptr, q + 2 * ce, q + 3 * ce};
   }
 
-  // ---- per-thread operand row state (computed once)
-  const TA* Ap = static_cast<const TA*>(p.a_ptr);
-  const TB* Bp = static_cast<const TB*>(p.b_ptr);
-  RowOperand<TA, A_MODE> ars[A_VM ? 1 : A_PER];
-  ColOperand<TA, A_MODE> acs[A_VM ? A_PER : 1];
-  RowOperand<TB, B_MODE> brs[B_VM ? 1 : B_PER];
-  ColOperand<TB, B_MODE> bcs[B_VM ? B_PER : 1];
+  // ---- operand sources and per-thread row state (computed once)
+  const Src<TA> sa = make_src<TA>(p.a_ptr, p.a_bytes, p.a_xf);
+  const Src<TB> sb = make_src<TB>(p.b_ptr, p.b_bytes, p.b_xf);
+  const PhaseInfo pq = make_phase(p, phase);
+  RowOperand<TA, A_MODE, VEC> ars[A_VM ? 1 : A_PER];
+  ColOperand<TA, A_MODE, VEC> acs[A_VM ? A_PER : 1];
+  RowOperand<TB, B_MODE, VEC> brs[B_VM ? 1 : B_PER];
+  ColOperand<TB, B_MODE, VEC> bcs[B_VM ? B_PER : 1];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const int o = tid + i * NTHREADS;
     if constexpr (!A_VM) ars[i].init(p, m0 + o / KO, p.M, phase, p.a_ld);
-    else acs[i].init(p, m0 + (o % (BM / 4)) * 4, p.M, p.a_ld, p.a_xf);
+    else acs[i].init(p, m0 + (o % (BM / 4)) * 4, p.M, p.a_xf);
   }
 #pragma unroll
   for (int i = 0; i < B_PER; ++i) {
     const int o = tid + i * NTHREADS;
     if constexpr (!B_VM) brs[i].init(p, n0 + o / KO, p.N, phase, p.b_ld);
-    else bcs[i].init(p, n0 + (o % (BN / 4)) * 4, p.N, p.b_ld, p.b_xf);
+    else bcs[i].init(p, n0 + (o % (BN / 4)) * 4, p.N, p.b_xf);
   }
 
   f32x4 acc[TM][TN];
@@ -598,17 +776,17 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
-      if (o < A_OCT) {
-        if constexpr (!A_VM) ars[i].load(p, p.a_xf, Ap, phase, kb + (o % KO) * 8, Kp, pa[i]);
-        else acs[i].load(p, p.a_xf, Ap, phase, kb + 2 * (o / (BM / 4)), Kp, pa[i]);
+      if (A_OCT % NTHREADS == 0 || o < A_OCT) {
+        if constexpr (!A_VM) ars[i].load(p, sa, pq, p.fd_ach, kb + (o % KO) * 8, Kp, pa[i]);
+        else acs[i].load(p, sa, pq, kb + 2 * (o / (BM / 4)), Kp, pa[i]);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int o = tid + i * NTHREADS;
-      if (o < B_OCT) {
-        if constexpr (!B_VM) brs[i].load(p, p.b_xf, Bp, phase, kb + (o % KO) * 8, Kp, pb[i]);
-        else bcs[i].load(p, p.b_xf, Bp, phase, kb + 2 * (o / (BN / 4)), Kp, pb[i]);
+      if (B_OCT % NTHREADS == 0 || o < B_OCT) {
+        if constexpr (!B_VM) brs[i].load(p, sb, pq, p.fd_bch, kb + (o % KO) * 8, Kp, pb[i]);
+        else bcs[i].load(p, sb, pq, kb + 2 * (o / (BN / 4)), Kp, pb[i]);
       }
     }
   };
@@ -616,28 +794,40 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
-      if (o < A_OCT) {
-        finish<A_VM>(p.a_xf, ta, pa[i]);
+      if (A_OCT % NTHREADS == 0 || o < A_OCT) {
+        if constexpr (VEC) {
+          if constexpr (!A_VM) store_vk<T, TA>(sa, ta, pa[i], As[buf] + (o / KO) * LDK + (o % KO) * 8);
+          else store_vm<T, TA, A_MODE>(sa, ta, pa[i], As[buf] + (o % (BM / 4)) * 4 * LDK + 2 * (o / (BM / 4)), LDK);
+          continue;
+        }
+        float v[8];
+        finish<TA, A_MODE, A_VM, VEC>(p, sa, ta, pa[i], v);
         if constexpr (!A_VM) {
-          st8(As[buf] + (o / KO) * LDK + (o % KO) * 8, pa[i].v);
+          st8(As[buf] + (o / KO) * LDK + (o % KO) * 8, v);
         } else {
           const int rq = o % (BM / 4), kp = o / (BM / 4);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) st2(As[buf] + (rq * 4 + j) * LDK + 2 * kp, pa[i].v[2 * j], pa[i].v[2 * j + 1]);
+          for (int j = 0; j < 4; ++j) st2(As[buf] + (rq * 4 + j) * LDK + 2 * kp, v[j], v[4 + j]);
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int o = tid + i * NTHREADS;
-      if (o < B_OCT) {
-        finish<B_VM>(p.b_xf, tb, pb[i]);
+      if (B_OCT % NTHREADS == 0 || o < B_OCT) {
+        if constexpr (VEC) {
+          if constexpr (!B_VM) store_vk<T, TB>(sb, tb, pb[i], Bs[buf] + (o / KO) * LDK + (o % KO) * 8);
+          else store_vm<T, TB, B_MODE>(sb, tb, pb[i], Bs[buf] + (o % (BN / 4)) * 4 * LDK + 2 * (o / (BN / 4)), LDK);
+          continue;
+        }
+        float v[8];
+        finish<TB, B_MODE, B_VM, VEC>(p, sb, tb, pb[i], v);
         if constexpr (!B_VM) {
-          st8(Bs[buf] + (o / KO) * LDK + (o % KO) * 8, pb[i].v);
+          st8(Bs[buf] + (o / KO) * LDK + (o % KO) * 8, v);
         } else {
           const int rq = o % (BN / 4), kp = o / (BN / 4);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) st2(Bs[buf] + (rq * 4 + j) * LDK + 2 * kp, pb[i].v[2 * j], pb[i].v[2 * j + 1]);
+          for (int j = 0; j < 4; ++j) st2(Bs[buf] + (rq * 4 + j) * LDK + 2 * kp, v[j], v[4 + j]);
         }
       }
     }
@@ -696,6 +886,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     if (first_block && p.dbc) closed_form_db(p.dbc_from_b ? p.b_xf : p.a_xf, p.dbc);
   }
   __syncthreads();   // tables ready
+  PROBE_MARK(1);
   if (kt0 < kt1) {
     store_tiles(0);
     __syncthreads();
@@ -709,6 +900,14 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
       buf ^= 1;
     }
   }
+
+  PROBE_MARK(2);
+#ifdef VAE_PROBE
+  struct ProbeEnd {
+    unsigned long long* pr; unsigned long long* clk; unsigned long long w0;
+    __device__ ~ProbeEnd() { PROBE_MARK(3); probe_write(pr, clk, w0); }
+  } probe_end{p.probe, clk, wall0};
+#endif
 
   // ------------------------------------------------------------------------ epilogue
   // lane holds rows 4*(lane>>4)+e, column lane&15 of each 16x16 tile
@@ -788,7 +987,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
   constexpr bool EPI_TBL = (EM == E_BNBWD);
   __shared__ float r1[4][64], r2[4][64];
   extern __shared__ float tabs[];
-  const int ce = p.epi_xf.channels;
+  const int ce = tab_stride(p.epi_xf.channels);
   const Tab te{tabs, tabs + ce, nullptr, tabs + 2 * ce, tabs + 3 * ce};
   if constexpr (EPI_TBL) tab_fill(p.epi_xf, te, true, false);
   __syncthreads();

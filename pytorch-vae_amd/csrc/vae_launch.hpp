@@ -3,6 +3,10 @@
 #pragma once
 #include "vae_igemm.hpp"
 
+#ifdef VAE_PROBE
+extern "C" unsigned long long* vae_probe_buffer(void);
+#endif
+
 namespace vae {
 namespace {
 
@@ -25,7 +29,9 @@ inline bool xf_ok(const vae_xform& x, const char* what) {
       fail(VAE_E_BADARG, "%s: BN_DY transform needs dgamma/dbeta/aux", what); return false;
     }
   }
-  if (x.kind == VAE_X_ACT && !(x.slope >= 0.f)) { fail(VAE_E_BADARG, "%s: bad slope", what); return false; }
+  if ((x.kind == VAE_X_ACT || x.kind == VAE_X_BN_ACT) && !(x.slope >= 0.f && x.slope <= 1.f)) {
+    fail(VAE_E_BADARG, "%s: LeakyReLU slope %g outside [0, 1]", what, x.slope); return false;
+  }
   return true;
 }
 
@@ -64,6 +70,51 @@ inline GemmParams base_params() {
   return p;
 }
 
+// Elements a tensor operand spans (the buffer-resource extent; aux tensors are shaped alike).
+template <int AM>
+inline long a_elems(const GemmParams& p) {
+  if (AM == A_CONV || AM == A_CONVT) return (long)p.gn * p.gh * p.gw * p.gc;
+  if (AM == A_DENSE) return (long)(p.M - 1) * p.a_ld + p.K;
+  return (long)(p.K - 1) * p.a_ld + p.M;   // A_KM
+}
+
+template <int BMD>
+inline long b_elems(const GemmParams& p) {
+  if (BMD == B_GATHER) return (long)p.gn * p.gh * p.gw * p.gc;
+  if (BMD == B_NK) return (long)(p.N - 1) * p.b_ld + p.K;
+  const long rows = p.b_taps ? (long)p.gc * p.gr * p.gr : p.K;   // B_KN
+  return (rows - 1) * p.b_ld + (p.ones_col >= 0 ? p.N - 1 : p.N);
+}
+
+inline bool aligned(const void* ptr, int bytes) { return ((uintptr_t)ptr & (uintptr_t)(bytes - 1)) == 0; }
+
+// Packed (vector) operand layout: V_K groups read 8 consecutive k of one row, V_M groups 4
+// consecutive rows of one k.  Needs aligned rows, and for a BatchNorm transform channels that
+// run consecutively inside a group.
+inline bool bn_kind(const vae_xform& x) { return x.kind == VAE_X_BN_ACT || x.kind == VAE_X_BN_DY; }
+
+template <int MODE>   // AMode, or 100 + BMode
+inline int operand_vec(const GemmParams& p, const void* ptr, const vae_xform& xf, int esize) {
+  const bool vk = MODE == A_CONV || MODE == A_CONVT || MODE == A_DENSE || MODE == 100 + B_NK;
+  const int grp = vk ? 8 : 4;
+  const int vbytes = (grp * esize) < 16 ? grp * esize : 16;
+  if (!aligned(ptr, vbytes) || (xf.kind == VAE_X_BN_DY && !aligned(xf.aux, vbytes))) return 0;
+  if (bn_kind(xf) && xf.channels % grp) return 0;
+  // V_K groups must not straddle the end of K, V_M groups the end of the rows: the packed path
+  // has no per-element masks (out-of-range groups read as 0 through the buffer resource)
+  const int nrows = p.N - (p.ones_col >= 0 ? 1 : 0);
+  switch (MODE) {
+    case A_CONV: return !p.g_nchw && p.gc % grp == 0;
+    case 100 + B_GATHER: return !p.g_nchw && p.gc % grp == 0 && nrows % grp == 0;
+    case A_CONVT: return p.gc % grp == 0;
+    case A_DENSE: return p.a_ld % grp == 0 && p.K % grp == 0;
+    case A_KM: return p.a_ld % grp == 0 && p.M % grp == 0;
+    case 100 + B_NK: return p.b_ld % grp == 0 && p.K % grp == 0;
+    case 100 + B_KN: return p.b_ld % grp == 0 && nrows % grp == 0;
+  }
+  return 0;
+}
+
 inline void finish_divs(GemmParams& p) {
   p.fd_gq = make_fastdiv(p.gq > 0 ? p.gq : 1);
   p.fd_gp = make_fastdiv(p.gp > 0 ? p.gp : 1);
@@ -71,6 +122,8 @@ inline void finish_divs(GemmParams& p) {
   p.fd_gr = make_fastdiv(p.gr > 0 ? p.gr : 1);
   p.fd_ntw[0] = make_fastdiv(p.ntap_w[0] > 0 ? p.ntap_w[0] : 1);
   p.fd_ntw[1] = make_fastdiv(p.ntap_w[1] > 0 ? p.ntap_w[1] : 1);
+  p.fd_ach = make_fastdiv(p.a_xf.channels > 0 ? p.a_xf.channels : 1);
+  p.fd_bch = make_fastdiv(p.b_xf.channels > 0 ? p.b_xf.channels : 1);
 }
 
 struct Tile { int bm, bn; };
@@ -111,19 +164,35 @@ inline int launch_finalize(const GemmParams& p, hipStream_t st) {
   return check_launch("igemm_finalize");
 }
 
-template <class T, class TA, class TB, int AM, int BMD, int EM>
-inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
+template <class T, class TA, class TB, int AM, int BMD, int EM, bool VEC>
+inline void launch_shape(const GemmParams& p, Tile t, hipStream_t st) {
   const dim3 block(NTHREADS);
   const dim3 grid((p.M + t.bm - 1) / t.bm, (p.N + t.bn - 1) / t.bn, p.nphase * p.ksplit);
   const size_t lds = (size_t)table_floats(p, EM == E_BNBWD) * 4;
   if (t.bm == 64 && t.bn == 64)
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 64, 64, AM, BMD, EM>), grid, block, lds, st, p);
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 64, 64, AM, BMD, EM, VEC>), grid, block, lds, st, p);
   else if (t.bm == 128 && t.bn == 32)
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 128, 32, AM, BMD, EM>), grid, block, lds, st, p);
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 128, 32, AM, BMD, EM, VEC>), grid, block, lds, st, p);
   else if (t.bm == 32 && t.bn == 64)
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 64, AM, BMD, EM>), grid, block, lds, st, p);
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 64, AM, BMD, EM, VEC>), grid, block, lds, st, p);
   else
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 32, AM, BMD, EM>), grid, block, lds, st, p);
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 32, AM, BMD, EM, VEC>), grid, block, lds, st, p);
+}
+
+template <class T, class TA, class TB, int AM, int BMD, int EM>
+inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
+  const long ab = a_elems<AM>(p) * (long)sizeof(TA), bb = b_elems<BMD>(p) * (long)sizeof(TB);
+  if (ab <= 0 || bb <= 0 || ab >= (1l << 31) || bb >= (1l << 31))
+    return fail(VAE_E_UNSUPPORTED, "igemm: operand of %ld / %ld bytes (buffer addressing needs < 2 GiB)", ab, bb);
+  p.a_bytes = (uint32_t)ab;
+  p.b_bytes = (uint32_t)bb;
+#ifdef VAE_PROBE
+  p.probe = vae_probe_buffer();
+#endif
+  const bool vec = operand_vec<AM>(p, p.a_ptr, p.a_xf, (int)sizeof(TA)) &&
+                   operand_vec<100 + BMD>(p, p.b_ptr, p.b_xf, (int)sizeof(TB));
+  if (vec) launch_shape<T, TA, TB, AM, BMD, EM, true>(p, t, st);
+  else launch_shape<T, TA, TB, AM, BMD, EM, false>(p, t, st);
   int rc = check_launch("igemm");
   if (rc) return rc;
   if (EM != E_ACC && p.slab) return launch_finalize<T, EM>(p, st);

@@ -465,6 +465,13 @@ using namespace vae;
 extern "C" int vae_abi_version(void) { return VAE_ABI_VERSION; }
 extern "C" const char* vae_last_error(void) { return g_err; }
 
+#ifdef VAE_PROBE
+// Diagnostics build only: device buffer the GEMM kernels append per-block phase records to.
+static unsigned long long* g_probe = nullptr;
+extern "C" void vae_probe_set(void* buf) { g_probe = static_cast<unsigned long long*>(buf); }
+extern "C" unsigned long long* vae_probe_buffer(void) { return g_probe; }
+#endif
+
 extern "C" int vae_head_fwd(const vae_head_args* a, void* stream) {
   HeadP p;
   int rc = head_setup(a, p, "head_fwd");

@@ -15,6 +15,9 @@ import torch  # noqa: F401  (must precede the library: one HIP runtime per proce
 
 LIB_NAME = "libvaehip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
+if os.environ.get("VAE_HIP_LIB") == "probe":
+    LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
 ABI_VERSION = 1
 
 F32, BF16 = 0, 1
