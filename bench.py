@@ -89,6 +89,8 @@ def head_cost(fn, a, dsz):
         return 2 * macs, x_b + 2 * img          # reads x, target; writes recon
     if fn == "vae_head_bwd_data":
         return 2 * macs, 2 * img + x_b + x_b    # recon, target, y (epilogue) -> dx
+    if fn == "vae_head_bwd":
+        return 4 * macs, 2 * img + x_b + x_b + 3 * a.c * 9 * 4   # data + filter in one pass
     return 2 * macs, x_b + 2 * img + 3 * a.c * 9 * 4
 
 

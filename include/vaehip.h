@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 1
+#define VAE_ABI_VERSION 4
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -77,6 +77,22 @@ typedef struct vae_xform {
   const void* aux;         /* BN_DY: pre-BN tensor y, indexed like the operand (dtype) */
   float* running_mean;     /* optional: updated once per call (unbiased var, as torch) */
   float* running_var;
+  /* Replicated statistics: sum/sumsq (and dgamma/dbeta) hold `reps` partial copies, replica r
+   * at offset r*rstride floats; the value of channel c is the sum over replicas.  Producers
+   * spread their per-block atomics over the replicas so that thousands of workgroups do not
+   * serialise on the same 2*C addresses.  reps <= 1: a single copy. */
+  int32_t reps;
+  int32_t rstride;
+  /* BN_DY only: when set, the operation writes the reduced dL/dgamma, dL/dbeta here
+   * (accumulating) — the BatchNorm affine gradients the optimizer reads. */
+  float* dgamma_out;
+  float* dbeta_out;
+  /* Precomputed coefficient table (vae_bn_finalize), planar fp32:
+   *   BN_ACT [4][C] = {gamma*invstd, beta - mean*gamma*invstd, invstd, -mean*invstd}
+   *   BN_DY  [3][C] = {A, B, C} with dy = A*g + B*y + C.
+   * When set, consumers load it instead of reducing the statistics themselves, and running
+   * statistics / dgamma_out / dbeta_out are left to vae_bn_finalize. */
+  const float* table;
 } vae_xform;
 
 /* One convolution-family operation.  Geometry is that of the reference layer:
@@ -97,6 +113,8 @@ typedef struct vae_conv_args {
   void* y;                 /* fwd: output pre-activation (NHWC, dtype) */
   float* y_sum;            /* fwd: optional per-channel Σ(acc), Σ(acc^2) for the next BN */
   float* y_sumsq;
+  int32_t sum_reps;        /* replicas of y_sum/y_sumsq (fwd) or dx_dgamma/dx_dbeta (bwd_data), */
+  int32_t sum_rstride;     /* see vae_xform.reps; <= 1: one copy */
   const void* residual;    /* fwd: optional y += xf(residual) (VQ-VAE ResidualLayer) */
   vae_xform residual_xf;
   /* backward */
@@ -129,6 +147,7 @@ typedef struct vae_linear_args {
   const void* dy;          /* [m][n] */
   int32_t dy_f32;          /* bwd: dy is fp32 (d[mu|logvar]) instead of dtype */
   void* dx; vae_xform dx_epi; float* dx_dgamma; float* dx_dbeta;
+  int32_t sum_reps, sum_rstride;   /* replicas of dx_dgamma / dx_dbeta (vae_xform.reps) */
   float* dw; float* db;
   /* reparameterization backward epilogue (decoder_input bwd_data): when mulv != NULL the
    * kernel turns dz into d[mu|logvar] (vanilla_vae.py:107-117 + the analytic KL of :143) */
@@ -156,9 +175,29 @@ typedef struct vae_head_args {
   float* sse;              /* [n] Σ(recon-target)^2 per image, accumulated */
   const float* coef;       /* bwd: [n] dL/d(sse_i); g = coef*(recon-target)*(1-recon^2) */
   void* dx; vae_xform dx_epi; float* dx_dgamma; float* dx_dbeta;
+  int32_t sum_reps, sum_rstride;   /* replicas of dx_dgamma / dx_dbeta (vae_xform.reps) */
   float* dw; float* db;
   const float* grad_recon; /* bwd alternative to coef: dL/drecon (NCHW fp32), g = grad*(1-recon^2) */
+  void* workspace;         /* bwd (bf16): fp32 scratch for per-workgroup dW/db partials (summed in a
+                              fixed order); NULL: atomics straight into dw/db */
+  int64_t workspace_bytes;
 } vae_head_args;
+
+/* One BatchNorm's per-step finalisation, run once between the kernel that produces its
+ * statistics and the kernels that consume them (vanilla_vae.py:30,56,71 BatchNorm2d in
+ * train mode; torch semantics for the running-statistic update).
+ *   mode 0 (forward):  xf.sum/sumsq replicas -> table [4][C]; running_mean/var updated
+ *                      (momentum, unbiased variance) when set.
+ *   mode 1 (backward): xf.dgamma/dbeta replicas -> table [3][C]; dL/dgamma, dL/dbeta added to
+ *                      xf.dgamma_out / dbeta_out; when db is set, the gradient of the bias of
+ *                      the conv feeding the BatchNorm is added in closed form,
+ *                      db_c = A*Σg + B*Σy + C*M. */
+typedef struct vae_bn_args {
+  int32_t mode;
+  vae_xform xf;
+  float* table;
+  float* db;
+} vae_bn_args;
 
 /* Loss kinds (vanilla_vae.py:124-146, beta_vae.py:129-152, iwae.py:129-160) */
 enum vae_loss_kind { VAE_LOSS_VANILLA = 0, VAE_LOSS_BETA_H = 1, VAE_LOSS_BETA_B = 2, VAE_LOSS_IWAE = 3 };
@@ -197,6 +236,11 @@ int vae_linear_bwd_filter(const vae_linear_args* a, void* stream);
 int vae_head_fwd(const vae_head_args* a, void* stream);
 int vae_head_bwd_data(const vae_head_args* a, void* stream);
 int vae_head_bwd_filter(const vae_head_args* a, void* stream);
+/* both halves of the head backward in one pass over the input tile (bf16 MFMA path; the fp32
+ * path runs bwd_data then bwd_filter) */
+int vae_head_bwd(const vae_head_args* a, void* stream);
+/* --- BatchNorm finalisation (see vae_bn_args) ------------------------------------------ */
+int vae_bn_finalize(const vae_bn_args* a, void* stream);
 /* --- reparameterization (vanilla_vae.py:107-117): z = eps*exp(.5*logvar) + mu,
  *     row r uses mu row r/samples.  z is written in `dtype`. */
 int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int32_t latent,

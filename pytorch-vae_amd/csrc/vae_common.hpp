@@ -18,6 +18,8 @@ namespace vae {
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);
 int check_launch(const char* what);
+// returned by a fast-path launcher whose preconditions do not hold (the caller falls back)
+constexpr int kHeadFallback = 0x7fff0001;
 
 // ---------------------------------------------------------------- scalar conversion
 __device__ __forceinline__ float ld_f(const float* p) { return *p; }
@@ -69,11 +71,30 @@ __device__ __forceinline__ void st2(__bf16* d, float a, float b) {
 __device__ __forceinline__ float lrelu(float v, float slope) { return fmaxf(v, v * slope); }
 
 // ---------------------------------------------------------------- BN statistics
+// Channel c of a replicated statistic (vae_xform.reps copies, rstride floats apart).  Loads go
+// out 16 at a time with clamped (never skipped) addresses, so a 32-replica sum costs two
+// dependent round trips, not 32.
+__device__ __forceinline__ float rsum(const float* a, const vae_xform& x, int c) {
+  if (x.reps <= 1) return a[c];
+  float acc = 0.f;
+  for (int r0 = 0; r0 < x.reps; r0 += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = min(r0 + u, x.reps - 1);
+      v[u] = a[(long)r * x.rstride + c];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += (r0 + u < x.reps) ? v[u] : 0.f;
+  }
+  return acc;
+}
+
 // mean/invstd/var of channel c from the producer's Σ(y-shift), Σ(y-shift)^2.
 __device__ __forceinline__ void bn_moments(const vae_xform& x, int c, float& mean, float& invstd, float& var) {
   const float inv_m = 1.0f / x.count;
-  const float s = x.sum[c] * inv_m;
-  var = fmaxf(x.sumsq[c] * inv_m - s * s, 0.0f);
+  const float s = rsum(x.sum, x, c) * inv_m;
+  var = fmaxf(rsum(x.sumsq, x, c) * inv_m - s * s, 0.0f);
   mean = s + (x.shift ? x.shift[c] : 0.0f);
   invstd = 1.0f / sqrtf(var + x.eps);
 }
@@ -108,8 +129,8 @@ struct XfTable {
       } else {
         const float inv_m = 1.0f / x.count;
         const float A = g * invstd;
-        const float mg = x.dbeta[ch] * inv_m;         // mean of g
-        const float mgx = x.dgamma[ch] * inv_m;       // mean of g*xhat
+        const float mg = rsum(x.dbeta, x, ch) * inv_m;         // mean of g
+        const float mgx = rsum(x.dgamma, x, ch) * inv_m;       // mean of g*xhat
         a[ch] = A;
         b[ch] = -A * invstd * mgx;
         c[ch] = -A * (mg - mean * invstd * mgx);

@@ -18,8 +18,9 @@ extern "C" int vae_convT2d_fwd(const vae_conv_args* a, void* stream) {
   p.gn = a->n; p.gh = a->h; p.gw = a->w; p.gc = a->c;
   p.gp = a->p / S; p.gq = a->q / S; p.gr = a->r; p.gs = S; p.gpad = a->pad; p.gho = a->p; p.gwo = a->q;
   p.out = a->y; p.out_ld = a->k; p.out_phase = 1; p.bias = a->bias; p.sum = a->y_sum; p.sumsq = a->y_sumsq;
+  p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.residual = a->residual; p.res_xf = sanitize(a->residual_xf);
-  return launch<A_CONVT, B_KN, E_STORE>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
+  return launch<A_CONVT, B_KN, E_STORE, false, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
                                         (hipStream_t)stream);
 }
 
@@ -35,8 +36,9 @@ extern "C" int vae_convT2d_bwd_data(const vae_conv_args* a, void* stream) {
   p.gr = a->r; p.gs = a->stride; p.gpad = a->pad;
   p.out = a->dx; p.out_ld = a->c;
   p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+  p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "convT2d_bwd_data: dgamma/dbeta");
-  return launch<A_CONV, B_NK, E_BNBWD>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
+  return launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
                                        (hipStream_t)stream);
 }
 
@@ -54,7 +56,7 @@ extern "C" int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream) {
   p.gn = a->n; p.gh = a->p; p.gw = a->q; p.gc = a->k; p.gp = a->h; p.gq = a->w;
   p.gr = a->r; p.gs = a->stride; p.gpad = a->pad;
   p.out = a->dw; p.out_ld = Nw;
-  int rc = launch<A_KM, B_GATHER, E_ACC>(a->dtype, false, false, p, a->split_k, nullptr, 0, (hipStream_t)stream);
+  int rc = launch<A_KM, B_GATHER, E_ACC, false, true>(a->dtype, false, false, p, a->split_k, nullptr, 0, (hipStream_t)stream);
   if (rc) return rc;
   if (a->db && !closed) return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
   return VAE_OK;

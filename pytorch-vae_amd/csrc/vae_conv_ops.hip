@@ -14,8 +14,9 @@ extern "C" int vae_conv2d_fwd(const vae_conv_args* a, void* stream) {
   p.gn = a->n; p.gh = a->h; p.gw = a->w; p.gc = a->c; p.gp = a->p; p.gq = a->q;
   p.gr = a->r; p.gs = a->stride; p.gpad = a->pad;
   p.out = a->y; p.out_ld = a->k; p.bias = a->bias; p.sum = a->y_sum; p.sumsq = a->y_sumsq;
+  p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.residual = a->residual; p.res_xf = sanitize(a->residual_xf);
-  return launch<A_CONV, B_NK, E_STORE, true>(a->dtype, a->x_nchw_f32 != 0, false, p, a->split_k, a->workspace,
+  return launch<A_CONV, B_NK, E_STORE, false, false, true>(a->dtype, a->x_nchw_f32 != 0, false, p, a->split_k, a->workspace,
                                              a->workspace_bytes, (hipStream_t)stream);
 }
 
@@ -38,8 +39,9 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   p.gp = a->h / S; p.gq = a->w / S; p.gr = a->r; p.gs = S; p.gpad = a->pad; p.gho = a->h; p.gwo = a->w;
   p.out = a->dx; p.out_ld = a->c; p.out_phase = 1;
   p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+  p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
-  return launch<A_CONVT, B_KN, E_BNBWD>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
+  return launch<A_CONVT, B_KN, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
                                         (hipStream_t)stream);
 }
 
@@ -59,6 +61,6 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
   p.gn = a->n; p.gh = a->h; p.gw = a->w; p.gc = a->c; p.gp = a->p; p.gq = a->q;
   p.gr = a->r; p.gs = a->stride; p.gpad = a->pad;
   p.out = a->dw; p.out_ld = Nw;
-  return launch<A_KM, B_GATHER, E_ACC, false, true>(a->dtype, false, a->x_nchw_f32 != 0, p, a->split_k, nullptr, 0,
+  return launch<A_KM, B_GATHER, E_ACC, true, false, false, true>(a->dtype, false, a->x_nchw_f32 != 0, p, a->split_k, nullptr, 0,
                                                     (hipStream_t)stream);
 }

@@ -1,0 +1,484 @@
+// Decoder head on MFMA (bf16 throughput mode): final_layer Conv2d(32->3, k3, s1, p1) + Tanh
+// (models/vanilla_vae.py:73-75), the reconstruction SSE of the ELBO (:140) and their backward.
+//
+// The layer has 3 output channels: as a GEMM over pixels its N is 3, so the forward pads N to
+// the 16 of one v_mfma_f32_16x16x32_bf16 (13/16 of the MFMA is wasted, and the MFMA is still far
+// from being the limit).  Everything is organised around one LDS tile per workgroup: 4 image
+// rows x 64 columns (+1 halo on every side) x 32 channels of act = lrelu(BN(y)), bf16, with the
+// 16-byte channel chunks of a pixel XOR-swizzled by (column & 3) so that 16 lanes reading 16
+// consecutive pixels hit 16 different bank slots.
+//
+//   forward : 16 pixels x 16 (3 real) outputs, K = 9 taps x 32 channels = 9 MFMAs;
+//             epilogue tanh -> recon (NCHW fp32, float4 stores), (recon - x)^2 -> SSE.
+//   backward: one persistent kernel, per tile
+//     data   dact[p][c] = sum_{tap,co} gseed[p + 1 - tap][co] W[co][tap][c]: K = 9 taps x 4 (3 co
+//            + pad) = 36 -> 2 k-steps, N = 32 channels; epilogue g = dact * lrelu'(z) (z = BN(y)),
+//            BatchNorm-backward sums (sum g, sum g*xhat) and g stored through LDS as whole rows;
+//     filter dW[co][tap][c] = sum_p gseed[p][co] act[p + tap - 1][c]: M = co (pad 16), N = 288,
+//            K = the tile's 256 pixels; the act operand is read transposed (ds_read_b64_tr_b16)
+//            from the same LDS tile; per-block partials go to a slab summed by vae_reduce_rows
+//            (fixed order: deterministic, and no same-address atomics).
+#include "vae_common.hpp"
+
+namespace vae {
+namespace {
+
+constexpr int HC = 32;                 // channels entering the head
+constexpr int HW = 64;                 // image width (one tile row)
+constexpr int ROWS = 4;                // image rows per tile
+constexpr int TR = ROWS + 2, TCOLS = HW + 2, TPIX = TR * TCOLS;   // tile with halo
+constexpr int OCT = TPIX * (HC / 8);   // 16-byte octets in the act tile
+constexpr int OCT_PER_T = (OCT + 255) / 256;
+constexpr int OWN = ROWS * HW;         // pixels a tile produces
+constexpr int NCO = 3;
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;
+
+struct HeadQ {
+  int n, h, samples, tiles;
+  const __bf16* x; vae_xform xf;       // fin (pre-BN), its BatchNorm+LeakyReLU
+  const float* wt; const float* bias;  // [3][3][3][32] fp32 native, [3]
+  const float* target; float* recon; float* sse;
+  const float* coef; const float* grad_recon;
+  __bf16* dx; float* dgamma; float* dbeta; int sum_reps, sum_rstride;
+  float* slab;                         // [grid][3*288 + 3] filter partials, or NULL: atomics into dw/db
+  float* dw; float* db;
+  int data, filter;
+};
+
+__device__ __forceinline__ rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// byte offset of (tile pixel, 16-byte channel chunk) in the act tile
+__device__ __forceinline__ int act_off(int trow, int tcol, int chunk) {
+  return (trow * TCOLS + tcol) * (HC * 2) + ((chunk ^ (tcol & 3)) << 4);
+}
+
+__device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
+
+// Per-channel BN coefficients in LDS (from vae_bn_finalize's table when present).
+__device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq) {
+  for (int c = threadIdx.x; c < HC; c += blockDim.x) {
+    if (xf.kind != VAE_X_BN_ACT) { ta[c] = 1.f; tb[c] = 0.f; tp[c] = 0.f; tq[c] = 0.f; continue; }
+    if (xf.table) {
+      ta[c] = xf.table[c]; tb[c] = xf.table[HC + c]; tp[c] = xf.table[2 * HC + c]; tq[c] = xf.table[3 * HC + c];
+    } else {
+      float mean, invstd, var;
+      bn_moments(xf, c, mean, invstd, var);
+      ta[c] = xf.gamma[c] * invstd; tb[c] = xf.beta[c] - mean * ta[c];
+      tp[c] = invstd; tq[c] = -mean * invstd;
+    }
+  }
+}
+
+// Raw y octets of the tile (halo included) -> registers; issued together (out of image: 0).
+__device__ __forceinline__ void tile_load(const HeadQ& q, rsrc_t ry, int n, int h0, u32x4 (&raw)[OCT_PER_T]) {
+#pragma unroll
+  for (int j = 0; j < OCT_PER_T; ++j) {
+    const int o = threadIdx.x + 256 * j;
+    const int pix = o >> 2, ch = o & 3;
+    const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+    const int hi = h0 + trow - 1, wi = tcol - 1;
+    const bool ok = o < OCT && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+    const uint32_t off = ok ? (uint32_t)((((n * q.h + hi) * HW + wi) * HC + ch * 8) * 2) : kOOB;
+    raw[j] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
+  }
+}
+
+// act = lrelu(a*y + b) (0 outside the image) -> bf16 tile in LDS
+__device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (&raw)[OCT_PER_T], char* tile,
+                                           const float* ta, const float* tb) {
+#pragma unroll
+  for (int j = 0; j < OCT_PER_T; ++j) {
+    const int o = threadIdx.x + 256 * j;
+    if (o >= OCT) continue;
+    const int pix = o >> 2, ch = o & 3;
+    const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+    const int hi = h0 + trow - 1, wi = tcol - 1;
+    const bool ok = hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+    u32x4 out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c0 = ch * 8 + 2 * e;
+      float lo = bf2f(raw[j][e] & 0xffffu), hi2 = bf2f(raw[j][e] >> 16);
+      lo = fmaf(lo, ta[c0], tb[c0]);
+      hi2 = fmaf(hi2, ta[c0 + 1], tb[c0 + 1]);
+      if (q.xf.kind != VAE_X_NONE) { lo = fmaxf(lo, lo * q.xf.slope); hi2 = fmaxf(hi2, hi2 * q.xf.slope); }
+      lo = ok ? lo : 0.f;
+      hi2 = ok ? hi2 : 0.f;
+      bf16x2 pk; pk[0] = (__bf16)lo; pk[1] = (__bf16)hi2;
+      out[e] = *reinterpret_cast<uint32_t*>(&pk);
+    }
+    *reinterpret_cast<u32x4*>(tile + act_off(trow, tcol, ch)) = out;
+  }
+}
+
+// ======================================================================= forward
+__global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
+  __shared__ __attribute__((aligned(16))) char tile[TPIX * HC * 2];
+  __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int tiles_per_img = q.h / ROWS;
+  const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x - n * tiles_per_img) * ROWS;
+  const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
+  u32x4 raw[OCT_PER_T];
+  tile_load(q, ry, n, h0, raw);
+  // B fragments: W[co = lane&15][tap][8*(lane>>4) .. +7] (zero for co >= 3)
+  const int co = lane & 15, g = lane >> 4;
+  bf16x8 bw[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bw[t][j] = (__bf16)(co < NCO ? q.wt[(co * 9 + t) * HC + 8 * g + j] : 0.f);
+  const float bco = co < NCO ? q.bias[co] : 0.f;
+  head_tables(q.xf, ta, tb, tp, tq);
+  __syncthreads();
+  tile_store(q, h0, raw, tile, ta, tb);
+  __syncthreads();
+  float sq = 0.f;
+  const int img_t = n / q.samples;
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    const int grp = wave * 4 + gi;                  // 16 groups of 16 pixels
+    const int row = grp >> 2, c0 = (grp & 3) * 16;
+    f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int r = t / 3, s = t - 3 * (t / 3);
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + act_off(row + r, c0 + (lane & 15) + s, g));
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[t], acc, 0, 0, 0);
+    }
+    // lane: output channel co, pixels c0 + 4g + i
+    if (co < NCO) {
+      const int hh = h0 + row, w0 = c0 + 4 * g;
+      f32x4v y;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = tanhf(acc[i] + bco);
+      *reinterpret_cast<f32x4v*>(q.recon + (((long)n * NCO + co) * q.h + hh) * HW + w0) = y;
+      const f32x4v tg = *reinterpret_cast<const f32x4v*>(q.target + (((long)img_t * NCO + co) * q.h + hh) * HW + w0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { const float d = y[i] - tg[i]; sq = fmaf(d, d, sq); }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+  if (lane == 0) red[wave] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(q.sse + n, (red[0] + red[1]) + (red[2] + red[3]));
+}
+
+// ds_read_b64_tr_b16: lane 4q+p of each 16-lane group gives the address of row q, columns
+// 4p..4p+3; lane i receives column i of the 4 rows (row q in element q).
+typedef __bf16 __attribute__((ext_vector_type(4))) __attribute__((address_space(3))) lds_bf16x4;
+__device__ __forceinline__ bf16x4v tr16_read(const char* generic_lds_addr) {
+  const uint32_t off = (uint32_t)(uintptr_t)generic_lds_addr;   // LDS addresses are 32-bit
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(uintptr_t)off);
+}
+
+// ======================================================================= backward
+// gseed = dL/d(pre-tanh) at one pixel/channel
+__device__ __forceinline__ float gseed(const HeadQ& q, int n, int co, int h, int w) {
+  const long oi = (((long)n * NCO + co) * q.h + h) * HW + w;
+  const float y = q.recon[oi];
+  if (q.grad_recon) return q.grad_recon[oi] * (1.f - y * y);
+  const float t = q.target[(((long)(n / q.samples) * NCO + co) * q.h + h) * HW + w];
+  return q.coef[n] * (y - t) * (1.f - y * y);
+}
+
+constexpr int NW = NCO * 9 * HC;        // 864 weight-gradient entries
+constexpr int SLAB_COLS = NW + NCO;     // + 3 bias-gradient entries
+
+__global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
+  __shared__ __attribute__((aligned(16))) char tile[TPIX * HC * 2];
+  __shared__ __attribute__((aligned(16))) uint2 gsA[TPIX];               // [pixel][co0..2, 0] bf16
+  __shared__ __attribute__((aligned(16))) __bf16 gsT[4][OWN];            // [co][own pixel]
+  __shared__ __attribute__((aligned(16))) __bf16 gst[4][16 * HC];        // per-wave output staging
+  __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
+  __shared__ float r1[4][HC], r2[4][HC], rdb[4][NCO];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int tiles_per_img = q.h / ROWS;
+  const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
+
+  // dgrad B fragments: B[k = tap*4 + co][n = c] = W[co][tap][c], k-step ks, n-frag nf
+  bf16x8 bd[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = ks * 8 + 2 * g + (j >> 2), c2 = j & 3, c = nf * 16 + li;
+        bd[ks][nf][j] = (__bf16)(tap < 9 && c2 < NCO ? q.wt[(c2 * 9 + tap) * HC + c] : 0.f);
+      }
+  // filter accumulators: this wave's n-frags f = wave + 4*i (18 n-frags of 16 over (tap, c))
+  constexpr int NFW = 5;
+  f32x4v accw[NFW];
+#pragma unroll
+  for (int i = 0; i < NFW; ++i) accw[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, dbp[NCO] = {0.f, 0.f, 0.f};
+
+  head_tables(q.xf, ta, tb, tp, tq);
+  for (int tile_i = blockIdx.x; tile_i < q.tiles; tile_i += gridDim.x) {
+    const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * ROWS;
+    u32x4 raw[OCT_PER_T];
+    tile_load(q, ry, n, h0, raw);
+    // gseed over the halo tile: threads walk pixels (2 per thread)
+    float gv[2][NCO];
+    int gpix[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pix = threadIdx.x + 256 * j;
+      gpix[j] = pix;
+      const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+      const int hi = h0 + trow - 1, wi = tcol - 1;
+      const bool ok = pix < TPIX && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+#pragma unroll
+      for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = ok ? gseed(q, n, c2, hi, wi) : 0.f;
+    }
+    __syncthreads();                    // previous tile's LDS reads done (and tables ready)
+    tile_store(q, h0, raw, tile, ta, tb);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int pix = gpix[j];
+      if (pix >= TPIX) continue;
+      bf16x4v v; v[0] = (__bf16)gv[j][0]; v[1] = (__bf16)gv[j][1]; v[2] = (__bf16)gv[j][2]; v[3] = (__bf16)0.f;
+      gsA[pix] = *reinterpret_cast<uint2*>(&v);
+      const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+      if (trow >= 1 && trow <= ROWS && tcol >= 1 && tcol <= HW) {
+        const int own = (trow - 1) * HW + (tcol - 1);
+#pragma unroll
+        for (int c2 = 0; c2 < NCO; ++c2) gsT[c2][own] = v[c2];
+        gsT[3][own] = (__bf16)0.f;
+#pragma unroll
+        for (int c2 = 0; c2 < NCO; ++c2) dbp[c2] += gv[j][c2];
+      }
+    }
+    __syncthreads();
+
+    if (q.data) {
+      // ---- dact for this wave's 4 groups of 16 pixels, N = 32 channels (2 n-frags)
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        const int grp = wave * 4 + gi;
+        const int row = grp >> 2, c0 = (grp & 3) * 16;
+        const int hh = h0 + row;
+        // epilogue inputs first: y at this lane's 4 pixels x 2 channels (L2-resident)
+        float yv[2][4];
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t off = (uint32_t)((((n * q.h + hh) * HW + c0 + 4 * g + i) * HC + nf * 16 + li) * 2);
+            yv[nf][i] = bf2f(__builtin_amdgcn_raw_buffer_load_b16(ry, off, 0, 0));
+          }
+        f32x4v acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 a;
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int tap = ks * 8 + 2 * g + half;
+            uint2 v = {0u, 0u};
+            if (tap < 9) {
+              const int r = tap / 3, s = tap - 3 * r;
+              v = gsA[(row + 2 - r) * TCOLS + (c0 + li + 2 - s)];
+            }
+            const bf16x4v b4 = *reinterpret_cast<bf16x4v*>(&v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[4 * half + j] = b4[j];
+          }
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bd[ks][nf], acc[nf], 0, 0, 0);
+        }
+        // g = dact * lrelu'(z); BN-backward sums; stage [16 px][32 ch] for whole-row stores
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          const int c = nf * 16 + li;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float y = yv[nf][i];
+            const float z = fmaf(y, ta[c], tb[c]);
+            const float gg = z > 0.f ? acc[nf][i] : acc[nf][i] * q.xf.slope;
+            s1[nf] += gg;
+            s2[nf] += gg * fmaf(y, tp[c], tq[c]);
+            gst[wave][(4 * g + i) * HC + c] = (__bf16)gg;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // 16 pixels x 64 B = 1 KB contiguous (NHWC): 16 B per lane
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&gst[wave][lane * 8]);
+        *reinterpret_cast<u32x4*>(q.dx + (((long)n * q.h + hh) * HW + c0) * HC + lane * 8) = v;
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+
+    if (q.filter) {
+      // ---- dW partials: M = co (rows 0..2 of 16), N = (tap, c), K = 256 own pixels
+#pragma unroll
+      for (int ks = 0; ks < OWN / 32; ++ks) {
+        const int k0 = ks * 32 + 8 * g;                 // this lane group's 8 pixels
+        const int row = k0 / HW, col = k0 - row * HW;
+        // rows co >= 3 of the M = 16 fragment read the all-zero row 3
+        const bf16x8 az = *reinterpret_cast<const bf16x8*>(&gsT[li < 4 ? li : 3][k0]);
+#pragma unroll
+        for (int i = 0; i < NFW; ++i) {
+          const int f = wave + 4 * i;
+          if (f < 18) {
+            const int tap = f >> 1, cb = (f & 1) * 16;
+            const int r = tap / 3, s = tap - 3 * r;
+            // lane 4qq+pp of the 16-lane group: pixel qq (+4), channels cb + 4pp .. +3
+            const int qq = li >> 2, pp = li & 3;
+            const int ch = cb + 4 * pp;
+            bf16x8 b;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+              const int tcol = col + 4 * half + qq + s, trow = row + r;
+              const char* addr = tile + act_off(trow, tcol, ch >> 3) + ((ch & 4) << 1);
+              const bf16x4v t4 = tr16_read(addr);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) b[4 * half + j] = t4[j];
+            }
+            accw[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az, b, accw[i], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- block reductions
+  if (q.data) {
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      float a = s1[nf], b = s2[nf];
+      a += __shfl_xor(a, 16); a += __shfl_xor(a, 32);
+      b += __shfl_xor(b, 16); b += __shfl_xor(b, 32);
+      if (g == 0) { r1[wave][nf * 16 + li] = a; r2[wave][nf * 16 + li] = b; }
+    }
+  }
+  __syncthreads();
+  if (q.data && threadIdx.x < HC) {
+    const int c = threadIdx.x;
+    const long roff = q.sum_reps > 1 ? (long)(blockIdx.x % q.sum_reps) * q.sum_rstride : 0;
+    atomicAdd(q.dbeta + roff + c, (r1[0][c] + r1[1][c]) + (r1[2][c] + r1[3][c]));
+    atomicAdd(q.dgamma + roff + c, (r2[0][c] + r2[1][c]) + (r2[2][c] + r2[3][c]));
+  }
+#pragma unroll
+  for (int c2 = 0; c2 < NCO; ++c2) {
+    float v = dbp[c2];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) rdb[wave][c2] = v;
+  }
+  __syncthreads();
+  if (q.filter && threadIdx.x < NCO && q.db) {
+    const float v = (rdb[0][threadIdx.x] + rdb[1][threadIdx.x]) + (rdb[2][threadIdx.x] + rdb[3][threadIdx.x]);
+    if (q.slab) q.slab[(long)blockIdx.x * SLAB_COLS + NW + threadIdx.x] = v;
+    else atomicAdd(q.db + threadIdx.x, v);
+  }
+  if (q.filter) {
+    // dW[co][tap][c]: lane li = column within the n-frag, rows 4g+i = co (g == 0, i < 3 real)
+    float* out = q.slab ? q.slab + (long)blockIdx.x * SLAB_COLS : q.dw;
+#pragma unroll
+    for (int i = 0; i < NFW; ++i) {
+      const int f = wave + 4 * i;
+      if (f >= 18 || g != 0) continue;
+      const int nn = f * 16 + li;                       // = tap*32 + c
+#pragma unroll
+      for (int e = 0; e < NCO; ++e) {
+        if (q.slab) out[e * 288 + nn] = accw[i][e];
+        else atomicAdd(out + e * 288 + nn, accw[i][e]);
+      }
+    }
+  }
+}
+
+// Column sums of a [rows][ld] fp32 slab (first `cols` columns) accumulated into dst, in a fixed
+// row order per column.
+__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, int cols, int ld, float* dst) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = threadIdx.x >> 6;
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (c < cols) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int r = part;
+    for (; r + 12 < rows; r += 16) {
+      a0 += src[(long)r * ld + c];
+      a1 += src[(long)(r + 4) * ld + c];
+      a2 += src[(long)(r + 8) * ld + c];
+      a3 += src[(long)(r + 12) * ld + c];
+    }
+    for (; r < rows; r += 4) a0 += src[(long)r * ld + c];
+    s = (a0 + a1) + (a2 + a3);
+  }
+  red[part][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (part == 0 && c < cols) dst[c] += (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+bool head_mfma_ok(const vae_head_args* a) {
+  return a->dtype == VAE_BF16 && a->c == HC && a->w == HW && a->h % ROWS == 0 && a->h > 0 && a->n > 0 &&
+         ((uintptr_t)a->x & 15) == 0 && ((uintptr_t)a->recon & 15) == 0 && ((uintptr_t)a->target & 15) == 0 &&
+         (a->x_xf.kind == VAE_X_BN_ACT || a->x_xf.kind == VAE_X_ACT || a->x_xf.kind == VAE_X_NONE);
+}
+
+HeadQ head_q(const vae_head_args* a) {
+  HeadQ q;
+  memset(&q, 0, sizeof(q));
+  q.n = a->n; q.h = a->h; q.samples = a->samples > 0 ? a->samples : 1; q.tiles = a->n * (a->h / ROWS);
+  q.x = static_cast<const __bf16*>(a->x); q.xf = a->x_xf;
+  if (q.xf.channels <= 0) q.xf.channels = a->c;
+  q.wt = a->wt; q.bias = a->bias; q.target = a->target; q.recon = a->recon; q.sse = a->sse;
+  q.coef = a->coef; q.grad_recon = a->grad_recon;
+  q.dx = static_cast<__bf16*>(a->dx); q.dgamma = a->dx_dgamma; q.dbeta = a->dx_dbeta;
+  q.sum_reps = a->sum_reps; q.sum_rstride = a->sum_rstride;
+  q.dw = a->dw; q.db = a->db;
+  return q;
+}
+
+}  // namespace
+
+// Entry points used by vae_misc.hip's C ABI for the bf16 MFMA path.
+int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
+  if (!head_mfma_ok(a)) return kHeadFallback;       // caller falls back to the VALU kernels
+  HeadQ q = head_q(a);
+  hipLaunchKernelGGL(head_fwd_mfma, dim3(q.tiles), dim3(256), 0, st, q);
+  return check_launch("head_fwd_mfma");
+}
+
+// data / filter: which halves of the backward to run.  The filter half writes per-block partials
+// into the caller's workspace (when large enough) and reduces them into dw/db in fixed order.
+int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStream_t st) {
+  if (!head_mfma_ok(a)) return kHeadFallback;
+  if (data && a->dx_epi.kind != VAE_X_BN_ACT) return kHeadFallback;   // the fused epilogue is BatchNorm+LReLU
+  HeadQ q = head_q(a);
+  q.data = data; q.filter = filter;
+  const int grid = q.tiles < 512 ? q.tiles : 512;
+  const long need = (long)grid * SLAB_COLS * 4;
+  float* ws = static_cast<float*>(a->workspace);
+  const bool slab = filter && ws && a->workspace_bytes >= need;
+  q.slab = slab ? ws : nullptr;
+  hipLaunchKernelGGL(head_bwd_mfma, dim3(grid), dim3(256), 0, st, q);
+  int rc = check_launch("head_bwd_mfma");
+  if (rc || !filter) return rc;
+  if (slab) {
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((NW + 63) / 64), dim3(256), 0, st, (const float*)ws, grid, NW,
+                       SLAB_COLS, a->dw);
+    if ((rc = check_launch("reduce_rows dw"))) return rc;
+    if (a->db) {
+      hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(256), 0, st, (const float*)(ws + NW), grid, NCO,
+                         SLAB_COLS, a->db);
+      rc = check_launch("reduce_rows db");
+    }
+  }
+  return rc;
+}
+
+}  // namespace vae

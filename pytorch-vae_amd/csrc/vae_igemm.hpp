@@ -41,21 +41,22 @@ constexpr int NTHREADS = 256;
 
 template <class T> constexpr int bk_of() { return sizeof(T) == 2 ? 64 : 32; }
 
-// Magic-number division for 0 <= n < 2^31 (round-up method; exact for every n in range).
+// Magic-number division for 0 <= n < 2^31, branch-free ("add" method):
+//   q = (umulhi(n, mul) + n) >> shr,  shr = ceil(log2 d),  mul = floor(2^32 (2^shr - d) / d) + 1
+// (d = 1: mul = 0, shr = 0).  umulhi(n, mul) < n, so the sum stays below 2^32.
 struct FastDiv {
   uint32_t d, mul, shr;
-  __device__ __forceinline__ uint32_t div(uint32_t n) const { return d == 1 ? n : (__umulhi(n, mul) >> shr); }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> shr; }
 };
 
 inline FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
   f.d = d < 1 ? 1 : d;
-  if (f.d == 1) { f.mul = 0; f.shr = 0; return f; }
   uint32_t l = 0;
-  while ((1u << l) < f.d) ++l;
-  const uint32_t p = 31 + l;
-  f.mul = (uint32_t)(((1ull << p) + f.d - 1) / f.d);
-  f.shr = p - 32;
+  while ((1ull << l) < f.d) ++l;
+  f.shr = l;
+  f.mul = (uint32_t)(((1ull << 32) * ((1ull << l) - f.d)) / f.d + 1);
+  if (f.d == 1) f.mul = 0;
   return f;
 }
 
@@ -74,6 +75,7 @@ struct GemmParams {
   //   A_CONVT: input tensor [gn][gh][gw][gc] -> output gho x gwo, phase grid gp x gq
   int gn, gh, gw, gc, gp, gq, gr, gs, gpad, gho, gwo;
   int ntap_h[2], ntap_w[2], tap0[2];   // phase ph: taps r = tap0[ph] + gs*t, t < ntap
+  int tap_d[2];                        // phase ph: input offset of tap 0, (ph + gpad - tap0[ph]) / gs
   FastDiv fd_gq, fd_gp, fd_gc, fd_gr, fd_ntw[2];
   // ---- epilogue
   void* out; int out_ld; int out_phase;      // out_phase: rows are phase-grid pixels
@@ -83,11 +85,14 @@ struct GemmParams {
   vae_xform epi_xf; float* dgamma; float* dbeta;
   float* bias_grad;
   float* dbc; int dbc_from_b;  // closed-form BN-followed bias gradient (wgrad, first block)
+  int sum_reps, sum_rstride; // replicas of the per-channel sums the epilogue accumulates
   const float* mulv; const float* eps; const float* kl_coef; float* dmulv; int samples, latent;
   float* slab;               // split-K partials [nphase][ksplit][M][N] (non-ACC epilogues)
   // ---- operand access (host-derived, see vae_launch.hpp)
   uint32_t a_bytes, b_bytes; // buffer-resource extents of the A / B tensors (and their aux)
   FastDiv fd_ach, fd_bch;    // transform channel counts of A / B
+  FastDiv fd_ech;            // epilogue transform channel count
+  uint32_t out_aux_bytes;    // extent of the out-shaped aux tensor (residual / stored pre-activation)
   unsigned long long* probe; // VAE_PROBE builds: per-block phase timestamps (diagnostics only)
 };
 
@@ -98,7 +103,8 @@ struct GemmParams {
 __device__ __forceinline__ void probe_write(unsigned long long* pr, const unsigned long long* clk,
                                            unsigned long long w0) {
   if (!pr || threadIdx.x != 0) return;
-  const unsigned long long slot = atomicAdd(pr, 1ull);
+  // one fixed slot per block (no shared counter: its atomics would serialise the blocks)
+  const unsigned long long slot = blockIdx.x + (unsigned long long)gridDim.x * (blockIdx.y + (unsigned long long)gridDim.y * blockIdx.z);
   if (slot >= pr[1]) return;                 // pr[1]: capacity in records
   unsigned long long* r = pr + 8 + slot * 8;
   r[0] = blockIdx.x | ((unsigned long long)blockIdx.y << 21) | ((unsigned long long)blockIdx.z << 42);
@@ -115,6 +121,7 @@ __device__ __forceinline__ void probe_write(unsigned long long* pr, const unsign
 // (runtime indexing of kernarg arrays makes the compiler copy the whole struct to scratch).
 struct PhaseInfo {
   int ph, pw, t0h, t0w, nth, ntw;
+  int dh, dw;      // input offset of tap 0: (ph + pad - t0h) / S, (pw + pad - t0w) / S
   FastDiv fdw;
 };
 
@@ -127,6 +134,8 @@ __device__ __forceinline__ PhaseInfo make_phase(const GemmParams& p, int phase) 
   q.nth = q.ph ? p.ntap_h[1] : p.ntap_h[0];
   q.ntw = q.pw ? p.ntap_w[1] : p.ntap_w[0];
   q.fdw = q.pw ? p.fd_ntw[1] : p.fd_ntw[0];
+  q.dh = q.ph ? p.tap_d[1] : p.tap_d[0];
+  q.dw = q.pw ? p.tap_d[1] : p.tap_d[0];
   return q;
 }
 
@@ -150,6 +159,20 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
     t.a[z] = 0.f; t.b[z] = 0.f;
     if (x.kind == VAE_X_BN_DY) t.c[z] = 0.f;
   }
+  if (x.table) {
+    // precomputed by vae_bn_finalize: one coalesced copy (all loads of a thread in flight)
+    const int C = x.channels;
+    const bool dy = x.kind == VAE_X_BN_DY;
+    for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
+      const float v0 = x.table[ch], v1 = x.table[C + ch];
+      const float v2 = (dy || epi) ? x.table[2 * C + ch] : 0.f;
+      const float v3 = (!dy && epi) ? x.table[3 * C + ch] : 0.f;
+      t.a[ch] = v0; t.b[ch] = v1;
+      if (dy) t.c[ch] = v2;
+      else if (epi) { t.p[ch] = v2; t.q[ch] = v3; }
+    }
+    return;
+  }
   for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
     float mean, invstd, var;
     bn_moments(x, ch, mean, invstd, var);
@@ -168,8 +191,8 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
     } else {
       const float inv_m = 1.0f / x.count;
       const float A = g * invstd;
-      const float mg = x.dbeta[ch] * inv_m;         // mean of g
-      const float mgx = x.dgamma[ch] * inv_m;       // mean of g*xhat
+      const float mg = rsum(x.dbeta, x, ch) * inv_m;         // mean of g
+      const float mgx = rsum(x.dgamma, x, ch) * inv_m;       // mean of g*xhat
       t.a[ch] = A;
       t.b[ch] = -A * invstd * mgx;
       t.c[ch] = -A * (mg - mean * invstd * mgx);
@@ -227,7 +250,7 @@ __device__ __forceinline__ Src<TIn> make_src(const void* ptr, uint32_t bytes, co
   Src<TIn> s;
   s.dy = xf.kind == VAE_X_BN_DY;
   s.x = make_rsrc(ptr, bytes);
-  s.y = make_rsrc(s.dy ? xf.aux : ptr, bytes);
+  s.y = make_rsrc(s.dy ? xf.aux : ptr, s.dy ? bytes : 0u);
   s.kind = xf.kind;
   s.C = xf.channels;
   s.zs = tab_pad(xf.channels);
@@ -256,19 +279,29 @@ __device__ __forceinline__ float raw_elem(const uint32_t* w, int e) {
   else return __uint_as_float(w[e] << 16);
 }
 
-template <class TIn, int NB>
+template <class TIn, int NB, bool DY>
 __device__ __forceinline__ void bload_pair(const Src<TIn>& s, uint32_t off, uint32_t* w, uint32_t* y) {
   bload<NB>(s.x, off, w);
-  if (s.dy) bload<NB>(s.y, off, y);
+  if constexpr (DY) bload<NB>(s.y, off, y);
 }
 
 // ------------------------------------------------------------------ V_K operand (row x 8 k)
-// Row state is computed once per thread slot; load() is called once per K-tile.
+// The k-decomposition of a K-tile is shared by all octets of a thread (they sit at the same k
+// offset of different rows): KTap is computed once per tile, then each octet needs only its
+// row's bounds check and base offset.
+struct KTap {
+  int r, s;        // conv modes: tap offset added to the row's (hi0, wi0)
+  int toff;        // element offset of (k) relative to the row base
+  int ch;          // transform channel of the octet's first element
+  int kin;         // k < kend
+};
+
 template <class TIn, int MODE, bool VEC>
 struct RowOperand {
   int valid;       // row in range
-  int n, hb, wb;   // A_CONV: image, top-left input coordinate; A_CONVT: image, ho, wo
-  int base;        // A_DENSE / B_NK: row offset (elements)
+  int hi0, wi0;    // conv modes: input coordinate of tap (0,0) for this output row
+  int base;        // element offset of (hi0, wi0, c = 0) (NHWC) / dense row offset
+  int n, hb, wb;   // non-packed A_CONV (NCHW image): image, top-left input coordinate
 
   __device__ __forceinline__ void init(const GemmParams& p, int row, int rows, int phase, int ld) {
     valid = row < rows;
@@ -278,15 +311,49 @@ struct RowOperand {
       const uint32_t t = p.fd_gq.div(row), oq = row - t * p.gq;
       const uint32_t nn = p.fd_gp.div(t), op = t - nn * p.gp;
       n = nn; hb = op * p.gs - p.gpad; wb = oq * p.gs - p.gpad;
+      hi0 = hb; wi0 = wb;
+      base = ((n * p.gh + hi0) * p.gw + wi0) * p.gc;
     } else if constexpr (MODE == A_CONVT) {
+      // phase (ph, pw) output pixel (hh*S+ph, ww*S+pw) takes input (hh + dh - th, ww + dw - tw)
+      // for its taps t = 0..ntap-1, dh = (ph + pad - t0h) / S (exact by construction)
       const PhaseInfo q = make_phase(p, phase);
       const uint32_t t = p.fd_gq.div(row), ww = row - t * p.gq;
       const uint32_t nn = p.fd_gp.div(t), hh = t - nn * p.gp;
-      n = nn; hb = hh * p.gs + q.ph; wb = ww * p.gs + q.pw;
+      n = nn;
+      hi0 = (int)hh + q.dh; wi0 = (int)ww + q.dw;
+      base = ((n * p.gh + hi0) * p.gw + wi0) * p.gc;
     }
   }
 
-  // element offset + in-range flag of k (per-element path, and the group's k0 in the packed one)
+  // decomposition of the octet's first k (shared by the thread's octets)
+  __device__ __forceinline__ static KTap tap(const GemmParams& p, const PhaseInfo& q, const FastDiv& fdc, int chans,
+                                            bool xf_bn, int k, int kend) {
+    KTap t;
+    t.kin = k < kend;
+    t.r = 0; t.s = 0; t.ch = 0;
+    if constexpr (MODE == A_DENSE || MODE == 100 + B_NK) {
+      t.toff = k;
+      if (xf_bn) t.ch = (int)(k - fdc.div(k) * chans);
+    } else if constexpr (MODE == A_CONV) {
+      const uint32_t tp = p.fd_gc.div(k);
+      const int c = k - tp * p.gc;
+      const uint32_t r = p.fd_gr.div(tp);
+      t.r = r; t.s = tp - r * p.gr;
+      t.toff = (t.r * p.gw + t.s) * p.gc + c;
+      t.ch = c;
+    } else {  // A_CONVT: k = (th, tw, c)
+      const uint32_t tt = p.fd_gc.div(k);
+      const int c = k - tt * p.gc;
+      const uint32_t th = q.fdw.div(tt);
+      const int tw = tt - th * q.ntw;
+      t.r = -(int)th; t.s = -tw;
+      t.toff = (t.r * p.gw + t.s) * p.gc + c;
+      t.ch = c;
+    }
+    return t;
+  }
+
+  // element offset + in-range flag of k (per-element path: NCHW image, unaligned channels)
   __device__ __forceinline__ int offset(const GemmParams& p, const PhaseInfo& q, int k, bool& ok) const {
     if constexpr (MODE == A_DENSE || MODE == 100 + B_NK) {
       ok = true;
@@ -306,28 +373,29 @@ struct RowOperand {
       const int c = k - tt * C;
       const uint32_t th = q.fdw.div(tt);
       const int tw = tt - th * q.ntw;
-      const int r = q.t0h + p.gs * (int)th, s = q.t0w + p.gs * (int)tw;
-      const int hi = (hb + p.gpad - r) / p.gs, wi = (wb + p.gpad - s) / p.gs;
+      const int hi = hi0 - (int)th, wi = wi0 - tw;
       ok = hi >= 0 && hi < p.gh && wi >= 0 && wi < p.gw;
       return ((n * p.gh + hi) * p.gw + wi) * C + c;
     }
   }
 
+  template <bool DY>
   __device__ __forceinline__ void load(const GemmParams& p, const Src<TIn>& s, const PhaseInfo& q, const FastDiv& fdc,
-                                       int k0, int Kp, Pend& g) const {
+                                       const KTap& t, int k0, int Kp, Pend& g) const {
     constexpr int E = sizeof(TIn);
     g.ones = 0u;
-    g.chb = s.kind >= VAE_X_BN_ACT ? (int)(k0 - fdc.div(k0) * s.C) : 0;
     if constexpr (VEC) {
       // whole group in or out (host: K % 8 == 0); out -> zeros and the zero-slot channel
-      bool ok;
-      const int idx = offset(p, q, k0, ok);
-      const bool gv = valid && ok && k0 < Kp;
-      g.chb = gv ? g.chb : s.zs;
-      const uint32_t off = gv ? (uint32_t)idx * E : kOOB;
-      bload_pair<TIn, 16>(s, off, g.w, g.y);
-      if constexpr (E == 4) bload_pair<TIn, 16>(s, off + 16, g.w + 4, g.y + 4);
+      bool ok = true;
+      if constexpr (MODE == A_CONV || MODE == A_CONVT)
+        ok = (uint32_t)(hi0 + t.r) < (uint32_t)p.gh && (uint32_t)(wi0 + t.s) < (uint32_t)p.gw;
+      const bool gv = valid && ok && t.kin;
+      g.chb = gv ? t.ch : s.zs;
+      const uint32_t off = gv ? (uint32_t)(base + t.toff) * E : kOOB;
+      bload_pair<TIn, 16, DY>(s, off, g.w, g.y);
+      if constexpr (E == 4) bload_pair<TIn, 16, DY>(s, off + 16, g.w + 4, g.y + 4);
     } else {
+      g.chb = s.kind >= VAE_X_BN_ACT ? (int)(k0 - fdc.div(k0) * s.C) : 0;
       uint32_t m = 0u;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -335,7 +403,7 @@ struct RowOperand {
         const int idx = offset(p, q, k0 + e, ok);
         ok = ok && valid && k0 + e < Kp;
         m |= (uint32_t)ok << e;
-        bload_pair<TIn, E>(s, ok ? (uint32_t)idx * E : kOOB, g.w + e, g.y + e);
+        bload_pair<TIn, E, DY>(s, ok ? (uint32_t)idx * E : kOOB, g.w + e, g.y + e);
       }
       g.m = m;
     }
@@ -403,6 +471,7 @@ struct ColOperand {
     }
   }
 
+  template <bool DY>
   __device__ __forceinline__ void load(const GemmParams& p, const Src<TIn>& s, const PhaseInfo& q, int k, int Kp,
                                        Pend& g) const {
     constexpr int E = sizeof(TIn);
@@ -420,8 +489,8 @@ struct ColOperand {
         if (t == 0) g.chb = ok ? ch0 : s.zs;
         else g.chb1 = ok ? ch0 : s.zs;
         const uint32_t off = ok ? (uint32_t)idx * E : kOOB;
-        if constexpr (E == 2) bload_pair<TIn, 8>(s, off, g.w + 2 * t, g.y + 2 * t);
-        else bload_pair<TIn, 16>(s, off, g.w + 4 * t, g.y + 4 * t);
+        if constexpr (E == 2) bload_pair<TIn, 8, DY>(s, off, g.w + 2 * t, g.y + 2 * t);
+        else bload_pair<TIn, 16, DY>(s, off, g.w + 4 * t, g.y + 4 * t);
       }
     } else {
 #pragma unroll
@@ -432,7 +501,7 @@ struct ColOperand {
           const int idx = offset(p, q, k + t, j, ok);
           ok = ok && k + t < Kp && ((rmask >> j) & 1u);
           m |= (uint32_t)ok << (4 * t + j);
-          bload_pair<TIn, E>(s, ok ? (uint32_t)idx * E : kOOB, g.w + 4 * t + j, g.y + 4 * t + j);
+          bload_pair<TIn, E, DY>(s, ok ? (uint32_t)idx * E : kOOB, g.w + 4 * t + j, g.y + 4 * t + j);
         }
     }
     g.m = m;
@@ -441,13 +510,13 @@ struct ColOperand {
 
 // Transform of a staged group (after its loads have landed) -> 8 floats in element order.
 // Masked elements become 0 after the transform (the transform of a zero pad is not zero).
-template <class TIn, int MODE, bool VM, bool VEC>
+template <class TIn, int MODE, bool VM, bool VEC, bool DY>
 __device__ __forceinline__ void finish(const GemmParams& p, const Src<TIn>& s, const Tab& t, const Pend& g,
                                        float (&v)[8]) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = raw_elem<TIn, VEC>(g.w, e);
-  if (s.kind == VAE_X_BN_ACT || s.kind == VAE_X_BN_DY) {
-    const bool dy = s.kind == VAE_X_BN_DY;
+  if (s.kind == VAE_X_BN_ACT || (DY && s.kind == VAE_X_BN_DY)) {
+    const bool dy = DY && s.kind == VAE_X_BN_DY;
     float a[8], b[8], c[8];
     if constexpr (VEC) {
       // channels are consecutive: V_K chb..chb+7, V_M chb..chb+3 (16-byte aligned table reads)
@@ -506,7 +575,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 tab4(const float* t, int ch) { return *reinterpret_cast<const f32x4*>(t + ch); }
 
-template <class T, class TIn>
+template <class T, class TIn, bool DY>
 __device__ __forceinline__ void store_vk(const Src<TIn>& s, const Tab& t, const Pend& g, T* dst) {
   if constexpr (sizeof(T) == sizeof(TIn)) {
     if (s.kind == VAE_X_NONE) {
@@ -528,7 +597,7 @@ __device__ __forceinline__ void store_vk(const Src<TIn>& s, const Tab& t, const 
       v[e] = lrelu(fmaf(v[e], a0[e], b0[e]), s.slope);
       v[e + 4] = lrelu(fmaf(v[e + 4], a1[e], b1[e]), s.slope);
     }
-  } else if (s.kind == VAE_X_BN_DY) {
+  } else if (DY && s.kind == VAE_X_BN_DY) {
     const f32x4 a0 = tab4(t.a, g.chb), a1 = tab4(t.a, g.chb + 4), b0 = tab4(t.b, g.chb), b1 = tab4(t.b, g.chb + 4);
     const f32x4 c0 = tab4(t.c, g.chb), c1 = tab4(t.c, g.chb + 4);
 #pragma unroll
@@ -541,7 +610,7 @@ __device__ __forceinline__ void store_vk(const Src<TIn>& s, const Tab& t, const 
 }
 
 // rows j = 0..3 of the group go to dst + j*ldk as the pair (k, k+1)
-template <class T, class TIn, int MODE>
+template <class T, class TIn, int MODE, bool DY>
 __device__ __forceinline__ void store_vm(const Src<TIn>& s, const Tab& t, const Pend& g, T* dst, int ldk) {
   if constexpr (sizeof(T) == 2 && sizeof(TIn) == 2) {
     if (s.kind == VAE_X_NONE && (MODE < 100 || g.ones == 0u)) {
@@ -567,7 +636,7 @@ __device__ __forceinline__ void store_vm(const Src<TIn>& s, const Tab& t, const 
       v[j] = lrelu(fmaf(v[j], a0[j], b0[j]), s.slope);
       v[4 + j] = lrelu(fmaf(v[4 + j], a1[j], b1[j]), s.slope);
     }
-  } else if (s.kind == VAE_X_BN_DY) {
+  } else if (DY && s.kind == VAE_X_BN_DY) {
     const f32x4 a0 = tab4(t.a, g.chb), a1 = tab4(t.a, g.chb1), b0 = tab4(t.b, g.chb), b1 = tab4(t.b, g.chb1);
     const f32x4 c0 = tab4(t.c, g.chb), c1 = tab4(t.c, g.chb1);
 #pragma unroll
@@ -587,59 +656,81 @@ __device__ __forceinline__ void store_vm(const Src<TIn>& s, const Tab& t, const 
 }
 
 // ------------------------------------------------------------------ epilogue helpers
-__device__ __forceinline__ long out_index(const GemmParams& p, int phase, int row, int col) {
+// Row part of the output offset of GEMM row `row` of phase `phase` (elements; the caller adds
+// the column).  Output tensors are < 2^31 elements (host-checked).
+__device__ __forceinline__ int out_row_base(const GemmParams& p, int phase, int row) {
   if (p.out_phase) {
     const int ph = phase >= p.gs ? 1 : 0, pw = phase - ph * p.gs;
     const uint32_t t = p.fd_gq.div(row), ww = row - t * p.gq;
     const uint32_t n = p.fd_gp.div(t), hh = t - n * p.gp;
     const int ho = hh * p.gs + ph, wo = ww * p.gs + pw;
-    return (((long)n * p.gho + ho) * p.gwo + wo) * p.out_ld + col;
+    return ((n * p.gho + ho) * p.gwo + wo) * p.out_ld;
   }
-  return (long)row * p.out_ld + col;
+  return row * p.out_ld;
 }
 
-// One output element of a non-accumulating epilogue.  s1/s2 collect the per-column sums.
+// One element of an out-shaped tensor through a buffer resource (out-of-range offset -> 0).
+template <class T>
+__device__ __forceinline__ float ld_elem(rsrc_t r, uint32_t off_bytes) {
+  if constexpr (sizeof(T) == 4) return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off_bytes, 0, 0));
+  else return __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, off_bytes, 0, 0) << 16);
+}
+
+// The out-shaped tensor an epilogue reads (E_STORE: residual, E_BNBWD: the stored pre-activation);
+// an empty resource when there is none.
+template <int EM>
+__device__ __forceinline__ rsrc_t epi_aux_rsrc(const GemmParams& p) {
+  const void* ptr = nullptr;
+  if constexpr (EM == E_STORE) ptr = p.residual;
+  if constexpr (EM == E_BNBWD) ptr = p.epi_xf.kind != VAE_X_NONE ? p.epi_xf.aux : nullptr;
+  return make_rsrc(ptr ? ptr : p.out, ptr ? p.out_aux_bytes : 0u);
+}
+
+// Epilogue of one element whose inputs (accumulator v, aux value, bias) are already in registers.
+// s1/s2 collect the per-column sums (BN statistics forward / BN-backward sums).
 template <class T, int EM>
-__device__ __forceinline__ void epi_elem(const GemmParams& p, const Tab& xe, int phase, int row,
-                                         int col, float v, float& s1, float& s2) {
-  if constexpr (EM == E_REPARAM) {
-    const int b = row / p.samples;
-    const float mu = p.mulv[(long)b * 2 * p.latent + col];
-    const float lv = p.mulv[(long)b * 2 * p.latent + p.latent + col];
-    const float ep = p.eps[(long)row * p.latent + col];
-    const float c = p.kl_coef ? p.kl_coef[row] : 0.f;
-    const float sd = expf(0.5f * lv);
-    atomicAdd(p.dmulv + (long)b * 2 * p.latent + col, v + c * mu);
-    atomicAdd(p.dmulv + (long)b * 2 * p.latent + p.latent + col, v * ep * 0.5f * sd + c * 0.5f * (expf(lv) - 1.f));
-  } else {
-    const long idx = out_index(p, phase, row, col);
-    if constexpr (EM == E_STORE) {
-      float y = v + (p.bias ? p.bias[col] : 0.f);
-      if (p.residual) {
-        float rv = ld_f(static_cast<const T*>(p.residual) + idx);
-        if (p.res_xf.kind == VAE_X_ACT) rv = lrelu(rv, p.res_xf.slope);
-        y += rv;
-      }
-      if (p.out_f32) static_cast<float*>(p.out)[idx] = y;
-      else static_cast<T*>(p.out)[idx] = cvt<T>(y);
-      s1 += v;
-      s2 += v * v;
-    } else {  // E_BNBWD
-      float g = v;
-      if (p.epi_xf.kind == VAE_X_BN_ACT) {
-        const int ch = col % p.epi_xf.channels;
-        const float yv = ld_f(static_cast<const T*>(p.epi_xf.aux) + idx);
-        const float z = fmaf(yv, xe.a[ch], xe.b[ch]);
-        g = z > 0.f ? v : v * p.epi_xf.slope;
-        s1 += g;
-        s2 += g * fmaf(yv, xe.p[ch], xe.q[ch]);
-      } else if (p.epi_xf.kind == VAE_X_ACT) {
-        const float yv = ld_f(static_cast<const T*>(p.epi_xf.aux) + idx);
-        g = yv > 0.f ? v : v * p.epi_xf.slope;
-      }
-      static_cast<T*>(p.out)[idx] = cvt<T>(g);
+__device__ __forceinline__ void epi_apply(const GemmParams& p, const Tab& xe, int col, int idx, float v, float aux,
+                                          float bias, float& s1, float& s2) {
+  if constexpr (EM == E_STORE) {
+    float y = v + bias;
+    if (p.residual) y += p.res_xf.kind == VAE_X_ACT ? lrelu(aux, p.res_xf.slope) : aux;
+    if (p.out_f32) static_cast<float*>(p.out)[idx] = y;
+    else static_cast<T*>(p.out)[idx] = cvt<T>(y);
+    s1 += v;
+    s2 += v * v;
+  } else if constexpr (EM == E_BNBWD) {
+    float g = v;
+    if (p.epi_xf.kind == VAE_X_BN_ACT) {
+      const int ch = (int)(col - p.fd_ech.div(col) * p.epi_xf.channels);
+      const float z = fmaf(aux, xe.a[ch], xe.b[ch]);
+      g = z > 0.f ? v : v * p.epi_xf.slope;
+      s1 += g;
+      s2 += g * fmaf(aux, xe.p[ch], xe.q[ch]);
+    } else if (p.epi_xf.kind == VAE_X_ACT) {
+      g = aux > 0.f ? v : v * p.epi_xf.slope;
     }
+    static_cast<T*>(p.out)[idx] = cvt<T>(g);
   }
+}
+
+// Reparameterization backward of one element (row = z row, col = latent index):
+//   dmu += dz + c*mu,  dlogvar += dz*eps*0.5*exp(0.5 lv) + c*0.5*(exp(lv) - 1)
+struct ReparamIn { float mu, lv, ep, c; };
+__device__ __forceinline__ ReparamIn reparam_load(const GemmParams& p, int row, int col, bool ok) {
+  ReparamIn r{0.f, 0.f, 0.f, 0.f};
+  if (!ok) return r;
+  const int b = row / p.samples;
+  r.mu = p.mulv[(long)b * 2 * p.latent + col];
+  r.lv = p.mulv[(long)b * 2 * p.latent + p.latent + col];
+  r.ep = p.eps[(long)row * p.latent + col];
+  r.c = p.kl_coef ? p.kl_coef[row] : 0.f;
+  return r;
+}
+__device__ __forceinline__ void reparam_apply(const GemmParams& p, int row, int col, float v, const ReparamIn& r) {
+  const int b = row / p.samples;
+  const float sd = expf(0.5f * r.lv);
+  atomicAdd(p.dmulv + (long)b * 2 * p.latent + col, v + r.c * r.mu);
+  atomicAdd(p.dmulv + (long)b * 2 * p.latent + p.latent + col, v * r.ep * 0.5f * sd + r.c * 0.5f * (expf(r.lv) - 1.f));
 }
 
 template <int EM>
@@ -650,28 +741,34 @@ __device__ __forceinline__ bool epi_wants_sums(const GemmParams& p) {
 }
 
 template <int EM>
-__device__ __forceinline__ void epi_flush_sums(const GemmParams& p, int col, float s1, float s2) {
-  float* g1 = (EM == E_STORE) ? p.sum : p.dbeta;
-  float* g2 = (EM == E_STORE) ? p.sumsq : p.dgamma;
-  const int ch = (EM == E_STORE) ? col : col % p.epi_xf.channels;
+__device__ __forceinline__ void epi_flush_sums(const GemmParams& p, int rep, int col, float s1, float s2) {
+  const long roff = p.sum_reps > 1 ? (long)(rep % p.sum_reps) * p.sum_rstride : 0;
+  float* g1 = ((EM == E_STORE) ? p.sum : p.dbeta) + roff;
+  float* g2 = ((EM == E_STORE) ? p.sumsq : p.dgamma) + roff;
+  const int ch = (EM == E_STORE) ? col : (int)(col - p.fd_ech.div(col) * p.epi_xf.channels);
   atomicAdd(g1 + ch, s1);
   atomicAdd(g2 + ch, s2);
 }
 
 // Closed-form bias gradient of a conv followed by train-mode BatchNorm:
-//   db = Σ dy = A·Σg + B·Σy + C·M per channel (A,B,C the BN-backward coefficients)
+//   db = Σ dy = A·Σg + B·Σy + C·M per channel (A,B,C the BN-backward coefficients);
+// also publishes the reduced BatchNorm affine gradients (dgamma_out / dbeta_out) when asked.
 __device__ __forceinline__ void closed_form_db(const vae_xform& x, float* db) {
   for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
     float mean, invstd, var;
     bn_moments(x, ch, mean, invstd, var);
     const float inv_m = 1.0f / x.count;
+    const float dgam = rsum(x.dgamma, x, ch), dbet = rsum(x.dbeta, x, ch);
+    if (x.dgamma_out) x.dgamma_out[ch] += dgam;
+    if (x.dbeta_out) x.dbeta_out[ch] += dbet;
+    if (!db) continue;
     const float A = x.gamma[ch] * invstd;
-    const float mgx = x.dgamma[ch] * inv_m;
-    const float mg = x.dbeta[ch] * inv_m;
+    const float mgx = dgam * inv_m;
+    const float mg = dbet * inv_m;
     const float B = -A * invstd * mgx;
     const float C = -A * (mg - mean * invstd * mgx);
-    const float sum_y = x.sum[ch] + x.count * (x.shift ? x.shift[ch] : 0.f);
-    db[ch] += A * x.dbeta[ch] + B * sum_y + C * x.count;
+    const float sum_y = rsum(x.sum, x, ch) + x.count * (x.shift ? x.shift[ch] : 0.f);
+    db[ch] += A * dbet + B * sum_y + C * x.count;
   }
 }
 
@@ -683,20 +780,35 @@ __host__ __device__ inline int table_floats(const GemmParams& p, bool epi_tbl) {
   return tab_floats(p.a_xf, false) + tab_floats(p.b_xf, false) + (epi_tbl ? tab_floats(p.epi_xf, true) : 0);
 }
 
+// Wave grid of a BM x BN block of 4 waves: thin N -> 4x1, thin M -> 1x4, else 2x2.
+template <int BM, int BN> struct WaveGrid {
+  static constexpr int WN = (BM <= 32 && BN <= 32) ? 2 : (BN <= 32 ? 1 : (BM <= 32 ? 4 : 2));
+  static constexpr int WM = 4 / WN;
+  static constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static_assert(TM >= 1 && TN >= 1, "wave tile below 16x16");
+};
+
+// Register stages of the K-loop prefetch ring: enough K-tiles in flight to cover the memory
+// latency, bounded by the staging registers one stage costs.
+template <int PER> constexpr int ring_stages() { return PER <= 2 ? 4 : (PER <= 4 ? 3 : 2); }
+
 // ------------------------------------------------------------------------------ kernel
 // T: LDS/MFMA type; TA: storage type of the A tensor (fp32 for the NCHW image / d[mu|logvar]);
 // TB: storage type of B (the gathered activation for B_GATHER, weights otherwise).
-template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM, bool VEC>
+// DYA / DYB: the A / B operand may carry a BN_DY transform (its aux tensor is loaded).
+template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM, bool VEC, bool DYA, bool DYB>
 __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   constexpr int BK = bk_of<T>();
   constexpr int LDK = BK + (sizeof(T) == 4 ? 4 : 8);        // padded LDS row (elements)
-  constexpr int WTM = BM / 2, WTN = BN / 2;                 // 2x2 waves
-  constexpr int TM = WTM / 16, TN = WTN / 16;
+  using WG = WaveGrid<BM, BN>;
+  constexpr int TM = WG::TM, TN = WG::TN;
+  constexpr int WTM = TM * 16, WTN = TN * 16;
   constexpr bool A_VM = a_is_vm<AM>();
   constexpr bool B_VM = b_is_vm<BMD>();
   constexpr int KO = BK / 8;                                // V_K octets per row
   constexpr int A_OCT = BM * BK / 8, B_OCT = BN * BK / 8;   // octets per tile
   constexpr int A_PER = (A_OCT + NTHREADS - 1) / NTHREADS, B_PER = (B_OCT + NTHREADS - 1) / NTHREADS;
+  constexpr int NS = ring_stages<A_PER + B_PER>();
   constexpr bool EPI_TBL = (EM == E_BNBWD);
   constexpr int A_MODE = AM;
   constexpr int B_MODE = 100 + BMD;
@@ -713,7 +825,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   PROBE_MARK(0);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WG::WN, wn = wave % WG::WN;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int phase = (p.nphase > 1) ? (int)(blockIdx.z / p.ksplit) : 0;
   const int ks = blockIdx.z - phase * p.ksplit;
@@ -728,6 +840,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   const int kper = (ktiles + p.ksplit - 1) / p.ksplit;
   const int kt0 = ks * kper;
   const int kt1 = min(ktiles, kt0 + kper);
+  const int kend = min(Kp, kt1 * BK);     // loads past this K (ring overrun, other slices) read 0
 
   // table views (carved in the order A, B, epilogue)
   Tab ta, tb, te;
@@ -769,39 +882,43 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Pend pa[A_PER], pb[B_PER];
-
-  auto load_tiles = [&](int kt) {
+  // K-tile loads of one ring slot: issued unconditionally (past kend they read zeros)
+  const bool a_bn = p.a_xf.kind >= VAE_X_BN_ACT, b_bn = p.b_xf.kind >= VAE_X_BN_ACT;
+  auto load_tiles = [&](int kt, Pend (&qa)[A_PER], Pend (&qb)[B_PER]) {
     const int kb = kt * BK;
+    const int kv = kb + (tid % KO) * 8;      // V_K operands: this thread's k (same for all its octets)
+    KTap tpa, tpb;
+    if constexpr (!A_VM && VEC) tpa = RowOperand<TA, A_MODE, VEC>::tap(p, pq, p.fd_ach, p.a_xf.channels, a_bn, kv, kend);
+    if constexpr (!B_VM && VEC) tpb = RowOperand<TB, B_MODE, VEC>::tap(p, pq, p.fd_bch, p.b_xf.channels, b_bn, kv, kend);
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (A_OCT % NTHREADS == 0 || o < A_OCT) {
-        if constexpr (!A_VM) ars[i].load(p, sa, pq, p.fd_ach, kb + (o % KO) * 8, Kp, pa[i]);
-        else acs[i].load(p, sa, pq, kb + 2 * (o / (BM / 4)), Kp, pa[i]);
+        if constexpr (!A_VM) ars[i].template load<DYA>(p, sa, pq, p.fd_ach, tpa, kv, kend, qa[i]);
+        else acs[i].template load<DYA>(p, sa, pq, kb + 2 * (o / (BM / 4)), kend, qa[i]);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (B_OCT % NTHREADS == 0 || o < B_OCT) {
-        if constexpr (!B_VM) brs[i].load(p, sb, pq, p.fd_bch, kb + (o % KO) * 8, Kp, pb[i]);
-        else bcs[i].load(p, sb, pq, kb + 2 * (o / (BN / 4)), Kp, pb[i]);
+        if constexpr (!B_VM) brs[i].template load<DYB>(p, sb, pq, p.fd_bch, tpb, kv, kend, qb[i]);
+        else bcs[i].template load<DYB>(p, sb, pq, kb + 2 * (o / (BN / 4)), kend, qb[i]);
       }
     }
   };
-  auto store_tiles = [&](int buf) {
+  auto store_tiles = [&](int buf, const Pend (&qa)[A_PER], const Pend (&qb)[B_PER]) {
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (A_OCT % NTHREADS == 0 || o < A_OCT) {
         if constexpr (VEC) {
-          if constexpr (!A_VM) store_vk<T, TA>(sa, ta, pa[i], As[buf] + (o / KO) * LDK + (o % KO) * 8);
-          else store_vm<T, TA, A_MODE>(sa, ta, pa[i], As[buf] + (o % (BM / 4)) * 4 * LDK + 2 * (o / (BM / 4)), LDK);
+          if constexpr (!A_VM) store_vk<T, TA, DYA>(sa, ta, qa[i], As[buf] + (o / KO) * LDK + (o % KO) * 8);
+          else store_vm<T, TA, A_MODE, DYA>(sa, ta, qa[i], As[buf] + (o % (BM / 4)) * 4 * LDK + 2 * (o / (BM / 4)), LDK);
           continue;
         }
         float v[8];
-        finish<TA, A_MODE, A_VM, VEC>(p, sa, ta, pa[i], v);
+        finish<TA, A_MODE, A_VM, VEC, DYA>(p, sa, ta, qa[i], v);
         if constexpr (!A_VM) {
           st8(As[buf] + (o / KO) * LDK + (o % KO) * 8, v);
         } else {
@@ -816,12 +933,12 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
       const int o = tid + i * NTHREADS;
       if (B_OCT % NTHREADS == 0 || o < B_OCT) {
         if constexpr (VEC) {
-          if constexpr (!B_VM) store_vk<T, TB>(sb, tb, pb[i], Bs[buf] + (o / KO) * LDK + (o % KO) * 8);
-          else store_vm<T, TB, B_MODE>(sb, tb, pb[i], Bs[buf] + (o % (BN / 4)) * 4 * LDK + 2 * (o / (BN / 4)), LDK);
+          if constexpr (!B_VM) store_vk<T, TB, DYB>(sb, tb, qb[i], Bs[buf] + (o / KO) * LDK + (o % KO) * 8);
+          else store_vm<T, TB, B_MODE, DYB>(sb, tb, qb[i], Bs[buf] + (o % (BN / 4)) * 4 * LDK + 2 * (o / (BN / 4)), LDK);
           continue;
         }
         float v[8];
-        finish<TB, B_MODE, B_VM, VEC>(p, sb, tb, pb[i], v);
+        finish<TB, B_MODE, B_VM, VEC, DYB>(p, sb, tb, qb[i], v);
         if constexpr (!B_VM) {
           st8(Bs[buf] + (o / KO) * LDK + (o % KO) * 8, v);
         } else {
@@ -876,28 +993,35 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     }
   };
 
-  // prologue: first tile's global loads go out before the table fill (they overlap it)
-  if (kt0 < kt1) load_tiles(kt0);
+  // prologue: the ring's first NS K-tiles go out before the table fill (they overlap it)
+  Pend pa[NS][A_PER], pb[NS][B_PER];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) load_tiles(kt0 + u, pa[u], pb[u]);
   tab_fill(p.a_xf, ta, false, first_block);
   tab_fill(p.b_xf, tb, false, false);
   if constexpr (EPI_TBL) tab_fill(p.epi_xf, te, true, false);
   for (int i = tid; i < BN; i += NTHREADS) { red1[i] = 0.f; red2[i] = 0.f; }
   if constexpr (EM == E_ACC) {
-    if (first_block && p.dbc) closed_form_db(p.dbc_from_b ? p.b_xf : p.a_xf, p.dbc);
+    const vae_xform& dyx = p.dbc_from_b ? p.b_xf : p.a_xf;
+    if (first_block && dyx.kind == VAE_X_BN_DY && (p.dbc || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.dbc);
   }
   __syncthreads();   // tables ready
   PROBE_MARK(1);
-  if (kt0 < kt1) {
-    store_tiles(0);
-    __syncthreads();
-    int buf = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const bool more = kt + 1 < kt1;
-      if (more) load_tiles(kt + 1);       // raw loads in flight during the MFMAs below
-      compute(buf);
-      if (more) store_tiles(buf ^ 1);     // transform + LDS write; other buffer, read 1 iter ago
-      __syncthreads();
-      buf ^= 1;
+
+  // main loop: K-tile kt is transformed into LDS buffer (kt - kt0) & 1 from ring slot
+  // (kt - kt0) % NS, whose registers are then refilled with tile kt + NS.  One barrier per
+  // K-tile: a buffer is rewritten two tiles after the compute that read it.
+  for (int kb = kt0; kb < kt1; kb += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const int kt = kb + u;
+      if (kt < kt1) {
+        const int buf = (kt - kt0) & 1;
+        store_tiles(buf, pa[u], pb[u]);
+        __syncthreads();
+        load_tiles(kt + NS, pa[u], pb[u]);
+        compute(buf);
+      }
     }
   }
 
@@ -911,16 +1035,18 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
 
   // ------------------------------------------------------------------------ epilogue
   // lane holds rows 4*(lane>>4)+e, column lane&15 of each 16x16 tile
+  const int rowq = m0 + wm * WTM + 4 * (lane >> 4);
+  const int colq = n0 + wn * WTN + (lane & 15);
   if constexpr (EM == E_ACC) {
     float* out = static_cast<float*>(p.out);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * WTN + j * 16 + (lane & 15);
+        const int col = colq + j * 16;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
+          const int row = rowq + i * 16 + e;
           if (row >= p.M || col >= p.N) continue;
           if (col == p.ones_col) {
             if (p.bias_grad) atomicAdd(p.bias_grad + row, acc[i][j][e]);
@@ -938,82 +1064,191 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int col = n0 + wn * WTN + j * 16 + (lane & 15);
+          const int col = colq + j * 16;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
+            const int row = rowq + i * 16 + e;
             if (row < p.M && col < p.N) sl[(long)row * p.N + col] = acc[i][j][e];
           }
         }
       return;
     }
-    const bool want_sums = epi_wants_sums<EM>(p);
+    if constexpr (EM == E_REPARAM) {
+      ReparamIn rin[TM][TN][4];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * WTN + j * 16 + (lane & 15);
-      const bool col_ok = col < p.N;
-      float s1 = 0.f, s2 = 0.f;
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            rin[i][j][e] = reparam_load(p, rowq + i * 16 + e, colq + j * 16, rowq + i * 16 + e < p.M && colq + j * 16 < p.N);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (rowq + i * 16 + e < p.M && colq + j * 16 < p.N)
+              reparam_apply(p, rowq + i * 16 + e, colq + j * 16, acc[i][j][e], rin[i][j][e]);
+      return;
+    } else {
+      // pass 1: every load the epilogue needs (aux tensor, bias), before any store
+      const rsrc_t raux = epi_aux_rsrc<EM>(p);
+      int obase[TM][4];
+      float aux[TM][TN][4], bias[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bias[j] = (EM == E_STORE && p.bias && colq + j * 16 < p.N) ? p.bias[colq + j * 16] : 0.f;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int row = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
-          if (row >= p.M || !col_ok) continue;
-          epi_elem<T, EM>(p, te, phase, row, col, acc[i][j][e], s1, s2);
+          const int row = rowq + i * 16 + e;
+          obase[i][e] = out_row_base(p, phase, row < p.M ? row : 0);
         }
-      if (want_sums) {
-        s1 += __shfl_xor(s1, 16);
-        s1 += __shfl_xor(s1, 32);
-        s2 += __shfl_xor(s2, 16);
-        s2 += __shfl_xor(s2, 32);
-        if (lane < 16 && col_ok) {
-          atomicAdd(&red1[wn * WTN + j * 16 + lane], s1);
-          atomicAdd(&red2[wn * WTN + j * 16 + lane], s2);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool ok = rowq + i * 16 + e < p.M && colq + j * 16 < p.N;
+            aux[i][j][e] = ld_elem<T>(raux, ok ? (uint32_t)(obase[i][e] + colq + j * 16) * (uint32_t)sizeof(T) : kOOB);
+          }
+      // pass 2: apply, store, per-column sums
+      const bool want_sums = epi_wants_sums<EM>(p);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = colq + j * 16;
+        const bool col_ok = col < p.N;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = rowq + i * 16 + e;
+            if (row >= p.M || !col_ok) continue;
+            epi_apply<T, EM>(p, te, col, obase[i][e] + col, acc[i][j][e], aux[i][j][e], bias[j], s1, s2);
+          }
+        if (want_sums) {
+          s1 += __shfl_xor(s1, 16);
+          s1 += __shfl_xor(s1, 32);
+          s2 += __shfl_xor(s2, 16);
+          s2 += __shfl_xor(s2, 32);
+          if (lane < 16 && col_ok) {
+            atomicAdd(&red1[wn * WTN + j * 16 + lane], s1);
+            atomicAdd(&red2[wn * WTN + j * 16 + lane], s2);
+          }
         }
       }
-    }
-    if (want_sums) {
-      __syncthreads();
-      for (int c = tid; c < BN; c += NTHREADS)
-        if (n0 + c < p.N) epi_flush_sums<EM>(p, n0 + c, red1[c], red2[c]);
+      if (want_sums) {
+        __syncthreads();
+        for (int c = tid; c < BN; c += NTHREADS)
+          if (n0 + c < p.N) epi_flush_sums<EM>(p, blockIdx.x + blockIdx.z * gridDim.x, n0 + c, red1[c], red2[c]);
+      }
     }
   }
 }
 
-// Split-K finalize: sums the K-slices' slabs in slice order and runs the epilogue.
-// grid: (ceil(M*nphase / 64), ceil(N / 64)); block 256 = 4 row groups x 64 columns.
-template <class T, int EM>
+// Split-K finalize: sums the K-slices' slabs in slice order (deterministic) and runs the
+// epilogue.  Block = 16 column quads x 16 row lanes, FIN_RPT rows per thread; every slab and
+// aux load of a thread is issued before the first one is consumed.
+constexpr int FIN_RPT = 2;
+constexpr int FIN_ROWS = 16 * FIN_RPT;
+template <class T, int EM, bool V4>
 __global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
   constexpr bool EPI_TBL = (EM == E_BNBWD);
-  __shared__ float r1[4][64], r2[4][64];
+  __shared__ float r1[16][64], r2[16][64];
   extern __shared__ float tabs[];
   const int ce = tab_stride(p.epi_xf.channels);
   const Tab te{tabs, tabs + ce, nullptr, tabs + 2 * ce, tabs + 3 * ce};
   if constexpr (EPI_TBL) tab_fill(p.epi_xf, te, true, false);
-  __syncthreads();
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int col = blockIdx.y * 64 + cl;
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int col0 = blockIdx.y * 64 + cq * 4;
   const long rows_total = (long)p.M * p.nphase;
-  float s1 = 0.f, s2 = 0.f;
-  if (col < p.N) {
-    for (int rr = rg; rr < 64; rr += 4) {
-      const long grow = (long)blockIdx.x * 64 + rr;
-      if (grow >= rows_total) break;
-      const int phase = (int)(grow / p.M);
-      const int row = (int)(grow - (long)phase * p.M);
-      const float* sl = p.slab + ((long)phase * p.ksplit * p.M + row) * p.N + col;
-      float v = 0.f;
-      for (int s = 0; s < p.ksplit; ++s) v += sl[(long)s * p.M * p.N];
-      epi_elem<T, EM>(p, te, phase, row, col, v, s1, s2);
-    }
+  const long slab_elems = rows_total * p.ksplit * p.N;
+  const rsrc_t rs = make_rsrc(p.slab, (uint32_t)(slab_elems * 4));
+  int phase[FIN_RPT], row[FIN_RPT];
+  bool rok[FIN_RPT];
+  float v[FIN_RPT][4];
+#pragma unroll
+  for (int r = 0; r < FIN_RPT; ++r) {
+    const long grow = (long)blockIdx.x * FIN_ROWS + rl + 16 * r;
+    rok[r] = grow < rows_total;
+    phase[r] = rok[r] ? (int)(grow / p.M) : 0;
+    row[r] = rok[r] ? (int)(grow - (long)phase[r] * p.M) : 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[r][c] = 0.f;
   }
-  if (epi_wants_sums<EM>(p)) {
-    r1[rg][cl] = s1;
-    r2[rg][cl] = s2;
-    __syncthreads();
-    if (rg == 0 && col < p.N)
-      epi_flush_sums<EM>(p, col, r1[0][cl] + r1[1][cl] + r1[2][cl] + r1[3][cl],
-                         r2[0][cl] + r2[1][cl] + r2[2][cl] + r2[3][cl]);
+  // slab sums, 4 slices per round (all loads of a round in flight together)
+  for (int s0 = 0; s0 < p.ksplit; s0 += 4) {
+    float t[4][FIN_RPT][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < FIN_RPT; ++r) {
+        const bool ok = rok[r] && s0 + u < p.ksplit;
+        const uint32_t base = (uint32_t)((((long)phase[r] * p.ksplit + s0 + u) * p.M + row[r]) * p.N + col0);
+        if constexpr (V4) {
+          const auto q = __builtin_amdgcn_raw_buffer_load_b128(rs, ok && col0 < p.N ? base * 4u : kOOB, 0, 0);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) t[u][r][c] = __uint_as_float(q[c]);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            t[u][r][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ok && col0 + c < p.N ? (base + c) * 4u : kOOB, 0, 0));
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < FIN_RPT; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[r][c] += t[u][r][c];
+  }
+  __syncthreads();   // epilogue table ready
+  if constexpr (EM == E_REPARAM) {
+    ReparamIn rin[FIN_RPT][4];
+#pragma unroll
+    for (int r = 0; r < FIN_RPT; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) rin[r][c] = reparam_load(p, row[r], col0 + c, rok[r] && col0 + c < p.N);
+#pragma unroll
+    for (int r = 0; r < FIN_RPT; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (rok[r] && col0 + c < p.N) reparam_apply(p, row[r], col0 + c, v[r][c], rin[r][c]);
+    return;
+  } else {
+    const rsrc_t raux = epi_aux_rsrc<EM>(p);
+    int obase[FIN_RPT];
+    float aux[FIN_RPT][4], bias[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) bias[c] = (EM == E_STORE && p.bias && col0 + c < p.N) ? p.bias[col0 + c] : 0.f;
+#pragma unroll
+    for (int r = 0; r < FIN_RPT; ++r) {
+      obase[r] = out_row_base(p, phase[r], row[r]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        aux[r][c] = ld_elem<T>(raux, rok[r] && col0 + c < p.N ? (uint32_t)(obase[r] + col0 + c) * (uint32_t)sizeof(T) : kOOB);
+    }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < FIN_RPT; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (rok[r] && col0 + c < p.N) epi_apply<T, EM>(p, te, col0 + c, obase[r] + col0 + c, v[r][c], aux[r][c], bias[c], s1[c], s2[c]);
+    if (epi_wants_sums<EM>(p)) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) { r1[rl][cq * 4 + c] = s1[c]; r2[rl][cq * 4 + c] = s2[c]; }
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        const int col = blockIdx.y * 64 + threadIdx.x;
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { a += r1[i][threadIdx.x]; b += r2[i][threadIdx.x]; }
+        if (col < p.N) epi_flush_sums<EM>(p, blockIdx.x, col, a, b);
+      }
+    }
   }
 }
 

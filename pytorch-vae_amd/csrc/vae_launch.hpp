@@ -57,6 +57,7 @@ inline bool make_taps(GemmParams& p, int S, int R, int P) {
     if (n < 1 || n > 4) return false;
     p.tap0[ph] = first;
     p.ntap_h[ph] = n; p.ntap_w[ph] = n;
+    p.tap_d[ph] = (ph + P - first) / S;
   }
   return true;
 }
@@ -124,21 +125,28 @@ inline void finish_divs(GemmParams& p) {
   p.fd_ntw[1] = make_fastdiv(p.ntap_w[1] > 0 ? p.ntap_w[1] : 1);
   p.fd_ach = make_fastdiv(p.a_xf.channels > 0 ? p.a_xf.channels : 1);
   p.fd_bch = make_fastdiv(p.b_xf.channels > 0 ? p.b_xf.channels : 1);
+  p.fd_ech = make_fastdiv(p.epi_xf.channels > 0 ? p.epi_xf.channels : 1);
 }
 
 struct Tile { int bm, bn; };
 
-// Largest tile that still fills the CUs; thin N prefers the 128x32 tile.
+inline long tile_blocks(long M, long N, int nphase, Tile t) {
+  return ((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn) * nphase;
+}
+
+// Tile (4 waves) for the grid: the largest one that still puts ~4 blocks on every CU, so that
+// several waves per SIMD overlap each other's load/transform/barrier stalls; the split-K planner
+// below raises the block count further when K is long.
+constexpr int kTileBlocks = 4 * kCUs;
 inline Tile pick_tile(long M, long N, int nphase) {
-  const Tile cands_thin[] = {{128, 32}, {64, 64}, {32, 64}, {32, 32}};
-  const Tile cands[] = {{64, 64}, {32, 64}, {32, 32}};
-  const Tile* c = N <= 32 ? cands_thin : cands;
-  const int nc = N <= 32 ? 4 : 3;
-  for (int i = 0; i < nc; ++i) {
-    const long blocks = ((M + c[i].bm - 1) / c[i].bm) * ((N + c[i].bn - 1) / c[i].bn) * nphase;
-    if (blocks >= kCUs) return c[i];
-  }
-  return {32, 32};
+  const Tile wide[] = {{64, 64}, {64, 32}, {32, 64}, {32, 32}};
+  const Tile thin_n[] = {{128, 32}, {64, 32}, {32, 32}};
+  const Tile thin_m[] = {{32, 128}, {32, 64}, {32, 32}};
+  const Tile* c = N <= 32 ? thin_n : (M <= 32 ? thin_m : wide);
+  const int nc = N <= 32 ? 3 : (M <= 32 ? 3 : 4);
+  for (int i = 0; i < nc; ++i)
+    if (tile_blocks(M, N, nphase, c[i]) >= kTileBlocks) return c[i];
+  return c[nc - 1];
 }
 
 // K-slices: enough blocks to cover the CUs twice, >= 4 K-tiles per slice, and (for slab
@@ -158,41 +166,61 @@ inline int pick_split(long blocks, int ktiles, bool slab, long slab_elems_per_sp
 template <class T, int EM>
 inline int launch_finalize(const GemmParams& p, hipStream_t st) {
   const long rows = (long)p.M * p.nphase;
-  const dim3 grid((unsigned)((rows + 63) / 64), (unsigned)((p.N + 63) / 64));
+  const dim3 grid((unsigned)((rows + FIN_ROWS - 1) / FIN_ROWS), (unsigned)((p.N + 63) / 64));
   const size_t lds = EM == E_BNBWD ? (size_t)tab_floats(p.epi_xf, true) * 4 : 0;
-  hipLaunchKernelGGL((igemm_finalize<T, EM>), grid, dim3(NTHREADS), lds, st, p);
+  if (p.N % 4 == 0) hipLaunchKernelGGL((igemm_finalize<T, EM, true>), grid, dim3(NTHREADS), lds, st, p);
+  else hipLaunchKernelGGL((igemm_finalize<T, EM, false>), grid, dim3(NTHREADS), lds, st, p);
   return check_launch("igemm_finalize");
 }
 
-template <class T, class TA, class TB, int AM, int BMD, int EM, bool VEC>
+#define VAE_TILE_CASE(BM_, BN_) \
+  if (t.bm == BM_ && t.bn == BN_) { \
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VEC, DYA, DYB>), grid, block, lds, st, p); \
+    return; \
+  }
+
+template <class T, class TA, class TB, int AM, int BMD, int EM, bool VEC, bool DYA, bool DYB>
 inline void launch_shape(const GemmParams& p, Tile t, hipStream_t st) {
   const dim3 block(NTHREADS);
   const dim3 grid((p.M + t.bm - 1) / t.bm, (p.N + t.bn - 1) / t.bn, p.nphase * p.ksplit);
   const size_t lds = (size_t)table_floats(p, EM == E_BNBWD) * 4;
-  if (t.bm == 64 && t.bn == 64)
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 64, 64, AM, BMD, EM, VEC>), grid, block, lds, st, p);
-  else if (t.bm == 128 && t.bn == 32)
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 128, 32, AM, BMD, EM, VEC>), grid, block, lds, st, p);
-  else if (t.bm == 32 && t.bn == 64)
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 64, AM, BMD, EM, VEC>), grid, block, lds, st, p);
-  else
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, 32, 32, AM, BMD, EM, VEC>), grid, block, lds, st, p);
+  VAE_TILE_CASE(64, 64)
+  VAE_TILE_CASE(128, 32)
+  VAE_TILE_CASE(32, 128)
+  VAE_TILE_CASE(64, 32)
+  VAE_TILE_CASE(32, 64)
+  VAE_TILE_CASE(32, 32)
+}
+#undef VAE_TILE_CASE
+
+// Output-tensor extent (elements) the epilogue's aux operand spans: rows of the phase grid or
+// plain rows, times the row pitch.
+inline long out_elems(const GemmParams& p) {
+  if (p.out_phase) return (long)p.gn * p.gho * p.gwo * p.out_ld;
+  return (long)p.M * p.out_ld;
 }
 
-template <class T, class TA, class TB, int AM, int BMD, int EM>
+template <class T, class TA, class TB, int AM, int BMD, int EM, bool DYA, bool DYB>
 inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
   const long ab = a_elems<AM>(p) * (long)sizeof(TA), bb = b_elems<BMD>(p) * (long)sizeof(TB);
   if (ab <= 0 || bb <= 0 || ab >= (1l << 31) || bb >= (1l << 31))
     return fail(VAE_E_UNSUPPORTED, "igemm: operand of %ld / %ld bytes (buffer addressing needs < 2 GiB)", ab, bb);
   p.a_bytes = (uint32_t)ab;
   p.b_bytes = (uint32_t)bb;
+  if (EM != E_ACC && EM != E_REPARAM) {
+    const long ob = out_elems(p) * (long)(p.out_f32 ? 4 : sizeof(T));
+    if (ob >= (1l << 31)) return fail(VAE_E_UNSUPPORTED, "igemm: output of %ld bytes (needs < 2 GiB)", ob);
+    p.out_aux_bytes = (uint32_t)(out_elems(p) * (long)sizeof(T));
+  }
+  if ((!DYA && p.a_xf.kind == VAE_X_BN_DY) || (!DYB && p.b_xf.kind == VAE_X_BN_DY))
+    return fail(VAE_E_UNSUPPORTED, "igemm: BN_DY transform on an operand this op does not support");
 #ifdef VAE_PROBE
   p.probe = vae_probe_buffer();
 #endif
   const bool vec = operand_vec<AM>(p, p.a_ptr, p.a_xf, (int)sizeof(TA)) &&
                    operand_vec<100 + BMD>(p, p.b_ptr, p.b_xf, (int)sizeof(TB));
-  if (vec) launch_shape<T, TA, TB, AM, BMD, EM, true>(p, t, st);
-  else launch_shape<T, TA, TB, AM, BMD, EM, false>(p, t, st);
+  if (vec) launch_shape<T, TA, TB, AM, BMD, EM, true, DYA, DYB>(p, t, st);
+  else launch_shape<T, TA, TB, AM, BMD, EM, false, DYA, DYB>(p, t, st);
   int rc = check_launch("igemm");
   if (rc) return rc;
   if (EM != E_ACC && p.slab) return launch_finalize<T, EM>(p, st);
@@ -201,7 +229,7 @@ inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
 
 // Plan tile + split-K, then launch.  A_F32 / B_F32: instantiate the bf16 variant whose A / B
 // tensor is fp32 (the NCHW image, d[mu|logvar]).
-template <int AM, int BMD, int EM, bool A_F32 = false, bool B_F32 = false>
+template <int AM, int BMD, int EM, bool DYA, bool DYB, bool A_F32 = false, bool B_F32 = false>
 inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req, void* ws, long ws_bytes,
                   hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return VAE_OK;
@@ -225,16 +253,16 @@ inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req
     else p.slab = static_cast<float*>(ws);
   }
   p.ksplit = split < 1 ? 1 : split;
-  if (dtype == VAE_F32) return launch_tiled<float, float, float, AM, BMD, EM>(p, t, st);
+  if (dtype == VAE_F32) return launch_tiled<float, float, float, AM, BMD, EM, DYA, DYB>(p, t, st);
   if (dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "dtype %d", dtype);
   if constexpr (A_F32) {
-    if (a_f32) return launch_tiled<__bf16, float, __bf16, AM, BMD, EM>(p, t, st);
+    if (a_f32) return launch_tiled<__bf16, float, __bf16, AM, BMD, EM, DYA, DYB>(p, t, st);
   }
   if constexpr (B_F32) {
-    if (b_f32) return launch_tiled<__bf16, __bf16, float, AM, BMD, EM>(p, t, st);
+    if (b_f32) return launch_tiled<__bf16, __bf16, float, AM, BMD, EM, DYA, DYB>(p, t, st);
   }
   if (a_f32 || b_f32) return fail(VAE_E_UNSUPPORTED, "fp32 operand not instantiated for this op");
-  return launch_tiled<__bf16, __bf16, __bf16, AM, BMD, EM>(p, t, st);
+  return launch_tiled<__bf16, __bf16, __bf16, AM, BMD, EM, DYA, DYB>(p, t, st);
 }
 
 // Column sums of a plain [rows][C] tensor (bias gradient of a layer whose dy is stored as is)

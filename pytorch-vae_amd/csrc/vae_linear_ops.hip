@@ -12,7 +12,7 @@ extern "C" int vae_linear_fwd(const vae_linear_args* a, void* stream) {
   p.a_ptr = a->x; p.a_ld = a->k; p.a_xf = sanitize(a->x_xf);
   p.b_ptr = a->wt; p.b_ld = a->k;
   p.out = a->y; p.out_ld = a->n; p.bias = a->bias; p.out_f32 = a->y_f32;
-  return launch<A_DENSE, B_NK, E_STORE>(a->dtype, false, false, p, 0, a->workspace, a->workspace_bytes,
+  return launch<A_DENSE, B_NK, E_STORE, false, false>(a->dtype, false, false, p, 0, a->workspace, a->workspace_bytes,
                                         (hipStream_t)stream);
 }
 
@@ -30,13 +30,14 @@ extern "C" int vae_linear_bwd_data(const vae_linear_args* a, void* stream) {
     if (!a->eps || !a->dmulv || a->samples <= 0) return fail(VAE_E_BADARG, "linear_bwd_data: reparam args");
     p.mulv = a->mulv; p.eps = a->eps; p.kl_coef = a->kl_coef; p.dmulv = a->dmulv;
     p.samples = a->samples; p.latent = a->k;
-    return launch<A_DENSE, B_KN, E_REPARAM, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace,
+    return launch<A_DENSE, B_KN, E_REPARAM, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace,
                                                   a->workspace_bytes, (hipStream_t)stream);
   }
   if (!a->dx) return fail(VAE_E_BADARG, "linear_bwd_data: dx");
   p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+  p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "linear_bwd_data: dgamma/dbeta");
-  return launch<A_DENSE, B_KN, E_BNBWD, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace, a->workspace_bytes,
+  return launch<A_DENSE, B_KN, E_BNBWD, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace, a->workspace_bytes,
                                               (hipStream_t)stream);
 }
 
@@ -50,5 +51,5 @@ extern "C" int vae_linear_bwd_filter(const vae_linear_args* a, void* stream) {
   p.a_ptr = a->dy; p.a_ld = a->n;
   p.b_ptr = a->x; p.b_ld = a->k; p.b_xf = sanitize(a->x_xf);
   p.out = a->dw; p.out_ld = a->k;
-  return launch<A_KM, B_KN, E_ACC, true>(a->dtype, a->dy_f32 != 0, false, p, 0, nullptr, 0, (hipStream_t)stream);
+  return launch<A_KM, B_KN, E_ACC, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, nullptr, 0, (hipStream_t)stream);
 }

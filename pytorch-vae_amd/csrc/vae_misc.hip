@@ -44,6 +44,7 @@ struct HeadP {
   const float* wt; const float* bias; const float* target;
   float* recon; float* sse; const float* coef;
   void* dx; vae_xform epi; float* dgamma; float* dbeta;
+  int sum_reps, sum_rstride;
   float* dw; float* db;
   const float* grad_recon;
 };
@@ -59,6 +60,14 @@ __device__ __forceinline__ float act_of(const vae_xform& xf, const float* ta, co
 __device__ void head_coefs(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq,
                            bool update_running = false) {
   if (xf.kind != VAE_X_BN_ACT) return;
+  if (xf.table) {
+    const int C = xf.channels;
+    for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
+      ta[ch] = xf.table[ch]; tb[ch] = xf.table[C + ch];
+      if (tp) { tp[ch] = xf.table[2 * C + ch]; tq[ch] = xf.table[3 * C + ch]; }
+    }
+    return;
+  }
   for (int ch = threadIdx.x; ch < xf.channels; ch += blockDim.x) {
     float mean, invstd, var;
     bn_moments(xf, ch, mean, invstd, var);
@@ -230,9 +239,10 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_data_kernel(HeadP p) {
   }
   if (p.epi.kind == VAE_X_BN_ACT) {
     __syncthreads();
+    const long roff = p.sum_reps > 1 ? (long)(blockIdx.x % p.sum_reps) * p.sum_rstride : 0;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      atomicAdd(p.dbeta + c, r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c]);
-      atomicAdd(p.dgamma + c, r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c]);
+      atomicAdd(p.dbeta + roff + c, r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c]);
+      atomicAdd(p.dgamma + roff + c, r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c]);
     }
   }
 }
@@ -318,10 +328,51 @@ int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
   p.x = a->x; p.xf = a->x_xf; p.wt = a->wt; p.bias = a->bias; p.target = a->target;
   p.recon = a->recon; p.sse = a->sse; p.coef = a->coef;
   p.dx = a->dx; p.epi = a->dx_epi; p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+  p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.dw = a->dw; p.db = a->db; p.grad_recon = a->grad_recon;
   if (p.xf.channels <= 0) p.xf.channels = a->c;
   if (p.epi.channels <= 0) p.epi.channels = a->c;
   return VAE_OK;
+}
+
+// ------------------------------------------------------------------ BatchNorm finalisation
+__global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) {
+  const vae_xform& x = a.xf;
+  const int C = x.channels;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
+    float mean, invstd, var;
+    bn_moments(x, c, mean, invstd, var);
+    const float g = x.gamma[c];
+    if (a.mode == 0) {
+      const float sc = g * invstd;
+      a.table[c] = sc;
+      a.table[C + c] = x.beta[c] - mean * sc;
+      a.table[2 * C + c] = invstd;
+      a.table[3 * C + c] = -mean * invstd;
+      if (x.running_mean) {
+        const float m = x.momentum;
+        const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
+        x.running_mean[c] = (1.f - m) * x.running_mean[c] + m * mean;
+        x.running_var[c] = (1.f - m) * x.running_var[c] + m * unb;
+      }
+    } else {
+      const float inv_m = 1.0f / x.count;
+      const float dgam = rsum(x.dgamma, x, c), dbet = rsum(x.dbeta, x, c);
+      const float A = g * invstd;
+      const float mgx = dgam * inv_m, mg = dbet * inv_m;
+      const float B = -A * invstd * mgx;
+      const float Cc = -A * (mg - mean * invstd * mgx);
+      a.table[c] = A;
+      a.table[C + c] = B;
+      a.table[2 * C + c] = Cc;
+      if (x.dgamma_out) x.dgamma_out[c] += dgam;
+      if (x.dbeta_out) x.dbeta_out[c] += dbet;
+      if (a.db) {
+        const float sum_y = rsum(x.sum, x, c) + x.count * (x.shift ? x.shift[c] : 0.f);
+        a.db[c] += A * dbet + B * sum_y + Cc * x.count;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ reparameterization
@@ -472,11 +523,18 @@ extern "C" void vae_probe_set(void* buf) { g_probe = static_cast<unsigned long l
 extern "C" unsigned long long* vae_probe_buffer(void) { return g_probe; }
 #endif
 
+namespace vae {
+int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st);
+int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStream_t st);
+}
+
 extern "C" int vae_head_fwd(const vae_head_args* a, void* stream) {
   HeadP p;
   int rc = head_setup(a, p, "head_fwd");
   if (rc) return rc;
   if (!a->sse) return fail(VAE_E_BADARG, "head_fwd: sse");
+  rc = head_fwd_mfma_launch(a, (hipStream_t)stream);   // bf16, 64-wide, 32 channels
+  if (rc != kHeadFallback) return rc;
   const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
   if (lds > 64 * 1024) return fail(VAE_E_UNSUPPORTED, "head_fwd: tile too large");
   if (a->dtype == VAE_F32) hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
@@ -492,6 +550,8 @@ extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
   if (p.epi.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta || !p.epi.aux)) return fail(VAE_E_BADARG, "head_bwd_data: BN epilogue");
   if (p.epi.kind != VAE_X_NONE && !p.epi.aux) return fail(VAE_E_BADARG, "head_bwd_data: epilogue aux");
   const hipStream_t st = (hipStream_t)stream;
+  rc = head_bwd_mfma_launch(a, true, false, st);
+  if (rc != kHeadFallback) return rc;
   const bool f = a->dtype == VAE_F32;
   switch (a->c) {
     case 32:
@@ -514,11 +574,36 @@ extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
   if (rc) return rc;
   if ((!a->coef && !a->grad_recon) || !a->dw) return fail(VAE_E_BADARG, "head_bwd_filter: coef/grad_recon/dw");
   if (9 * a->c > 3 * HEAD_T) return fail(VAE_E_UNSUPPORTED, "head_bwd_filter: channels");
+  rc = head_bwd_mfma_launch(a, false, true, (hipStream_t)stream);
+  if (rc != kHeadFallback) return rc;
   const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
   const int grid = p.tiles < 256 ? p.tiles : 256;
   if (a->dtype == VAE_F32) hipLaunchKernelGGL(head_bwd_filter_kernel<float>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   else hipLaunchKernelGGL(head_bwd_filter_kernel<__bf16>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   return check_launch("head_bwd_filter");
+}
+
+extern "C" int vae_bn_finalize(const vae_bn_args* a, void* stream) {
+  if (!a || !a->table || a->xf.channels <= 0 || !a->xf.sum || !a->xf.sumsq || !a->xf.gamma || !a->xf.beta ||
+      a->xf.count <= 0.f)
+    return fail(VAE_E_BADARG, "bn_finalize: args");
+  if (a->mode != 0 && a->mode != 1) return fail(VAE_E_BADARG, "bn_finalize: mode %d", a->mode);
+  if (a->mode == 1 && (!a->xf.dgamma || !a->xf.dbeta)) return fail(VAE_E_BADARG, "bn_finalize: backward sums");
+  const int grid = (a->xf.channels + 255) / 256;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
+  return check_launch("bn_finalize");
+}
+
+extern "C" int vae_head_bwd(const vae_head_args* a, void* stream) {
+  HeadP p;
+  int rc = head_setup(a, p, "head_bwd");
+  if (rc) return rc;
+  if ((!a->coef && !a->grad_recon) || !a->dx || !a->dw) return fail(VAE_E_BADARG, "head_bwd: coef/grad_recon/dx/dw");
+  if (p.epi.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta || !p.epi.aux)) return fail(VAE_E_BADARG, "head_bwd: BN epilogue");
+  rc = head_bwd_mfma_launch(a, true, true, (hipStream_t)stream);
+  if (rc != kHeadFallback) return rc;
+  if ((rc = vae_head_bwd_data(a, stream))) return rc;
+  return vae_head_bwd_filter(a, stream);
 }
 
 extern "C" int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int32_t latent, const float* mulv,

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 1
+ABI_VERSION = 4
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -34,7 +34,9 @@ class Xform(ctypes.Structure):
                 ("eps", c_float), ("momentum", c_float),
                 ("sum", c_void_p), ("sumsq", c_void_p), ("shift", c_void_p), ("gamma", c_void_p),
                 ("beta", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("aux", c_void_p),
-                ("running_mean", c_void_p), ("running_var", c_void_p)]
+                ("running_mean", c_void_p), ("running_var", c_void_p),
+                ("reps", c_int32), ("rstride", c_int32), ("dgamma_out", c_void_p), ("dbeta_out", c_void_p),
+                ("table", c_void_p)]
 
 
 class ConvArgs(ctypes.Structure):
@@ -42,7 +44,8 @@ class ConvArgs(ctypes.Structure):
                 ("k", c_int32), ("p", c_int32), ("q", c_int32), ("r", c_int32), ("stride", c_int32),
                 ("pad", c_int32), ("x_nchw_f32", c_int32),
                 ("x", c_void_p), ("x_xf", Xform), ("wt", c_void_p), ("bias", c_void_p), ("y", c_void_p),
-                ("y_sum", c_void_p), ("y_sumsq", c_void_p), ("residual", c_void_p), ("residual_xf", Xform),
+                ("y_sum", c_void_p), ("y_sumsq", c_void_p), ("sum_reps", c_int32), ("sum_rstride", c_int32),
+                ("residual", c_void_p), ("residual_xf", Xform),
                 ("dy", c_void_p), ("dy_xf", Xform), ("dx", c_void_p), ("dx_epi", Xform),
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
                 ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
@@ -53,7 +56,8 @@ class LinearArgs(ctypes.Structure):
                 ("x", c_void_p), ("x_xf", Xform), ("wt", c_void_p), ("bias", c_void_p), ("y", c_void_p),
                 ("y_f32", c_int32), ("dy", c_void_p), ("dy_f32", c_int32), ("dx", c_void_p), ("dx_epi", Xform),
                 ("dx_dgamma", c_void_p),
-                ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
+                ("dx_dbeta", c_void_p), ("sum_reps", c_int32), ("sum_rstride", c_int32),
+                ("dw", c_void_p), ("db", c_void_p),
                 ("mulv", c_void_p), ("eps", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p),
                 ("samples", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
 
@@ -63,7 +67,9 @@ class HeadArgs(ctypes.Structure):
                 ("x", c_void_p), ("x_xf", Xform), ("wt", c_void_p), ("bias", c_void_p),
                 ("target", c_void_p), ("samples", c_int32), ("recon", c_void_p), ("sse", c_void_p),
                 ("coef", c_void_p), ("dx", c_void_p), ("dx_epi", Xform), ("dx_dgamma", c_void_p),
-                ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p), ("grad_recon", c_void_p)]
+                ("dx_dbeta", c_void_p), ("sum_reps", c_int32), ("sum_rstride", c_int32),
+                ("dw", c_void_p), ("db", c_void_p), ("grad_recon", c_void_p),
+                ("workspace", c_void_p), ("workspace_bytes", c_int64)]
 
 
 class ElboArgs(ctypes.Structure):
@@ -72,6 +78,10 @@ class ElboArgs(ctypes.Structure):
                 ("c_max", c_float), ("c_stop_iter", c_float), ("iter", c_void_p), ("mulv", c_void_p),
                 ("sse", c_void_p), ("out", c_void_p), ("per_img", c_void_p), ("head_coef", c_void_p),
                 ("kl_coef", c_void_p)]
+
+
+class BnArgs(ctypes.Structure):
+    _fields_ = [("mode", c_int32), ("xf", Xform), ("table", c_void_p), ("db", c_void_p)]
 
 
 # name -> (argtypes)
@@ -90,6 +100,8 @@ _SIGS = {
     "vae_head_fwd": [POINTER(HeadArgs), c_void_p],
     "vae_head_bwd_data": [POINTER(HeadArgs), c_void_p],
     "vae_head_bwd_filter": [POINTER(HeadArgs), c_void_p],
+    "vae_head_bwd": [POINTER(HeadArgs), c_void_p],
+    "vae_bn_finalize": [POINTER(BnArgs), c_void_p],
     "vae_reparam_fwd": [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p],
     "vae_elbo_fwd": [POINTER(ElboArgs), c_void_p],
     "vae_adam_step": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float,

@@ -153,17 +153,26 @@ class StepPlan:
         self.g_h0 = torch.empty_like(self.h0)
         self.g_dec = [torch.empty_like(t) for t in self.dec]
         self.g_fin = torch.empty_like(self.fin)
-        # zero region: grads | BN sums | sse | dmulv   (16-B aligned pieces)
-        nbn = sum(b.channels for b in net.layout.bns)
-        nz = net.layout.total + 2 * nbn + _pad4(BS) + _pad4(B * 2 * D)
+        # zero region: grads | BN statistics | sse | dmulv   (16-B aligned pieces).  Every
+        # BatchNorm has forward sums (Σ, Σ²) and backward sums (Σg·x̂, Σg), each kept in
+        # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
+        nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
+        nz = net.layout.total + nbn + _pad4(BS) + _pad4(B * 2 * D)
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
-        self.bnsum: Dict[str, torch.Tensor] = {}
+        self.bnfwd: Dict[str, torch.Tensor] = {}     # [2][reps][C]: Σ(y-shift), Σ(y-shift)²
+        self.bnbwd: Dict[str, torch.Tensor] = {}     # [2][reps][C]: Σg·x̂ (dγ), Σg (dβ)
         for b in net.layout.bns:
-            self.bnsum[b.prefix] = self.zero[o:o + 2 * b.channels]; o += 2 * b.channels
+            n = 2 * bn_reps(b.channels) * b.channels
+            self.bnfwd[b.prefix] = self.zero[o:o + n].view(2, bn_reps(b.channels), b.channels); o += n
+            self.bnbwd[b.prefix] = self.zero[o:o + n].view(2, bn_reps(b.channels), b.channels); o += n
         self.sse = self.zero[o:o + BS]; o += _pad4(BS)
         self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
+        # per-BatchNorm coefficient tables, rewritten every step by vae_bn_finalize:
+        # forward [4][C] (BN_ACT) then backward [3][C] (BN_DY)
+        self.bntab: Dict[str, torch.Tensor] = {
+            b.prefix: torch.zeros(7 * b.channels, **f32) for b in net.layout.bns}
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
         # split-K partial slabs (fp32), reused by every launch of the step on the stream
         self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
@@ -179,19 +188,25 @@ class StepPlan:
     def _bn_prod_bias(self, prefix: str) -> str:
         return prefix[:-2] + ".0.bias"          # "encoder.3.1" -> "encoder.3.0.bias"
 
-    def bn_xf(self, prefix: str, kind: int, count: int, aux=None, running: bool = False) -> L.Xform:
+    def bn_xf(self, prefix: str, kind: int, count: int, aux=None, running: bool = False,
+              table: bool = True) -> L.Xform:
         net = self.net
         C = net.layout.bn_by_prefix[prefix].channels
-        s = self.bnsum[prefix]
+        s = self.bnfwd[prefix]
         xf = L.Xform(kind=kind, channels=C, slope=SLOPE, count=float(count), eps=BN_EPS, momentum=BN_MOMENTUM)
-        xf.sum = s.data_ptr()
-        xf.sumsq = s.data_ptr() + 4 * C
+        xf.sum = s[0].data_ptr()
+        xf.sumsq = s[1].data_ptr()
+        xf.reps = s.shape[1]
+        xf.rstride = C
         xf.shift = net.p(self._bn_prod_bias(prefix))
         xf.gamma = net.p(prefix + ".weight")
         xf.beta = net.p(prefix + ".bias")
         if kind == L.X_BN_DY:
-            xf.dgamma = self.g(prefix + ".weight")
-            xf.dbeta = self.g(prefix + ".bias")
+            xf.dgamma = self.bnbwd[prefix][0].data_ptr()
+            xf.dbeta = self.bnbwd[prefix][1].data_ptr()
+        if table:
+            t = self.bntab[prefix]
+            xf.table = t.data_ptr() + (4 * 4 * C if kind == L.X_BN_DY else 0)
         if aux is not None:
             xf.aux = aux.data_ptr()
         if running:
@@ -199,8 +214,34 @@ class StepPlan:
             xf.running_var = net.run_var(prefix)
         return xf
 
+    def fwd_sums(self, arg, prefix: str):
+        """Producer side of a BatchNorm's forward statistics (conv / convT fwd epilogue)."""
+        s = self.bnfwd[prefix]
+        arg.y_sum, arg.y_sumsq = s[0].data_ptr(), s[1].data_ptr()
+        arg.sum_reps, arg.sum_rstride = s.shape[1], s.shape[2]
+
+    def bwd_sums(self, arg, prefix: str):
+        """Producer side of a BatchNorm's backward sums (bwd_data epilogue of the next layer)."""
+        s = self.bnbwd[prefix]
+        arg.dx_dgamma, arg.dx_dbeta = s[0].data_ptr(), s[1].data_ptr()
+        arg.sum_reps, arg.sum_rstride = s.shape[1], s.shape[2]
+
+    def bn_finalize(self, lst, prefix: str, mode: int, count: int):
+        """Queue vae_bn_finalize for one BatchNorm: mode 0 after the conv producing its input
+        (table + running statistics), mode 1 after the kernel producing its backward sums
+        (table + dγ, dβ + the producing conv's bias gradient in closed form)."""
+        C = self.net.layout.bn_by_prefix[prefix].channels
+        a = L.BnArgs(mode=mode)
+        a.xf = self.bn_xf(prefix, L.X_BN_DY if mode else L.X_BN_ACT, count, running=(mode == 0), table=False)
+        a.table = self.bntab[prefix].data_ptr() + (4 * 4 * C if mode else 0)
+        if mode:
+            a.xf.dgamma_out = self.g(prefix + ".weight")
+            a.xf.dbeta_out = self.g(prefix + ".bias")
+            a.db = self.g(self._bn_prod_bias(prefix))
+        self._add(lst, "vae_bn_finalize", a)
+
     def _add(self, lst, fn, arg):
-        if isinstance(arg, (L.ConvArgs, L.LinearArgs)):
+        if isinstance(arg, (L.ConvArgs, L.LinearArgs, L.HeadArgs)):
             arg.workspace = self.workspace.data_ptr()
             arg.workspace_bytes = self.workspace.numel() * 4
         self._keep.append(arg)
@@ -239,9 +280,9 @@ class StepPlan:
             a.wt = net.w(f"encoder.{i}.0.weight")
             a.bias = net.p(f"encoder.{i}.0.bias")
             a.y = self.enc[i].data_ptr()
-            a.y_sum = self.bnsum[enc_pre[i]].data_ptr()
-            a.y_sumsq = a.y_sum + 4 * h[i]
+            self.fwd_sums(a, enc_pre[i])
             self._add(F, "vae_conv2d_fwd", a)
+            self.bn_finalize(F, enc_pre[i], 0, cnt(self.enc[i]))
             sp //= 2
         # ---------------------------------------------------------------- fc_mu | fc_var
         a = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
@@ -274,9 +315,9 @@ class StepPlan:
             a.wt = net.w(dec_w[i] + ".weight")
             a.bias = net.p(dec_w[i] + ".bias")
             a.y = dec_out[i].data_ptr()
-            a.y_sum = self.bnsum[dec_pre[i]].data_ptr()
-            a.y_sumsq = a.y_sum + 4 * cout
+            self.fwd_sums(a, dec_pre[i])
             self._add(F, "vae_convT2d_fwd", a)
+            self.bn_finalize(F, dec_pre[i], 0, cnt(dec_out[i]))
             prev, prev_pre = dec_out[i], dec_pre[i]
             sp *= 2
         # ---------------------------------------------------------------- head + SSE
@@ -315,12 +356,10 @@ class StepPlan:
         hb.dx = self.g_fin.data_ptr()
         hb.dx_epi = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin))
         hb.dx_epi.aux = self.fin.data_ptr()
-        hb.dx_dgamma = self.g("final_layer.1.weight")
-        hb.dx_dbeta = self.g("final_layer.1.bias")
+        self.bwd_sums(hb, "final_layer.1")
         hb.dw = self.g("final_layer.3.weight")
         hb.db = self.g("final_layer.3.bias")
-        self._add(Bw, "vae_head_bwd_data", hb)
-        self._add(Bw, "vae_head_bwd_filter", hb)
+        self._add(Bw, "vae_head_bwd", hb)
         # decoder, last block first
         sps = [2 * 2 ** i for i in range(len(r))]          # input spatial of each ConvT
         for i in reversed(range(len(r))):
@@ -329,6 +368,7 @@ class StepPlan:
             cout = r[i + 1] if i < len(r) - 1 else r[-1]
             x_t = self.h0 if i == 0 else dec_out[i - 1]
             gx_t = self.g_h0 if i == 0 else g_dec_out[i - 1]
+            self.bn_finalize(Bw, dec_pre[i], 1, cnt(dec_out[i]))
             dy_xf = self.bn_xf(dec_pre[i], L.X_BN_DY, cnt(dec_out[i]), aux=dec_out[i])
             a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
             a.dy = g_dec_out[i].data_ptr()
@@ -337,8 +377,7 @@ class StepPlan:
             a.dx = gx_t.data_ptr()
             if i > 0:
                 a.dx_epi = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t), aux=x_t)
-                a.dx_dgamma = self.g(dec_pre[i - 1] + ".weight")
-                a.dx_dbeta = self.g(dec_pre[i - 1] + ".bias")
+                self.bwd_sums(a, dec_pre[i - 1])
             self._add(Bw, "vae_convT2d_bwd_data", a)
             f = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
             f.x = x_t.data_ptr()
@@ -346,8 +385,7 @@ class StepPlan:
                 f.x_xf = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t))
             f.dy = g_dec_out[i].data_ptr()
             f.dy_xf = dy_xf
-            f.dw = self.g(dec_w[i] + ".weight")
-            f.db = self.g(dec_w[i] + ".bias")
+            f.dw = self.g(dec_w[i] + ".weight")      # bias gradient: closed form in vae_bn_finalize
             self._add(Bw, "vae_convT2d_bwd_filter", f)
         # decoder_input: dz -> d[mu|logvar] (reparameterization + KL), and its weight grads
         a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
@@ -372,8 +410,7 @@ class StepPlan:
         a.wt = net.w("fc_mu.weight")
         a.dx = self.g_enc[-1].data_ptr()
         a.dx_epi = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), aux=self.enc[-1])
-        a.dx_dgamma = self.g(enc_pre[-1] + ".weight")
-        a.dx_dbeta = self.g(enc_pre[-1] + ".bias")
+        self.bwd_sums(a, enc_pre[-1])
         self._add(Bw, "vae_linear_bwd_data", a)
         f = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
         f.dy = self.dmulv.data_ptr()
@@ -388,6 +425,7 @@ class StepPlan:
         for i in reversed(range(nenc)):
             sp = sps[i]
             cin = 3 if i == 0 else h[i - 1]
+            self.bn_finalize(Bw, enc_pre[i], 1, cnt(self.enc[i]))
             dy_xf = self.bn_xf(enc_pre[i], L.X_BN_DY, cnt(self.enc[i]), aux=self.enc[i])
             f = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
             f.dy = self.g_enc[i].data_ptr()
@@ -398,8 +436,7 @@ class StepPlan:
             else:
                 f.x = self.enc[i - 1].data_ptr()
                 f.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]))
-            f.dw = self.g(f"encoder.{i}.0.weight")
-            f.db = self.g(f"encoder.{i}.0.bias")
+            f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form in vae_bn_finalize
             self._add(Bw, "vae_conv2d_bwd_filter", f)
             if i > 0:
                 a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
@@ -408,8 +445,7 @@ class StepPlan:
                 a.wt = net.w(f"encoder.{i}.0.weight")
                 a.dx = self.g_enc[i - 1].data_ptr()
                 a.dx_epi = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]), aux=self.enc[i - 1])
-                a.dx_dgamma = self.g(enc_pre[i - 1] + ".weight")
-                a.dx_dbeta = self.g(enc_pre[i - 1] + ".bias")
+                self.bwd_sums(a, enc_pre[i - 1])
                 self._add(Bw, "vae_conv2d_bwd_data", a)
 
     # ------------------------------------------------------------------ execution
@@ -436,6 +472,13 @@ class StepPlan:
         o = self.out.tolist()
         third = "KLD"
         return {"loss": o[0], "Reconstruction_Loss": o[1], third: o[2]}
+
+
+def bn_reps(channels: int) -> int:
+    """Replicas of a BatchNorm's statistics: enough that the ~1000 workgroups of a producing
+    kernel add into each address only a few dozen times, few enough that a consumer block
+    reads at most ~8K floats to reduce them."""
+    return max(1, min(32, 4096 // max(1, channels)))
 
 
 def _pad4(n: int) -> int:

@@ -221,8 +221,10 @@ def test_linear_all(dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-def test_head_fwd_bwd(dtype):
-    """final Conv2d(32->3,k3,s1,p1)+Tanh and MSE vs autograd (vanilla_vae.py:73-75, :140)."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_head_fwd_bwd(dtype, fused):
+    """final Conv2d(32->3,k3,s1,p1)+Tanh and MSE vs autograd (vanilla_vae.py:73-75, :140);
+    fused: vae_head_bwd (data + filter in one pass, per-block partials summed from a workspace)."""
     L = _L()
     torch.manual_seed(6)
     N, C, H = 2, 32, 64
@@ -250,9 +252,16 @@ def test_head_fwd_bwd(dtype):
     a.recon = recon.data_ptr(); a.sse = sse.data_ptr(); a.coef = coef.data_ptr()
     a.dx = dx.data_ptr(); a.dx_epi = bn.xf(aux=bn.y_dev); a.dx_dgamma = dgp.data_ptr(); a.dx_dbeta = dbp.data_ptr()
     a.dw = dw.data_ptr(); a.db = db.data_ptr()
+    ws = torch.empty(1 << 20, device="cuda")
+    if fused:
+        a.workspace = ws.data_ptr()
+        a.workspace_bytes = ws.numel() * 4
     L.call("vae_head_fwd", ctypes.byref(a), _stream())
-    L.call("vae_head_bwd_data", ctypes.byref(a), _stream())
-    L.call("vae_head_bwd_filter", ctypes.byref(a), _stream())
+    if fused:
+        L.call("vae_head_bwd", ctypes.byref(a), _stream())
+    else:
+        L.call("vae_head_bwd_data", ctypes.byref(a), _stream())
+        L.call("vae_head_bwd_filter", ctypes.byref(a), _stream())
     torch.cuda.synchronize()
     t = tol(dtype)
     assert rel(recon.cpu(), rec.detach()) < t
@@ -261,3 +270,11 @@ def test_head_fwd_bwd(dtype):
     assert rel(db.cpu(), b.grad) < 5 * t
     assert rel(dgp.cpu(), gp.grad) < 20 * t
     assert rel(dbp.cpu(), bp.grad) < 20 * t
+    # dx = dL/dz of the BatchNorm output z feeding the head (LeakyReLU backward applied)
+    z = F.batch_norm(y_prev.detach(), None, None, gam, bet, True, 0.1, 1e-5).requires_grad_()
+    rec2 = torch.tanh(F.conv2d(F.leaky_relu(z, 0.01), w.detach(), b.detach(), padding=1))
+    F.mse_loss(rec2, tgt).backward()
+    # norm-relative: with y stored in bf16 a handful of pixels with z = BN(y) ~ 0 take the other
+    # LeakyReLU branch (a factor 1/slope on an element that is ~0 anyway)
+    d = dx.float().permute(0, 3, 1, 2).cpu()
+    assert float((d - z.grad).norm() / z.grad.norm()) < t
