@@ -1,0 +1,287 @@
+"""BaseVAE-compatible models on the MI355X kernels — the drop-in for the reference's
+`models` package on the training hot path.
+
+Mirrors the reference interface (paths relative to the reference root):
+  BaseVAE                 models/base.py:5-28       encode/decode/sample/generate/forward/loss_function
+  VanillaVAE              models/vanilla_vae.py:8-173
+  BetaVAE                 models/beta_vae.py:8-179  (loss_type 'H' / 'B', per-instance num_iter)
+  IWAE                    models/iwae.py:8-188      (num_samples; row-major b*S+s latent order)
+  vae_models registry     models/__init__.py:35-56
+
+`forward(x)` runs the HIP encoder/decoder (libvaehip.so) and returns the reference's list
+([recons, input, mu, log_var], IWAE: [recons, input, mu, log_var, z, eps]); `loss_function`
+is the reference formula evaluated by torch on those tensors (so every loss variant and its
+returned dict are the reference's own); `loss.backward()` reaches `_VAEStep.backward`, which
+runs the fused HIP backward seeded with dL/drecon and dL/d[mu, log_var] and returns the
+gradient of the flat parameter buffer.  Optimizers see one flat nn.Parameter (`model.flat`);
+`reference_state_dict()` / `load_reference_state_dict()` convert to the reference's keys and
+layouts (vae_amd/layout.py).
+
+Training-mode BatchNorm only: eval-mode inference (running statistics) is the next row of the
+build plan; sample()/generate() in eval mode raise NotImplementedError.
+"""
+from __future__ import annotations
+
+from abc import abstractmethod
+from typing import Any, Dict, List, Optional
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from . import _lib as L
+from .net import StepPlan, VAENet
+
+Tensor = torch.Tensor
+
+
+class BaseVAE(nn.Module):
+    """models/base.py:5-28."""
+
+    def __init__(self) -> None:
+        super().__init__()
+
+    def encode(self, input: Tensor) -> List[Tensor]:
+        raise NotImplementedError
+
+    def decode(self, input: Tensor) -> Any:
+        raise NotImplementedError
+
+    def sample(self, batch_size: int, current_device: int, **kwargs) -> Tensor:
+        raise NotImplementedError
+
+    def generate(self, x: Tensor, **kwargs) -> Tensor:
+        raise NotImplementedError
+
+    @abstractmethod
+    def forward(self, *inputs: Tensor) -> Tensor:
+        pass
+
+    @abstractmethod
+    def loss_function(self, *inputs: Any, **kwargs) -> Tensor:
+        pass
+
+
+class _VAEStep(torch.autograd.Function):
+    """Forward of the HIP network; backward = the fused HIP backward of the whole network."""
+
+    @staticmethod
+    def forward(ctx, flat: Tensor, x: Tensor, eps: Tensor, model: "_HipVAE"):
+        plan = model._plan(x.shape[0])
+        st = L.stream_ptr()
+        model.net.sync_lowp()                          # optimizer may have moved the fp32 master
+        plan.x.copy_(x.detach().to(plan.x.dtype))
+        plan.eps.copy_(eps.detach().reshape(plan.eps.shape))
+        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, plan.step.data_ptr(), st)
+        plan.forward(st)
+        model.net.num_batches_tracked += 1
+        ctx.plan = plan
+        D = model.latent_dim
+        recon = plan.recon.clone()
+        mu = plan.mulv[:, :D].clone()
+        log_var = plan.mulv[:, D:].clone()
+        return recon, mu, log_var
+
+    @staticmethod
+    def backward(ctx, g_recon: Optional[Tensor], g_mu: Optional[Tensor], g_lv: Optional[Tensor]):
+        plan = ctx.plan
+        D = plan.net.latent_dim
+        if g_recon is None:
+            plan.grad_recon.zero_()
+        else:
+            plan.grad_recon.copy_(g_recon.reshape(plan.grad_recon.shape))
+        dm = plan.dmulv.view(plan.B, 2 * D)
+        dm[:, :D].copy_(g_mu if g_mu is not None else torch.zeros_like(dm[:, :D]))
+        dm[:, D:].copy_(g_lv if g_lv is not None else torch.zeros_like(dm[:, D:]))
+        plan.backward(L.stream_ptr())
+        return plan.grads.clone(), None, None, None
+
+
+class _HipVAE(BaseVAE):
+    """Shared machinery of the VanillaVAE-family models on libvaehip."""
+
+    samples = 1
+
+    def __init__(self, in_channels: int, latent_dim: int, hidden_dims: List = None, *,
+                 dtype: torch.dtype = torch.float32, device=None, img_size: int = 64, seed: Optional[int] = None,
+                 **kwargs) -> None:
+        super().__init__()
+        self.latent_dim = latent_dim
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        self.net = VAENet(in_channels=in_channels, latent_dim=latent_dim, hidden_dims=hidden_dims,
+                          img_size=img_size, dtype=dtype, device=device, generator=gen)
+        self.flat = nn.Parameter(self.net.params)      # shares storage with the kernels' buffer
+        self._plans: Dict[int, StepPlan] = {}
+
+    def _plan(self, batch: int) -> StepPlan:
+        if batch not in self._plans:
+            self._plans[batch] = StepPlan(self.net, batch, loss="iwae" if self.samples > 1 else "vanilla",
+                                          samples=self.samples, fused_loss=False)
+        return self._plans[batch]
+
+    def _check_train(self, what: str):
+        if not self.training:
+            raise NotImplementedError(f"{what}: eval-mode BatchNorm (running statistics) is not implemented "
+                                      f"on the MI355X path yet (DESIGN.md §7); call model.train()")
+
+    # ---- reference state dict interop (models/vanilla_vae.py parameter names and layouts)
+    def reference_state_dict(self) -> Dict[str, Tensor]:
+        return self.net.reference_state_dict()
+
+    def load_reference_state_dict(self, sd: Dict[str, Tensor]):
+        with torch.no_grad():
+            self.net.load_reference_state_dict(sd)
+
+    # ---- BaseVAE
+    def reparameterize(self, mu: Tensor, logvar: Tensor) -> Tensor:
+        """vanilla_vae.py:107-117 (torch ops; the fused path runs it on the GPU inside forward)."""
+        std = torch.exp(0.5 * logvar)
+        eps = torch.randn_like(std)
+        return eps * std + mu
+
+    def encode(self, input: Tensor) -> List[Tensor]:
+        self._check_train("encode")
+        plan = self._plan(input.shape[0])
+        st = L.stream_ptr()
+        self.net.sync_lowp()
+        plan.x.copy_(input.detach())
+        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, plan.step.data_ptr(), st)
+        plan.encode(st)
+        D = self.latent_dim
+        return [plan.mulv[:, :D].clone(), plan.mulv[:, D:].clone()]
+
+    def decode(self, z: Tensor) -> Tensor:
+        self._check_train("decode")
+        rows = z.reshape(-1, self.latent_dim).shape[0]
+        plan = self._plan(rows // self.samples)
+        st = L.stream_ptr()
+        self.net.sync_lowp()
+        plan.z.copy_(z.detach().reshape(plan.z.shape))
+        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, plan.step.data_ptr(), st)
+        plan.decode(st)
+        return plan.recon.clone()
+
+    def _run(self, input: Tensor, eps: Optional[Tensor] = None):
+        self._check_train("forward")
+        B = input.shape[0]
+        if eps is None:                                 # torch.randn_like(std), vanilla_vae.py:116
+            eps = torch.randn(B * self.samples, self.latent_dim, device=input.device)
+        return _VAEStep.apply(self.flat, input, eps, self) + (eps,)
+
+    def sample(self, num_samples: int, current_device: int, **kwargs) -> Tensor:
+        """vanilla_vae.py:148-161 (needs eval-mode BatchNorm: next row)."""
+        self._check_train("sample")
+        z = torch.randn(num_samples, self.latent_dim, device=current_device)
+        return self.decode(z)
+
+    def generate(self, x: Tensor, **kwargs) -> Tensor:
+        """vanilla_vae.py:163-173."""
+        return self.forward(x)[0]
+
+
+class VanillaVAE(_HipVAE):
+    """models/vanilla_vae.py:8-173 on libvaehip."""
+
+    def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
+        recon, mu, log_var, _ = self._run(input, kwargs.get("eps"))
+        return [recon, input, mu, log_var]
+
+    def loss_function(self, *args, **kwargs) -> dict:
+        """vanilla_vae.py:124-146."""
+        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
+        kld_weight = kwargs['M_N']
+        recons_loss = F.mse_loss(recons, input)
+        kld_loss = torch.mean(-0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=1), dim=0)
+        loss = recons_loss + kld_weight * kld_loss
+        return {'loss': loss, 'Reconstruction_Loss': recons_loss.detach(), 'KLD': -kld_loss.detach()}
+
+
+class BetaVAE(_HipVAE):
+    """models/beta_vae.py:8-179 on libvaehip."""
+
+    num_iter = 0  # beta_vae.py:10 (class attribute, shared like the reference's)
+
+    def __init__(self, in_channels: int, latent_dim: int, hidden_dims: List = None, beta: int = 4,
+                 gamma: float = 1000., max_capacity: int = 25, Capacity_max_iter: int = 1e5, loss_type: str = 'B',
+                 **kwargs) -> None:
+        super().__init__(in_channels, latent_dim, hidden_dims, **kwargs)
+        self.beta = beta
+        self.gamma = gamma
+        self.loss_type = loss_type
+        self.C_max = torch.Tensor([max_capacity])
+        self.C_stop_iter = Capacity_max_iter
+
+    def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
+        recon, mu, log_var, _ = self._run(input, kwargs.get("eps"))
+        return [recon, input, mu, log_var]
+
+    def loss_function(self, *args, **kwargs) -> dict:
+        """beta_vae.py:129-152."""
+        self.num_iter += 1
+        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
+        kld_weight = kwargs['M_N']
+        recons_loss = F.mse_loss(recons, input)
+        kld_loss = torch.mean(-0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=1), dim=0)
+        if self.loss_type == 'H':
+            loss = recons_loss + self.beta * kld_weight * kld_loss
+        elif self.loss_type == 'B':
+            self.C_max = self.C_max.to(input.device)
+            C = torch.clamp(self.C_max / self.C_stop_iter * self.num_iter, 0, self.C_max.data[0])
+            loss = recons_loss + self.gamma * kld_weight * (kld_loss - C).abs()
+        else:
+            raise ValueError('Undefined loss type.')
+        return {'loss': loss, 'Reconstruction_Loss': recons_loss, 'KLD': kld_loss}
+
+
+class IWAE(_HipVAE):
+    """models/iwae.py:8-188 on libvaehip (decoder batched at B*S; latents in row-major b*S+s
+    order — the semantics of iwae.py:103 on torch < 1.5)."""
+
+    def __init__(self, in_channels: int, latent_dim: int, hidden_dims: List = None, num_samples: int = 5,
+                 **kwargs) -> None:
+        self.samples = num_samples
+        super().__init__(in_channels, latent_dim, hidden_dims, **kwargs)
+        self.num_samples = num_samples
+
+    def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
+        B, S, D = input.shape[0], self.num_samples, self.latent_dim
+        recon, mu, log_var, eps = self._run(input, kwargs.get("eps"))
+        mu_r = mu.repeat(S, 1, 1).permute(1, 0, 2)          # [B x S x D], iwae.py:123-124
+        lv_r = log_var.repeat(S, 1, 1).permute(1, 0, 2)
+        eps_r = eps.reshape(B, S, D)
+        z = eps_r * torch.exp(0.5 * lv_r) + mu_r
+        eps_ret = (z - mu_r) / lv_r                         # iwae.py:126 (returned, unused by the loss)
+        return [recon.view(B, S, *recon.shape[1:]), input, mu_r, lv_r, z, eps_ret]
+
+    def loss_function(self, *args, **kwargs) -> dict:
+        """iwae.py:129-160."""
+        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
+        input = input.repeat(self.num_samples, 1, 1, 1, 1).permute(1, 0, 2, 3, 4)
+        kld_weight = kwargs['M_N']
+        log_p_x_z = ((recons - input) ** 2).flatten(2).mean(-1)
+        kld_loss = -0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=2)
+        log_weight = (log_p_x_z + kld_weight * kld_loss)
+        weight = F.softmax(log_weight, dim=-1)
+        loss = torch.mean(torch.sum(weight * log_weight, dim=-1), dim=0)
+        return {'loss': loss, 'Reconstruction_Loss': log_p_x_z.mean(), 'KLD': -kld_loss.mean()}
+
+
+# models/__init__.py:35-56: the families on the MI355X path; the others raise on use.
+_ON_PATH = {'VanillaVAE': VanillaVAE, 'BetaVAE': BetaVAE, 'IWAE': IWAE}
+_REFERENCE_NAMES = ['HVAE', 'LVAE', 'IWAE', 'SWAE', 'MIWAE', 'VQVAE', 'DFCVAE', 'DIPVAE', 'BetaVAE', 'InfoVAE',
+                    'WAE_MMD', 'VampVAE', 'GammaVAE', 'MSSIMVAE', 'JointVAE', 'BetaTCVAE', 'FactorVAE',
+                    'LogCoshVAE', 'VanillaVAE', 'ConditionalVAE', 'CategoricalVAE', 'Autoencoder']
+
+
+def _not_on_path(name):
+    def ctor(*args, **kwargs):
+        raise NotImplementedError(f"{name} is not on the MI355X training path of this build "
+                                  f"(VanillaVAE, BetaVAE, IWAE are; DESIGN.md §7)")
+    return ctor
+
+
+vae_models = {name: _ON_PATH.get(name) or _not_on_path(name) for name in _REFERENCE_NAMES}
+VAE = VanillaVAE      # models/__init__.py:29-33 aliases
+GaussianVAE = VanillaVAE
+CVAE = _not_on_path('ConditionalVAE')
+GumbelVAE = _not_on_path('CategoricalVAE')

@@ -110,9 +110,14 @@ class StepPlan:
 
     def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
-                 capacity_max_iter: float = 1e5):
+                 capacity_max_iter: float = 1e5, fused_loss: bool = True):
         self.net = net
         self.B = batch
+        # fused_loss: the ELBO runs on the GPU inside the step and seeds the backward itself.
+        # False (the BaseVAE drop-in, vae_amd.models): the loss is computed by the caller from
+        # recon/mu/log_var and the backward is seeded with dL/drecon (grad_recon) and
+        # dL/d[mu|log_var] (written into dmulv) instead.
+        self.fused_loss = fused_loss
         self.S = samples if loss == "iwae" else 1
         self.loss_kind = {"vanilla": L.LOSS_VANILLA, "betaH": L.LOSS_BETA_H, "betaB": L.LOSS_BETA_B,
                           "iwae": L.LOSS_IWAE}[loss]
@@ -143,6 +148,7 @@ class StepPlan:
             self.dec.append(torch.empty(BS, sp, sp, r[i + 1], dtype=T, device=dev))
         self.fin = torch.empty(BS, img, img, r[-1], dtype=T, device=dev)
         self.recon = torch.empty(BS, 3, img, img, **f32)
+        self.grad_recon = None if fused_loss else torch.zeros(BS, 3, img, img, **f32)
         self.out = torch.zeros(4, **f32)                                  # loss, recon, KLD(report), kld
         self.per_img = torch.zeros(BS, **f32)
         self.head_coef = torch.zeros(BS, **f32)
@@ -293,8 +299,10 @@ class StepPlan:
         a.y = self.mulv.data_ptr()
         a.y_f32 = 1
         self._add(F, "vae_linear_fwd", a)
+        self.n_encode = len(F)                 # calls of encode(): encoder + fc_mu|fc_var
         self._reparam = (T, BS, self.S, D, self.mulv.data_ptr(), self.eps.data_ptr(), self.z.data_ptr())
         F.append(("vae_reparam_fwd", None))
+        self.n_decode0 = len(F)                # decode(): decoder_input .. head
         # ---------------------------------------------------------------- decoder_input
         a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
         a.x = self.z.data_ptr()
@@ -341,7 +349,9 @@ class StepPlan:
         e.per_img = self.per_img.data_ptr()
         e.head_coef = self.head_coef.data_ptr()
         e.kl_coef = self.kl_coef.data_ptr()
-        self._add(F, "vae_elbo_fwd", e)
+        self.n_decode1 = len(F)
+        if self.fused_loss:
+            self._add(F, "vae_elbo_fwd", e)
 
         # ================================================================ backward
         Bw = self.bwd_calls
@@ -352,7 +362,10 @@ class StepPlan:
         hb.bias = net.p("final_layer.3.bias")
         hb.target = self.x.data_ptr()
         hb.recon = self.recon.data_ptr()
-        hb.coef = self.head_coef.data_ptr()
+        if self.fused_loss:
+            hb.coef = self.head_coef.data_ptr()
+        else:
+            hb.grad_recon = self.grad_recon.data_ptr()
         hb.dx = self.g_fin.data_ptr()
         hb.dx_epi = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin))
         hb.dx_epi.aux = self.fin.data_ptr()
@@ -393,7 +406,7 @@ class StepPlan:
         a.wt = net.w("decoder_input.weight")
         a.mulv = self.mulv.data_ptr()
         a.eps = self.eps.data_ptr()
-        a.kl_coef = self.kl_coef.data_ptr()
+        a.kl_coef = self.kl_coef.data_ptr() if self.fused_loss else None
         a.dmulv = self.dmulv.data_ptr()
         a.samples = self.S
         self._add(Bw, "vae_linear_bwd_data", a)
@@ -467,6 +480,14 @@ class StepPlan:
 
     def backward(self, stream=None):
         self._run(self.bwd_calls, stream if stream is not None else L.stream_ptr())
+
+    def encode(self, stream=None):
+        """encoder + fc_mu|fc_var only (mu | log_var land in self.mulv)."""
+        self._run(self.fwd_calls[:self.n_encode], stream if stream is not None else L.stream_ptr())
+
+    def decode(self, stream=None):
+        """decoder_input .. head from self.z (reconstruction lands in self.recon)."""
+        self._run(self.fwd_calls[self.n_decode0:self.n_decode1], stream if stream is not None else L.stream_ptr())
 
     def loss_dict(self) -> Dict[str, float]:
         o = self.out.tolist()
