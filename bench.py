@@ -115,29 +115,32 @@ def kernel_costs(plan, dsz):
 
 
 def time_kernels(plan, reps=20):
-    """Per-launch duration of every kernel of the step, each bracketed by HIP events on the
-    stream it runs on, queued behind a spin kernel so host launch latency is not measured."""
+    """Per-launch duration of every call of the step: `reps` back-to-back launches of the call
+    bracketed by HIP events on the stream it runs on, queued behind a spin kernel so host launch
+    latency is not measured; average per launch.  (The calls accumulate into the plan's gradient
+    buffers; this runs after the timed region and its loss terms were read.)"""
     from vae_amd import _lib as L
     st = torch.cuda.current_stream()
     sp = st.cuda_stream
     res = []
     for fn, ref in plan.fwd_calls + plan.bwd_calls:
-        times = []
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(400000)               # spin: everything below is queued behind it
+        e0.record(st)
         for _ in range(reps):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            torch.cuda._sleep(200000)           # ~100 µs spin: everything below is queued behind it
-            e0.record(st)
             if fn == "vae_reparam_fwd":
                 L.call(fn, *plan._reparam, sp)
             else:
                 L.call(fn, ref, sp)
-            e1.record(st)
-            torch.cuda.synchronize()
-            times.append(e0.elapsed_time(e1) * 1e3)   # µs
-        times.sort()
-        res.append((fn, ref, times[len(times) // 2]))
+        e1.record(st)
+        torch.cuda.synchronize()
+        res.append((fn, ref, e0.elapsed_time(e1) * 1e3 / reps))   # µs per launch
     return res
+
+
+# device symbols of the ABI calls with a kernel of their own (profiles/*pmc*.json is keyed by symbol)
+KERNEL_SYMBOL = {"vae_head_bwd": "head_bwd_mfma", "vae_head_fwd": "head_fwd_mfma", "vae_elbo_fwd": "elbo_kernel"}
 
 
 def pmc_traffic(kernel_symbol_hint: str):
@@ -275,7 +278,7 @@ def main():
     else:
         roof = {"bound": "hbm", "achieved": round(by / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    roof["traffic"] = pmc_traffic(fn)
+    roof["traffic"] = pmc_traffic(KERNEL_SYMBOL[fn]) if fn in KERNEL_SYMBOL else None
     roof["kernel"] = f"{fn} (launch #{idx} of the step)"
     roof["us_per_launch"] = round(us, 2)
     roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}

@@ -1,7 +1,8 @@
 // Host-side planning and launching of the implicit-GEMM kernels: tile shape, split-K, FastDiv
 // setup, slab workspace and the finalize pass.  Included by the entry-point translation units.
 #pragma once
-#include "vae_igemm.hpp"
+#include "vae_fgemm.hpp"
+#include <stdlib.h>
 
 #ifdef VAE_PROBE
 extern "C" unsigned long long* vae_probe_buffer(void);
@@ -227,6 +228,74 @@ inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
   return VAE_OK;
 }
 
+// ------------------------------------------------------------------ direct-fragment GEMM path
+// Shapes fgemm_kernel takes: k-contiguous weights (B_NK), gathered tensors with C % 32 == 0 (a
+// 32-deep k-step stays inside one tap), 16-byte aligned rows, packed BatchNorm channels.
+template <int AM, int BMD, int EM>
+inline bool fgemm_ok(const GemmParams& p, int esize_a, int esize_b) {
+  if constexpr (BMD != B_NK || AM == A_KM || EM == E_ACC) return false;
+  if (getenv("VAE_NO_FGEMM")) return false;
+  if (p.g_nchw || p.ones_col >= 0) return false;
+  // Measured (profiles/r1_v2_kernel_breakdown.txt): direct fragments win on the deep-K Linear
+  // shapes (fc_mu||fc_var 9.7 -> 4.0 us) but lose on the conv / convT ones, whose blocks run two
+  // residency rounds of latency-bound phases; those stay on the LDS-staged kernel unless asked.
+  if ((AM == A_CONV || AM == A_CONVT) && !getenv("VAE_FGEMM_CONV")) return false;
+  if (AM == A_CONV || AM == A_CONVT) {
+    if (p.gc % 32) return false;
+  } else {
+    if (p.K % 32 || p.a_ld % 8) return false;
+  }
+  if (p.b_ld % 8 || p.K % 32 && AM != A_CONVT) return false;
+  if (!aligned(p.a_ptr, 16) || !aligned(p.b_ptr, 16)) return false;
+  if (p.a_xf.kind == VAE_X_BN_DY && !aligned(p.a_xf.aux, 16)) return false;
+  if (bn_kind(p.a_xf) && p.a_xf.channels % 8) return false;
+  (void)esize_a; (void)esize_b;
+  return true;
+}
+
+template <class T, class TA, int AM, int EM, bool DYA>
+inline int launch_fgemm(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
+  constexpr int BM = 32, BN = 32;
+  const long ab = a_elems<AM>(p) * (long)sizeof(TA), bb = b_elems<B_NK>(p) * (long)sizeof(T);
+  if (ab <= 0 || bb <= 0 || ab >= (1l << 31) || bb >= (1l << 31))
+    return fail(VAE_E_UNSUPPORTED, "fgemm: operand of %ld / %ld bytes (buffer addressing needs < 2 GiB)", ab, bb);
+  p.a_bytes = (uint32_t)ab;
+  p.b_bytes = (uint32_t)bb;
+  if (EM != E_REPARAM) p.out_aux_bytes = (uint32_t)(out_elems(p) * (long)sizeof(T));
+  int kmax = p.K;
+  if (AM == A_CONVT) {
+    kmax = 0;
+    for (int ph = 0; ph < p.nphase; ++ph) {
+      const int k = p.ntap_h[ph / p.gs] * p.ntap_w[ph % p.gs] * p.gc;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  const int steps = (kmax + 31) / 32;
+  const long tiles = (long)((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * p.nphase;
+  // split-K over workgroups (slabs + igemm_finalize) until ~2 workgroups per CU, >= 4 k-steps
+  // per workgroup (one per wave)
+  int split = 1;
+  if (tiles < 2 * kCUs && ws) {
+    split = (int)((2 * kCUs + tiles - 1) / tiles);
+    if (split > steps / 4) split = steps / 4;
+    const long per = (long)p.M * p.N * p.nphase * 4;
+    if (split > ws_bytes / per) split = (int)(ws_bytes / per);
+    if (split < 2) split = 1;
+  }
+  p.ksplit = split;
+  p.slab = split > 1 ? static_cast<float*>(ws) : nullptr;
+#ifdef VAE_PROBE
+  p.probe = vae_probe_buffer();
+#endif
+  const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.nphase * p.ksplit);
+  const size_t lds = (size_t)(tab_floats(p.a_xf, false) + (EM == E_BNBWD ? tab_floats(p.epi_xf, true) : 0)) * 4;
+  hipLaunchKernelGGL((fgemm_kernel<T, TA, BM, BN, AM, EM, DYA>), grid, dim3(256), lds, st, p);
+  int rc = check_launch("fgemm");
+  if (rc) return rc;
+  if (p.slab) return launch_finalize<T, EM>(p, st);
+  return VAE_OK;
+}
+
 // Plan tile + split-K, then launch.  A_F32 / B_F32: instantiate the bf16 variant whose A / B
 // tensor is fp32 (the NCHW image, d[mu|logvar]).
 template <int AM, int BMD, int EM, bool DYA, bool DYB, bool A_F32 = false, bool B_F32 = false>
@@ -234,6 +303,12 @@ inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req
                   hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return VAE_OK;
   finish_divs(p);
+  if constexpr (BMD == B_NK && AM != A_KM && EM != E_ACC) {
+    if (!a_f32 && !b_f32 && split_req <= 0 && fgemm_ok<AM, BMD, EM>(p, 0, 0)) {
+      if (dtype == VAE_F32) return launch_fgemm<float, float, AM, EM, DYA>(p, ws, ws_bytes, st);
+      if (dtype == VAE_BF16) return launch_fgemm<__bf16, __bf16, AM, EM, DYA>(p, ws, ws_bytes, st);
+    }
+  }
   const Tile t = pick_tile(p.M, p.N, p.nphase);
   const int bk = dtype == VAE_F32 ? 32 : 64;
   int kmax = p.K;

@@ -6,5 +6,5 @@ cd /tmp && export TMPDIR=/tmp
 mkdir -p $R/gpurun_out
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/${TAG}_a -o run -- python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/${TAG}_a.log 2>&1 || exit $?
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM --output-format csv -d $R/gpurun_out/${TAG}_b -o run -- python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/${TAG}_b.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum TCC_MISS_sum --output-format csv -d $R/gpurun_out/${TAG}_c -o run -- python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/${TAG}_c.log 2>&1 || exit $?
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/${TAG}_d -o run -- python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/${TAG}_d.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/${TAG}_c -o run -- python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/${TAG}_c.log 2>&1 || exit $?
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --output-format csv -d $R/gpurun_out/${TAG}_d -o run -- python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph > $R/gpurun_out/${TAG}_d.log 2>&1
