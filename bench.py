@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
-    ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae"])
+    ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae", "vq"],
+                    help="vq: BASELINE.json configs[4], VQ-VAE B=128 (pass --batch 128)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -94,6 +95,12 @@ def head_cost(fn, a, dsz):
     return 2 * macs, x_b + 2 * img + 3 * a.c * 9 * 4
 
 
+def vq_cost(fn, a, dsz):
+    if fn == "vae_vq_fwd":       # distance GEMM rows x codes x dim (+ argmin, gather)
+        return 2 * a.rows * a.codes * a.dim, 2 * a.rows * a.dim * dsz + a.codes * a.dim * 4 + a.rows * 8
+    return 0, 3 * a.rows * a.dim * dsz + a.rows * 8 + a.codes * a.dim * 4
+
+
 def kernel_costs(plan, dsz):
     from vae_amd import _lib as L
     out = []
@@ -108,6 +115,8 @@ def kernel_costs(plan, dsz):
             f, b = linear_cost(fn, a, dsz)
         elif isinstance(a, L.HeadArgs):
             f, b = head_cost(fn, a, dsz)
+        elif isinstance(a, L.VqArgs):
+            f, b = vq_cost(fn, a, dsz)
         else:
             f, b = 0, 0
         out.append((fn, ref, f, b))
@@ -158,32 +167,38 @@ def pmc_traffic(kernel_symbol_hint: str):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(batch, seconds):
-    """The oracle's fp32 step (fwd + ELBO + bwd + Adam) on the host cores, bounded sample."""
+def cpu_baseline(batch, seconds, arch="vanilla"):
+    """The oracle's fp32 step (fwd + loss + bwd + Adam) on the host cores, bounded sample."""
     from oracle import vae_oracle as O
     threads = torch.get_num_threads()
-    sd = O.make_params(O.vanilla_param_spec(), 1265)
+    vq = arch == "vq"
+    sd = O.make_params(O.vq_param_spec() if vq else O.vanilla_param_spec(), 1265)
     P = {k: (v.clone().requires_grad_(True) if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))
              else v.clone()) for k, v in sd.items()}
     leaves = [v for v in P.values() if v.requires_grad]
     m = [torch.zeros_like(v) for v in leaves]
     v2 = [torch.zeros_like(v) for v in leaves]
     x, eps = O.make_inputs(batch, 128, 1265)
-    hd = O.DEFAULT_HIDDEN
 
     def step(it):
         stats = {}
-        mu, lv = O.vanilla_encode(P, x, hd, True, stats)
-        z = O.reparameterize(mu, lv, eps)
-        rec = O.vanilla_decode(P, z, hd, True, stats)
-        ld = O.vanilla_loss(rec, x, mu, lv, 1e-8)
+        if vq:
+            hd = O.VQ_HIDDEN
+            q, vq_loss, _, _ = O.vq_quantize(O.vq_encode(P, x, hd), P["vq_layer.embedding.weight"], 0.25)
+            rec = O.vq_decode(P, q, hd)
+            loss = torch.nn.functional.mse_loss(rec, x) + vq_loss
+        else:
+            hd = O.DEFAULT_HIDDEN
+            mu, lv = O.vanilla_encode(P, x, hd, True, stats)
+            z = O.reparameterize(mu, lv, eps)
+            rec = O.vanilla_decode(P, z, hd, True, stats)
+            loss = O.vanilla_loss(rec, x, mu, lv, 1e-8)["loss"]
         for t in leaves:
             t.grad = None
-        ld["loss"].backward()
+        loss.backward()
         with torch.no_grad():
             for i, t in enumerate(leaves):
                 O.adam_step(t, t.grad, m[i], v2[i], it, 0.005)
-        return ld
 
     step(1)
     n, t0 = 0, time.perf_counter()
@@ -193,8 +208,9 @@ def cpu_baseline(batch, seconds):
         el = time.perf_counter() - t0
         if el >= seconds or n >= 200:
             break
+    name = "VQVAE" if vq else "VanillaVAE"
     return {"value": round(n * batch / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"oracle VanillaVAE fp32 train step (fwd+ELBO+bwd+Adam), B={batch}, {n} steps / {el:.1f}s "
+            "sample": f"oracle {name} fp32 train step (fwd+loss+bwd+Adam), B={batch}, {n} steps / {el:.1f}s "
                       f"on {threads} threads ({os.cpu_count()} visible CPUs)"}
 
 
@@ -217,17 +233,24 @@ def main():
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     dsz = 2 if args.dtype == "bf16" else 4
     gen = torch.Generator().manual_seed(1265)                     # same init on every rank
-    net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
     S = 5 if args.arch == "iwae" else 1
-    loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
-    kld = {"vanilla": 1e-8, "betaH": 2.5e-4, "iwae": 2.5e-4}[args.arch]
-    lr = {"vanilla": 0.005, "betaH": 0.005, "iwae": 0.007}[args.arch]
-    plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S)
-    opt = FusedAdam(net, lr=lr)
+    if args.arch == "vq":
+        from vae_amd.vq import VQNet, VQStepPlan
+        net = VQNet(dtype=dtype, device="cuda", generator=gen)
+        plan = VQStepPlan(net, args.batch)
+        opt = FusedAdam(net, lr=0.001)                             # configs/vq_vae.yaml LR
+    else:
+        net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
+        loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
+        kld = {"vanilla": 1e-8, "betaH": 2.5e-4, "iwae": 2.5e-4}[args.arch]
+        lr = {"vanilla": 0.005, "betaH": 0.005, "iwae": 0.007}[args.arch]
+        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S)
+        opt = FusedAdam(net, lr=lr)
     # synthetic data resident in HBM (per-rank seed 1265+rank): U[0,1) images, N(0,1) eps
     g = torch.Generator(device="cuda").manual_seed(1265 + rank)
     plan.x.copy_(torch.rand(plan.x.shape, generator=g, device="cuda"))
-    plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
+    if hasattr(plan, "eps"):
+        plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
     step = TrainStep(net, plan, opt, graph=not args.no_graph)
 
     for _ in range(args.warmup):
@@ -286,12 +309,12 @@ def main():
 
     cpu = None
     if not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.batch, args.cpu_seconds)
+        cpu = cpu_baseline(args.batch, args.cpu_seconds, args.arch)
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
     line = {
-        "metric": METRIC,
+        "metric": METRIC if args.arch == "vanilla" else f"train images/sec {args.arch} 64x64 bs={args.batch} (1 GPU config)",
         "value": round(value, 1),
         "unit": "images/s",
         "n_gpus": world,
@@ -303,11 +326,14 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic: U[0,1) 64x64x3 images + N(0,1) eps resident in HBM, random-init weights",
-        "config": {"workload": f"{'VanillaVAE' if args.arch == 'vanilla' else args.arch} latent_dim=128 "
-                               f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}",
+        "config": {"workload": ("VQVAE embedding_dim=64 num_embeddings=512 64x64 train step (fwd+loss+bwd+Adam)"
+                                if args.arch == "vq" else
+                                f"{'VanillaVAE' if args.arch == 'vanilla' else args.arch} latent_dim=128 "
+                                f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}"),
                    "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                    "parallelism": f"dp{world}", "graph": not args.no_graph},
-        "elbo": {"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1], "KLD": loss_terms[2], "finite": finite},
+        "elbo": {"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1],
+                 ("VQ_Loss" if args.arch == "vq" else "KLD"): loss_terms[2], "finite": finite},
         "sum_kernel_us_isolated": round(step_kernel_us, 1),
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 4
+#define VAE_ABI_VERSION 5
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -115,7 +115,9 @@ typedef struct vae_conv_args {
   float* y_sumsq;
   int32_t sum_reps;        /* replicas of y_sum/y_sumsq (fwd) or dx_dgamma/dx_dbeta (bwd_data), */
   int32_t sum_rstride;     /* see vae_xform.reps; <= 1: one copy */
-  const void* residual;    /* fwd: optional y += xf(residual) (VQ-VAE ResidualLayer) */
+  const void* residual;    /* fwd: optional y += xf(residual) (VQ-VAE ResidualLayer,
+                              models/vq_vae.py:69); conv2d bwd_data: optional dx += residual (the
+                              gradient reaching x through the skip connection) before dx_epi */
   vae_xform residual_xf;
   /* backward */
   const void* dy;          /* gradient w.r.t. the layer output (stored, dtype) */
@@ -199,8 +201,9 @@ typedef struct vae_bn_args {
   float* db;
 } vae_bn_args;
 
-/* Loss kinds (vanilla_vae.py:124-146, beta_vae.py:129-152, iwae.py:129-160) */
-enum vae_loss_kind { VAE_LOSS_VANILLA = 0, VAE_LOSS_BETA_H = 1, VAE_LOSS_BETA_B = 2, VAE_LOSS_IWAE = 3 };
+/* Loss kinds (vanilla_vae.py:124-146, beta_vae.py:129-152, iwae.py:129-160, vq_vae.py:194-211) */
+enum vae_loss_kind { VAE_LOSS_VANILLA = 0, VAE_LOSS_BETA_H = 1, VAE_LOSS_BETA_B = 2, VAE_LOSS_IWAE = 3,
+                     VAE_LOSS_VQ = 4 };
 
 typedef struct vae_elbo_args {
   int32_t kind;            /* vae_loss_kind */
@@ -215,7 +218,55 @@ typedef struct vae_elbo_args {
   float* per_img;          /* [batch*samples] per-image MSE (experiment.py:60-62) */
   float* head_coef;        /* [batch*samples] dL/d(sse_i) for vae_head_bwd_* */
   float* kl_coef;          /* [batch*samples] per-row KL gradient coefficient */
+  /* VAE_LOSS_VQ (mulv / head_coef / kl_coef unused): loss = recon + VQ_Loss with
+   * VQ_Loss = (1 + vq_beta) * vq_sse / vq_elems (commitment*beta + embedding, vq_vae.py:47-50);
+   * out = {loss, Reconstruction_Loss, VQ_Loss, 0} */
+  const float* vq_sse;     /* [1] Σ(q - latents)^2 written by vae_vq_fwd */
+  float vq_beta;
+  float vq_elems;          /* number of latent elements (N*H*W*D) */
 } vae_elbo_args;
+
+/* VectorQuantizer (models/vq_vae.py:24-55) on NHWC latents [rows][dim] (rows = N*H*W, the
+ * reference's flat_latents after its permute, :25-27) against the fp32 codebook [codes][dim].
+ *   fwd: dist_k = (Σz² + Σ_e E_ke²) - 2 z·E_k in fp32 (the reference's formula, :30-32),
+ *        indices = argmin with the first-minimum tie-break of torch.argmin (:35), q = E[index]
+ *        written in `dtype` (the straight-through decoder input, :43,53), sse += Σ(q - z)².
+ *   bwd: g = dq + s*beta*2(z - q)/n  ->  dlat = g*act'(lat)  (commitment loss + straight-through,
+ *        :47,53; act' of lat_xf), dcodebook[index] += s*2(q - z)/n (embedding loss, :48), with
+ *        n = rows*dim and s = *loss_grad (dL/dVQ_Loss; 1 when NULL). */
+typedef struct vae_vq_args {
+  int32_t dtype;
+  int32_t rows, dim, codes;
+  const void* lat;         /* [rows][dim] stored encoder output (pre-activation, see lat_xf) */
+  vae_xform lat_xf;        /* NONE or ACT (the encoder's final LeakyReLU, vq_vae.py:117-121) */
+  const float* codebook;   /* fp32 [codes][dim] (vq_layer.embedding.weight) */
+  int64_t* indices;        /* fwd out [rows] */
+  void* q;                 /* fwd out [rows][dim] (dtype) */
+  float* sse;              /* fwd: [1] accumulated */
+  float beta;              /* commitment weight (0.25) */
+  const void* dq;          /* bwd: [rows][dim] dL/dq from the decoder (dtype) */
+  const float* loss_grad;  /* bwd: device scalar dL/dVQ_Loss, or NULL for 1 */
+  void* dlat;              /* bwd out [rows][dim] (dtype) */
+  float* dcodebook;        /* bwd: fp32 [codes][dim], accumulated */
+} vae_vq_args;
+
+/* Tanh output layer + reconstruction error on an NHWC pre-activation y [n,h,w,c] (the
+ * VQ-VAE decoder's last ConvTranspose2d + Tanh, vq_vae.py:156-160, and F.mse_loss at :203).
+ *   fwd: recon (fp32 NCHW) = tanh(y); sse[i] += Σ(recon - target)² per image; when dy is set
+ *        and grad_recon is NULL also dy = grad_scale*2(recon - target)*(1 - recon²)
+ *        (the fused-loss backward seed, grad_scale = dL/dΣ = 1/(n*c*h*w) for a mean).
+ *   bwd: dy = grad_recon*(1 - recon²) from a caller-supplied fp32 NCHW dL/drecon. */
+typedef struct vae_recon_args {
+  int32_t dtype;
+  int32_t n, h, w, c;
+  const void* y;
+  const float* target;     /* fp32 NCHW */
+  float* recon;            /* fp32 NCHW */
+  float* sse;              /* [n] accumulated */
+  void* dy;                /* NHWC (dtype) or NULL */
+  float grad_scale;
+  const float* grad_recon;
+} vae_recon_args;
 
 int vae_abi_version(void);
 const char* vae_last_error(void);
@@ -245,6 +296,12 @@ int vae_bn_finalize(const vae_bn_args* a, void* stream);
  *     row r uses mu row r/samples.  z is written in `dtype`. */
 int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int32_t latent,
                     const float* mulv, const float* eps, void* z, void* stream);
+/* --- VectorQuantizer (vq_vae.py:24-55), see vae_vq_args ------------------------------ */
+int vae_vq_fwd(const vae_vq_args* a, void* stream);
+int vae_vq_bwd(const vae_vq_args* a, void* stream);
+/* --- Tanh output + reconstruction SSE (vq_vae.py:156-160, :203), see vae_recon_args --- */
+int vae_recon_fwd(const vae_recon_args* a, void* stream);
+int vae_recon_bwd(const vae_recon_args* a, void* stream);
 /* --- ELBO terms + backward seeds (vanilla_vae.py:124-146 and variants) -------------- */
 int vae_elbo_fwd(const vae_elbo_args* a, void* stream);
 /* --- Adam (experiment.py:308-311; torch.optim.Adam semantics), flat fp32 buffers.

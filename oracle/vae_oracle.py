@@ -293,13 +293,15 @@ def vq_encode(P, x, hidden_dims):
     return h
 
 
-def vq_quantize(latents, E, beta):
+def vq_quantize(latents, E, beta, force_indices=None):
     """VectorQuantizer.forward — models/vq_vae.py:24-55.  Returns also the int64 indices
-    and the per-row distance gap d2-d1 (used to judge index exactness near ties)."""
+    and the per-row distance gap d2-d1 (used to judge index exactness near ties).
+    force_indices: teacher forcing — use these codes instead of the argmin (for checking the
+    rest of the step when a near-tie row resolved differently under another summation order)."""
     lat = latents.permute(0, 2, 3, 1).contiguous()
     flat = lat.view(-1, E.shape[1])
     dist = torch.sum(flat ** 2, dim=1, keepdim=True) + torch.sum(E ** 2, dim=1) - 2 * torch.matmul(flat, E.t())
-    inds = torch.argmin(dist, dim=1)
+    inds = torch.argmin(dist, dim=1) if force_indices is None else force_indices.to(torch.int64).view(-1)
     top2 = torch.topk(dist.detach(), 2, dim=1, largest=False).values
     gap = top2[:, 1] - top2[:, 0]
     q = E[inds].view(lat.shape)              # == one-hot @ E (exact)
@@ -356,7 +358,7 @@ TRAINABLE_KINDS = ("conv_w", "convT_w", "lin_w", "bias", "bn_w", "bn_b", "codebo
 
 def train_step(arch: str, sd, x, eps=None, *, M_N: float, lr: float = 0.005, hidden_dims=None,
                beta=4.0, gamma=1000.0, loss_type="H", max_capacity=25.0, Capacity_max_iter=1e5,
-               num_iter=1, vq_beta=0.25, do_adam=True, training=True):
+               num_iter=1, vq_beta=0.25, do_adam=True, training=True, vq_indices=None):
     """forward -> loss_function -> backward -> Adam on a copy of ``sd``.
 
     Returns a dict: outputs (recon, mu, log_var / vq_loss, indices), loss terms, per-image
@@ -392,7 +394,7 @@ def train_step(arch: str, sd, x, eps=None, *, M_N: float, lr: float = 0.005, hid
     elif arch == "VQVAE":
         hd = list(hidden_dims or VQ_HIDDEN)
         enc = vq_encode(P, x, hd)
-        q, vq_loss, inds, gap = vq_quantize(enc, P["vq_layer.embedding.weight"], vq_beta)
+        q, vq_loss, inds, gap = vq_quantize(enc, P["vq_layer.embedding.weight"], vq_beta, vq_indices)
         recon = vq_decode(P, q, hd)
         recons_loss = F.mse_loss(recon, x)
         ld = {"loss": recons_loss + vq_loss, "Reconstruction_Loss": recons_loss, "VQ_Loss": vq_loss}

@@ -21,7 +21,7 @@ extern "C" int vae_conv2d_fwd(const vae_conv_args* a, void* stream) {
 }
 
 // dx[n,h,w,c] = Σ_{r,s,k: h = p*S-P+r} dy'[n,p,q,k] · W[k][r][s][c]  (transposed conv of dy);
-// epilogue: g = dx·act'(z) of x's BatchNorm/LeakyReLU, Σg -> dβ, Σg·x̂ -> dγ
+// epilogue: [+ residual gradient], g = dx·act'(z) of x's BatchNorm/LeakyReLU, Σg -> dβ, Σg·x̂ -> dγ
 extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "conv2d_bwd_data") || !a->dy || !a->wt || !a->dx) return fail(VAE_E_BADARG, "conv2d_bwd_data: null tensor");
   if (!xf_ok(a->dy_xf, "conv2d_bwd_data.dy") || !epi_ok(a->dx_epi, "conv2d_bwd_data.epi")) return VAE_E_BADARG;
@@ -40,6 +40,7 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   p.out = a->dx; p.out_ld = a->c; p.out_phase = 1;
   p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
+  p.residual = a->residual;                                    // + gradient through a skip connection
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
   return launch<A_CONVT, B_KN, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
                                         (hipStream_t)stream);

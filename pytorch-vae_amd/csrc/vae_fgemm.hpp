@@ -286,13 +286,16 @@ __global__ void __launch_bounds__(256) fgemm_kernel(const GemmParams p) {
     return;
   } else {
     const rsrc_t raux = epi_aux_rsrc<EM>(p);
+    const rsrc_t rres = epi_res_rsrc<EM>(p);
+    const bool has_res = EM == E_BNBWD && p.residual != nullptr;
     const int ob = out_row_base(p, phase, row < p.M ? row : 0);
-    float aux[EPR], bias[EPR];
+    float aux[EPR], res[EPR], bias[EPR];
 #pragma unroll
     for (int e = 0; e < EPR; ++e) {
       const int col = n0 + col_l + e;
       const bool ok = row < p.M && col < p.N;
       aux[e] = ld_elem<T>(raux, ok ? (uint32_t)(ob + col) * (uint32_t)sizeof(T) : kOOB);
+      res[e] = has_res ? ld_elem<T>(rres, ok ? (uint32_t)(ob + col) * (uint32_t)sizeof(T) : kOOB) : 0.f;
       bias[e] = (EM == E_STORE && p.bias && col < p.N) ? p.bias[col] : 0.f;
     }
     float s1[EPR], s2[EPR];
@@ -300,7 +303,7 @@ __global__ void __launch_bounds__(256) fgemm_kernel(const GemmParams p) {
     for (int e = 0; e < EPR; ++e) {
       s1[e] = 0.f; s2[e] = 0.f;
       const int col = n0 + col_l + e;
-      if (row < p.M && col < p.N) epi_apply<T, EM>(p, te, col, ob + col, v[e], aux[e], bias[e], s1[e], s2[e]);
+      if (row < p.M && col < p.N) epi_apply<T, EM>(p, te, col, ob + col, v[e], aux[e], bias[e], s1[e], s2[e], res[e]);
     }
     if (epi_wants_sums<EM>(p)) {
       // lanes holding the same columns differ in the bits above log2(BN / EPR)

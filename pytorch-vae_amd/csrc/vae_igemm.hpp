@@ -686,11 +686,19 @@ __device__ __forceinline__ rsrc_t epi_aux_rsrc(const GemmParams& p) {
   return make_rsrc(ptr ? ptr : p.out, ptr ? p.out_aux_bytes : 0u);
 }
 
+// E_BNBWD: the gradient arriving through a residual connection, added before the activation
+// backward (an empty resource when there is none).
+template <int EM>
+__device__ __forceinline__ rsrc_t epi_res_rsrc(const GemmParams& p) {
+  const void* ptr = EM == E_BNBWD ? p.residual : nullptr;
+  return make_rsrc(ptr ? ptr : p.out, ptr ? p.out_aux_bytes : 0u);
+}
+
 // Epilogue of one element whose inputs (accumulator v, aux value, bias) are already in registers.
 // s1/s2 collect the per-column sums (BN statistics forward / BN-backward sums).
 template <class T, int EM>
 __device__ __forceinline__ void epi_apply(const GemmParams& p, const Tab& xe, int col, int idx, float v, float aux,
-                                          float bias, float& s1, float& s2) {
+                                          float bias, float& s1, float& s2, float res = 0.f) {
   if constexpr (EM == E_STORE) {
     float y = v + bias;
     if (p.residual) y += p.res_xf.kind == VAE_X_ACT ? lrelu(aux, p.res_xf.slope) : aux;
@@ -699,6 +707,7 @@ __device__ __forceinline__ void epi_apply(const GemmParams& p, const Tab& xe, in
     s1 += v;
     s2 += v * v;
   } else if constexpr (EM == E_BNBWD) {
+    v += res;                       // residual branch gradient (VQ-VAE ResidualLayer), 0 otherwise
     float g = v;
     if (p.epi_xf.kind == VAE_X_BN_ACT) {
       const int ch = (int)(col - p.fd_ech.div(col) * p.epi_xf.channels);
@@ -1094,8 +1103,10 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     } else {
       // pass 1: every load the epilogue needs (aux tensor, bias), before any store
       const rsrc_t raux = epi_aux_rsrc<EM>(p);
+      const rsrc_t rres = epi_res_rsrc<EM>(p);
+      const bool has_res = EM == E_BNBWD && p.residual != nullptr;
       int obase[TM][4];
-      float aux[TM][TN][4], bias[TN];
+      float aux[TM][TN][4], res[TM][TN][4], bias[TN];
 #pragma unroll
       for (int j = 0; j < TN; ++j) bias[j] = (EM == E_STORE && p.bias && colq + j * 16 < p.N) ? p.bias[colq + j * 16] : 0.f;
 #pragma unroll
@@ -1113,6 +1124,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
           for (int e = 0; e < 4; ++e) {
             const bool ok = rowq + i * 16 + e < p.M && colq + j * 16 < p.N;
             aux[i][j][e] = ld_elem<T>(raux, ok ? (uint32_t)(obase[i][e] + colq + j * 16) * (uint32_t)sizeof(T) : kOOB);
+            res[i][j][e] = has_res ? ld_elem<T>(rres, ok ? (uint32_t)(obase[i][e] + colq + j * 16) * (uint32_t)sizeof(T) : kOOB) : 0.f;
           }
       // pass 2: apply, store, per-column sums
       const bool want_sums = epi_wants_sums<EM>(p);
@@ -1127,7 +1139,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
           for (int e = 0; e < 4; ++e) {
             const int row = rowq + i * 16 + e;
             if (row >= p.M || !col_ok) continue;
-            epi_apply<T, EM>(p, te, col, obase[i][e] + col, acc[i][j][e], aux[i][j][e], bias[j], s1, s2);
+            epi_apply<T, EM>(p, te, col, obase[i][e] + col, acc[i][j][e], aux[i][j][e], bias[j], s1, s2, res[i][j][e]);
           }
         if (want_sums) {
           s1 += __shfl_xor(s1, 16);
@@ -1220,23 +1232,28 @@ __global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
     return;
   } else {
     const rsrc_t raux = epi_aux_rsrc<EM>(p);
+    const rsrc_t rres = epi_res_rsrc<EM>(p);
+    const bool has_res = EM == E_BNBWD && p.residual != nullptr;
     int obase[FIN_RPT];
-    float aux[FIN_RPT][4], bias[4];
+    float aux[FIN_RPT][4], res[FIN_RPT][4], bias[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) bias[c] = (EM == E_STORE && p.bias && col0 + c < p.N) ? p.bias[col0 + c] : 0.f;
 #pragma unroll
     for (int r = 0; r < FIN_RPT; ++r) {
       obase[r] = out_row_base(p, phase[r], row[r]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        aux[r][c] = ld_elem<T>(raux, rok[r] && col0 + c < p.N ? (uint32_t)(obase[r] + col0 + c) * (uint32_t)sizeof(T) : kOOB);
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t off = rok[r] && col0 + c < p.N ? (uint32_t)(obase[r] + col0 + c) * (uint32_t)sizeof(T) : kOOB;
+        aux[r][c] = ld_elem<T>(raux, off);
+        res[r][c] = has_res ? ld_elem<T>(rres, off) : 0.f;
+      }
     }
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < FIN_RPT; ++r)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        if (rok[r] && col0 + c < p.N) epi_apply<T, EM>(p, te, col0 + c, obase[r] + col0 + c, v[r][c], aux[r][c], bias[c], s1[c], s2[c]);
+        if (rok[r] && col0 + c < p.N) epi_apply<T, EM>(p, te, col0 + c, obase[r] + col0 + c, v[r][c], aux[r][c], bias[c], s1[c], s2[c], res[r][c]);
     if (epi_wants_sums<EM>(p)) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) { r1[rl][cq * 4 + c] = s1[c]; r2[rl][cq * 4 + c] = s2[c]; }

@@ -245,7 +245,7 @@ inline bool fgemm_ok(const GemmParams& p, int esize_a, int esize_b) {
   } else {
     if (p.K % 32 || p.a_ld % 8) return false;
   }
-  if (p.b_ld % 8 || p.K % 32 && AM != A_CONVT) return false;
+  if (p.b_ld % 8 || (p.K % 32 && AM != A_CONVT)) return false;
   if (!aligned(p.a_ptr, 16) || !aligned(p.b_ptr, 16)) return false;
   if (p.a_xf.kind == VAE_X_BN_DY && !aligned(p.a_xf.aux, 16)) return false;
   if (bn_kind(p.a_xf) && p.a_xf.channels % 8) return false;

@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
   const int B = a.batch, S = a.samples > 0 ? a.samples : 1, D = a.latent;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // kld_b = -0.5 Σ_d (1 + lv - mu^2 - exp(lv))  (one wave per row)
-  for (int b = wv; b < B; b += 4) {
+  for (int b = wv; b < B && a.kind != VAE_LOSS_VQ; b += 4) {
     float s = 0.f;
     for (int d = lane; d < D; d += 64) {
       const float mu = a.mulv[(long)b * 2 * D + d], lv = a.mulv[(long)b * 2 * D + D + d];
@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
   // totals: Σ sse, Σ kld_b
   float ts = 0.f, tk = 0.f;
   for (int i = threadIdx.x; i < B * S; i += 256) ts += a.sse[i];
-  for (int b = threadIdx.x; b < B; b += 256) tk += kld_row[b];
+  for (int b = threadIdx.x; b < B && a.kind != VAE_LOSS_VQ; b += 256) tk += kld_row[b];
   for (int off = 32; off > 0; off >>= 1) { ts += __shfl_xor(ts, off); tk += __shfl_xor(tk, off); }
   if (lane == 0) { red[0][wv] = ts; red[1][wv] = tk; }
   __syncthreads();
@@ -415,6 +415,12 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
   const float kld_mean = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)B;
   for (int i = threadIdx.x; i < B * S; i += 256) a.per_img[i] = a.sse[i] * inv_img;
 
+  if (a.kind == VAE_LOSS_VQ) {                  // vq_vae.py:203-211
+    const float recon = sse_tot / ((float)B * (float)a.img_elems);
+    const float vq = (1.f + a.vq_beta) * (*a.vq_sse) / a.vq_elems;
+    if (threadIdx.x == 0) { a.out[0] = recon + vq; a.out[1] = recon; a.out[2] = vq; a.out[3] = 0.f; }
+    return;
+  }
   if (a.kind != VAE_LOSS_IWAE) {
     const float recon = sse_tot / ((float)B * (float)a.img_elems);
     float loss, klc, kld_report;
@@ -618,9 +624,15 @@ extern "C" int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int
 }
 
 extern "C" int vae_elbo_fwd(const vae_elbo_args* a, void* stream) {
-  if (!a || !a->mulv || !a->sse || !a->out || !a->per_img || !a->head_coef || !a->kl_coef) return fail(VAE_E_BADARG, "elbo_fwd: args");
-  if (a->batch <= 0 || a->batch > 1024 || a->latent <= 0 || a->img_elems <= 0) return fail(VAE_E_BADSHAPE, "elbo_fwd: sizes");
-  if (a->kind < VAE_LOSS_VANILLA || a->kind > VAE_LOSS_IWAE) return fail(VAE_E_BADARG, "elbo_fwd: kind");
+  if (!a || !a->sse || !a->out || !a->per_img) return fail(VAE_E_BADARG, "elbo_fwd: args");
+  if (a->kind < VAE_LOSS_VANILLA || a->kind > VAE_LOSS_VQ) return fail(VAE_E_BADARG, "elbo_fwd: kind");
+  if (a->kind == VAE_LOSS_VQ) {
+    if (!a->vq_sse || !(a->vq_elems > 0.f)) return fail(VAE_E_BADARG, "elbo_fwd: vq_sse / vq_elems");
+    if (a->batch <= 0 || a->img_elems <= 0 || (a->samples > 1)) return fail(VAE_E_BADSHAPE, "elbo_fwd: sizes");
+  } else {
+    if (!a->mulv || !a->head_coef || !a->kl_coef) return fail(VAE_E_BADARG, "elbo_fwd: args");
+    if (a->batch <= 0 || a->batch > 1024 || a->latent <= 0 || a->img_elems <= 0) return fail(VAE_E_BADSHAPE, "elbo_fwd: sizes");
+  }
   hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *a);
   return check_launch("elbo_fwd");
 }

@@ -18,11 +18,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
-LOSS_VANILLA, LOSS_BETA_H, LOSS_BETA_B, LOSS_IWAE = 0, 1, 2, 3
+LOSS_VANILLA, LOSS_BETA_H, LOSS_BETA_B, LOSS_IWAE, LOSS_VQ = 0, 1, 2, 3, 4
 
 
 class VaeHipError(RuntimeError):
@@ -77,7 +77,20 @@ class ElboArgs(ctypes.Structure):
                 ("img_elems", c_int32), ("kld_weight", c_float), ("beta", c_float), ("gamma", c_float),
                 ("c_max", c_float), ("c_stop_iter", c_float), ("iter", c_void_p), ("mulv", c_void_p),
                 ("sse", c_void_p), ("out", c_void_p), ("per_img", c_void_p), ("head_coef", c_void_p),
-                ("kl_coef", c_void_p)]
+                ("kl_coef", c_void_p), ("vq_sse", c_void_p), ("vq_beta", c_float), ("vq_elems", c_float)]
+
+
+class VqArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("rows", c_int32), ("dim", c_int32), ("codes", c_int32),
+                ("lat", c_void_p), ("lat_xf", Xform), ("codebook", c_void_p), ("indices", c_void_p),
+                ("q", c_void_p), ("sse", c_void_p), ("beta", c_float), ("dq", c_void_p), ("loss_grad", c_void_p),
+                ("dlat", c_void_p), ("dcodebook", c_void_p)]
+
+
+class ReconArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
+                ("y", c_void_p), ("target", c_void_p), ("recon", c_void_p), ("sse", c_void_p), ("dy", c_void_p),
+                ("grad_scale", c_float), ("grad_recon", c_void_p)]
 
 
 class BnArgs(ctypes.Structure):
@@ -104,6 +117,10 @@ _SIGS = {
     "vae_bn_finalize": [POINTER(BnArgs), c_void_p],
     "vae_reparam_fwd": [c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p],
     "vae_elbo_fwd": [POINTER(ElboArgs), c_void_p],
+    "vae_vq_fwd": [POINTER(VqArgs), c_void_p],
+    "vae_vq_bwd": [POINTER(VqArgs), c_void_p],
+    "vae_recon_fwd": [POINTER(ReconArgs), c_void_p],
+    "vae_recon_bwd": [POINTER(ReconArgs), c_void_p],
     "vae_adam_step": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float,
                       c_float, c_float, c_void_p, c_void_p],
     "vae_cast_bf16": [c_int64, c_void_p, c_void_p, c_void_p],

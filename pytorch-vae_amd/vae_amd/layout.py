@@ -195,6 +195,62 @@ def vanilla_layout(in_channels: int, latent_dim: int, hidden_dims: List[int]) ->
     return L
 
 
+def vq_layout(in_channels: int, embedding_dim: int, num_embeddings: int, hidden_dims: List[int]) -> Layout:
+    """VQVAE (models/vq_vae.py:73-166): the reference's parameters in backward completion order
+    (decoder output layer first, codebook, encoder last), each weight followed by its bias.
+    No BatchNorm.  The codebook stays fp32 for the VectorQuantizer kernels."""
+    spec = vq_param_spec(in_channels, embedding_dim, num_embeddings, hidden_dims)
+    L = Layout()
+    groups: List[List[PSpec]] = []
+    for name, shape, kind in spec:
+        ps = PSpec(name, tuple(shape), kind, gemm_weight=kind in ("conv_w", "convT_w"))
+        if kind == "bias":
+            groups[-1].append(ps)
+        else:
+            groups.append([ps])
+    dec = [g for g in groups if g[0].name.startswith("decoder.")]
+    cb = [g for g in groups if g[0].name.startswith("vq_layer.")]
+    enc = [g for g in groups if g[0].name.startswith("encoder.")]
+    for g in dec[::-1] + cb + enc[::-1]:
+        L.params += g
+    return L.finalize()
+
+
+def vq_param_spec(in_channels: int, embedding_dim: int, num_embeddings: int, hidden_dims: List[int]):
+    """(name, reference shape, kind) of every VQVAE parameter in the reference's registration
+    order (vq_vae.py:94-166; Sequential indices include the parameter-free LeakyReLUs)."""
+    h = list(hidden_dims)
+    spec = []
+    cin, idx = in_channels, 0
+    for hd in h:                                                    # :95-102 Conv k4 s2 p1
+        spec += [(f"encoder.{idx}.0.weight", (hd, cin, 4, 4), "conv_w"), (f"encoder.{idx}.0.bias", (hd,), "bias")]
+        cin, idx = hd, idx + 1
+    spec += [(f"encoder.{idx}.0.weight", (cin, cin, 3, 3), "conv_w"), (f"encoder.{idx}.0.bias", (cin,), "bias")]
+    idx += 1
+    for _ in range(6):                                              # :111-112 ResidualLayer
+        spec += [(f"encoder.{idx}.resblock.0.weight", (cin, cin, 3, 3), "conv_w"),
+                 (f"encoder.{idx}.resblock.2.weight", (cin, cin, 1, 1), "conv_w")]
+        idx += 1
+    idx += 1                                                        # :113 LeakyReLU
+    spec += [(f"encoder.{idx}.0.weight", (embedding_dim, cin, 1, 1), "conv_w"),
+             (f"encoder.{idx}.0.bias", (embedding_dim,), "bias")]
+    spec += [("vq_layer.embedding.weight", (num_embeddings, embedding_dim), "codebook")]
+    spec += [("decoder.0.0.weight", (h[-1], embedding_dim, 3, 3), "conv_w"), ("decoder.0.0.bias", (h[-1],), "bias")]
+    idx = 1
+    for _ in range(6):
+        spec += [(f"decoder.{idx}.resblock.0.weight", (h[-1], h[-1], 3, 3), "conv_w"),
+                 (f"decoder.{idx}.resblock.2.weight", (h[-1], h[-1], 1, 1), "conv_w")]
+        idx += 1
+    idx += 1                                                        # LeakyReLU
+    r = h[::-1]
+    for i in range(len(r) - 1):                                     # :142-152 ConvT k4 s2 p1
+        spec += [(f"decoder.{idx}.0.weight", (r[i], r[i + 1], 4, 4), "convT_w"),
+                 (f"decoder.{idx}.0.bias", (r[i + 1],), "bias")]
+        idx += 1
+    spec += [(f"decoder.{idx}.0.weight", (r[-1], 3, 4, 4), "convT_w"), (f"decoder.{idx}.0.bias", (3,), "bias")]
+    return spec
+
+
 def reference_key_order(in_channels: int, latent_dim: int, hidden_dims: List[int]) -> List[str]:
     """The reference's state_dict key order (module registration order, vanilla_vae.py:20-75)."""
     h = list(hidden_dims)

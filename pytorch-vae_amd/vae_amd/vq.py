@@ -1,0 +1,398 @@
+"""VQ-VAE on libvaehip: the reference's VQVAE (models/vq_vae.py:73-211) training step.
+
+Network (hidden_dims default [128, 256], embedding_dim 64, num_embeddings 512, 64x64 images):
+  encoder  Conv(k4,s2,p1)+LReLU per hidden dim (:95-102), Conv3x3+LReLU (:104-109),
+           6 x ResidualLayer x + Conv1x1(ReLU(Conv3x3(x))) (:57-70, :111-112), LReLU (:113),
+           Conv1x1 -> embedding_dim + LReLU (:115-121)
+  vq_layer VectorQuantizer (:24-55): argmin over the codebook, straight-through estimator
+  decoder  Conv3x3+LReLU (:128-135), 6 x ResidualLayer, LReLU, ConvT(k4,s2,p1)+LReLU per
+           reversed hidden dim (:142-152), ConvT(k4,s2,p1) -> 3 + Tanh (:154-160)
+  loss     mse(recon, x) + vq_loss (:194-211)
+
+Same design as the VanillaVAE plan (net.py): NHWC activations stored before their activation
+(every LeakyReLU / ReLU is applied by the consuming kernel on load, and its backward by the
+producing kernel's epilogue); residual adds fused into the 1x1 conv epilogue forward and into
+the 3x3 conv data-gradient epilogue backward; the VectorQuantizer, the Tanh output and the
+loss are their own small kernels.  All convolutions are MFMA implicit GEMMs (vae_igemm.hpp).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import torch
+
+from . import _lib as L
+from .layout import Layout, default_init, vq_layout, vq_param_spec
+from .net import SLOPE, WORKSPACE_BYTES, _pad4
+
+NRES = 6             # ResidualLayers per stack (vq_vae.py:111, :138)
+
+
+class VQNet:
+    """Parameters of the VQVAE on one device (flat fp32 master + bf16 GEMM copy)."""
+
+    def __init__(self, in_channels: int = 3, embedding_dim: int = 64, num_embeddings: int = 512,
+                 hidden_dims: Optional[List[int]] = None, img_size: int = 64, dtype: torch.dtype = torch.float32,
+                 device=None, generator: Optional[torch.Generator] = None):
+        if in_channels != 3:
+            raise ValueError("the output layer reconstructs 3 channels (vq_vae.py:156); in_channels must be 3")
+        self.in_channels = in_channels
+        self.embedding_dim = embedding_dim
+        self.num_embeddings = num_embeddings
+        self.hidden_dims = list(hidden_dims or [128, 256])
+        self.img_size = img_size
+        if img_size % (2 ** len(self.hidden_dims)):
+            raise ValueError("img_size must be divisible by 2**len(hidden_dims)")
+        self.dtype = dtype
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.layout: Layout = vq_layout(in_channels, embedding_dim, num_embeddings, self.hidden_dims)
+        self.ref_order = [n for n, _, _ in vq_param_spec(in_channels, embedding_dim, num_embeddings, self.hidden_dims)]
+        cpu_p = torch.zeros(self.layout.total)
+        default_init(self.layout, cpu_p, torch.zeros(0), generator)
+        self.params = cpu_p.to(self.device)
+        self.running = torch.zeros(1, dtype=torch.float32, device=self.device)   # no BatchNorm
+        self.lowp = (torch.zeros(self.layout.total, dtype=torch.bfloat16, device=self.device)
+                     if dtype == torch.bfloat16 else None)
+        self.num_batches_tracked = 0
+        self.sync_lowp()
+
+    @property
+    def dcode(self) -> int:
+        return L.dtype_code(self.dtype)
+
+    def sync_lowp(self):
+        if self.lowp is not None:
+            L.call("vae_cast_bf16", self.params.numel(), self.params.data_ptr(), self.lowp.data_ptr(), L.stream_ptr())
+
+    def load_reference_state_dict(self, sd: Dict[str, torch.Tensor]):
+        self.layout.load_reference(self.params, self.running, {k: v.to(self.device) for k, v in sd.items()})
+        self.sync_lowp()
+
+    def reference_state_dict(self) -> Dict[str, torch.Tensor]:
+        return self.layout.export_reference(self.params, None, 0, self.ref_order)
+
+    def p(self, name: str) -> int:
+        s = self.layout.by_name[name]
+        return self.params.data_ptr() + 4 * s.offset
+
+    def w(self, name: str) -> int:
+        s = self.layout.by_name[name]
+        if self.lowp is not None:
+            return self.lowp.data_ptr() + 2 * s.offset
+        return self.params.data_ptr() + 4 * s.offset
+
+
+def _act(slope: float = SLOPE, aux: Optional[torch.Tensor] = None) -> L.Xform:
+    xf = L.Xform(kind=L.X_ACT, channels=1, slope=slope)
+    if aux is not None:
+        xf.aux = aux.data_ptr()
+    return xf
+
+
+class VQStepPlan:
+    """Buffers and prebuilt launches of one VQ-VAE training step for a fixed batch.
+
+    grads land in `self.grads` (net.params layout); `zero` (grads, per-image SSE, the VQ SSE)
+    is cleared by vae_step_begin.  fused_loss=False (the BaseVAE drop-in) seeds the backward
+    from `grad_recon` (dL/drecon) and `vq_grad` (dL/dvq_loss) instead of the fixed loss."""
+
+    loss_kind = L.LOSS_VQ
+
+    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True):
+        self.net, self.B, self.beta, self.fused_loss = net, batch, beta, fused_loss
+        dev, T = net.device, net.dtype
+        h, E, img = net.hidden_dims, net.embedding_dim, net.img_size
+        B = batch
+        self._keep = []
+        f32 = dict(dtype=torch.float32, device=dev)
+        act = dict(dtype=T, device=dev)
+        self.x = torch.zeros(B, 3, img, img, **f32)
+        sp = img
+        self.enc = []
+        for c in h:
+            sp //= 2
+            self.enc.append(torch.empty(B, sp, sp, c, **act))
+        self.s, C = sp, h[-1]
+        self.lat_hw = sp
+        m = (B, sp, sp, C)
+        self.e_in = torch.empty(*m, **act)                          # encoder Conv3x3 output
+        self.e_t = [torch.empty(*m, **act) for _ in range(NRES)]    # residual Conv3x3 outputs
+        self.e_h = [torch.empty(*m, **act) for _ in range(NRES)]    # residual layer outputs
+        self.latpre = torch.empty(B, sp, sp, E, **act)
+        self.q = torch.empty(B, sp, sp, E, **act)
+        self.indices = torch.zeros(B * sp * sp, dtype=torch.int64, device=dev)
+        self.d_in = torch.empty(*m, **act)
+        self.d_t = [torch.empty(*m, **act) for _ in range(NRES)]
+        self.d_h = [torch.empty(*m, **act) for _ in range(NRES)]
+        r = h[::-1]
+        self.up = []
+        s2 = sp
+        for i in range(len(r) - 1):
+            s2 *= 2
+            self.up.append(torch.empty(B, s2, s2, r[i + 1], **act))
+        self.y = torch.empty(B, img, img, 3, **act)                 # pre-Tanh output
+        self.recon = torch.empty(B, 3, img, img, **f32)
+        self.grad_recon = None if fused_loss else torch.zeros(B, 3, img, img, **f32)
+        self.vq_grad = torch.ones(1, **f32)
+        self.out = torch.zeros(4, **f32)
+        self.per_img = torch.zeros(B, **f32)
+        self.num_iter = torch.zeros(1, **f32)
+        # backward buffers
+        self.g_y = torch.empty_like(self.y)
+        self.g_up = [torch.empty_like(t) for t in self.up]
+        self.g_h = [torch.empty(*m, **act) for _ in range(2)]       # ping-pong residual-stream grads
+        self.g_t = torch.empty(*m, **act)
+        self.g_q = torch.empty_like(self.q)
+        self.g_lat = torch.empty_like(self.latpre)
+        self.g_enc = [torch.empty_like(t) for t in self.enc]
+        nz = net.layout.total + _pad4(B) + 4
+        self.zero = torch.zeros(nz, **f32)
+        o = 0
+        self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
+        self.sse = self.zero[o:o + B]; o += _pad4(B)
+        self.vq_sse = self.zero[o:o + 1]
+        self.step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
+        self.fwd_calls: List = []
+        self.bwd_calls: List = []
+        self._build()
+
+    # ------------------------------------------------------------------ helpers
+    def g(self, name: str) -> int:
+        s = self.net.layout.by_name[name]
+        return self.grads.data_ptr() + 4 * s.offset
+
+    def _add(self, lst, fn, arg):
+        if isinstance(arg, L.ConvArgs):
+            arg.workspace = self.workspace.data_ptr()
+            arg.workspace_bytes = self.workspace.numel() * 4
+        self._keep.append(arg)
+        lst.append((fn, ctypes.byref(arg)))
+
+    def _conv(self, t_in, cin, cout, r, stride, pad, transposed=False):
+        n, hh, ww = t_in.shape[0], t_in.shape[1], t_in.shape[2]
+        if transposed:
+            p = q = hh * stride
+        else:
+            p = q = (hh + 2 * pad - r) // stride + 1
+        return L.ConvArgs(dtype=self.net.dcode, n=n, h=hh, w=ww, c=cin, k=cout, p=p, q=q, r=r, stride=stride, pad=pad)
+
+    def _res_stack(self, pre: str, first_idx: int, x0: torch.Tensor, ts, hs):
+        """Forward of the 6 ResidualLayers on input lrelu(x0): t_j = Conv3x3(h_j),
+        h_{j+1} = h_j + Conv1x1(relu(t_j)) (vq_vae.py:57-70)."""
+        F, net = self.fwd_calls, self.net
+        C = x0.shape[3]
+        for j in range(NRES):
+            idx = first_idx + j
+            hin, hin_xf = (x0, _act()) if j == 0 else (hs[j - 1], L.Xform())
+            a = self._conv(hin, C, C, 3, 1, 1)
+            a.x, a.x_xf = hin.data_ptr(), hin_xf
+            a.wt = net.w(f"{pre}.{idx}.resblock.0.weight")
+            a.y = ts[j].data_ptr()
+            self._add(F, "vae_conv2d_fwd", a)
+            b = self._conv(ts[j], C, C, 1, 1, 0)
+            b.x, b.x_xf = ts[j].data_ptr(), _act(0.0)                       # ReLU(True), :66
+            b.wt = net.w(f"{pre}.{idx}.resblock.2.weight")
+            b.residual, b.residual_xf = hin.data_ptr(), (_act() if j == 0 else L.Xform())
+            b.y = hs[j].data_ptr()
+            self._add(F, "vae_conv2d_fwd", b)
+
+    def _res_stack_bwd(self, pre: str, first_idx: int, x0: torch.Tensor, ts, hs, gi: int) -> int:
+        """Backward of the residual stack.  g_h[gi] holds dL/dh_6 on entry; returns the index of
+        the buffer holding dL/dx0 (the gradient w.r.t. the stored pre-activation x0)."""
+        Bw, net = self.bwd_calls, self.net
+        C = x0.shape[3]
+        for j in reversed(range(NRES)):
+            idx = first_idx + j
+            dh, dnext = self.g_h[gi], self.g_h[1 - gi]
+            hin, hin_xf = (x0, _act()) if j == 0 else (hs[j - 1], L.Xform())
+            # Conv1x1: dt = W1^T dh * relu'(t)
+            a = self._conv(ts[j], C, C, 1, 1, 0)
+            a.dy, a.wt = dh.data_ptr(), net.w(f"{pre}.{idx}.resblock.2.weight")
+            a.dx, a.dx_epi = self.g_t.data_ptr(), _act(0.0, ts[j])
+            self._add(Bw, "vae_conv2d_bwd_data", a)
+            f = self._conv(ts[j], C, C, 1, 1, 0)
+            f.x, f.x_xf = ts[j].data_ptr(), _act(0.0)
+            f.dy, f.dw = dh.data_ptr(), self.g(f"{pre}.{idx}.resblock.2.weight")
+            self._add(Bw, "vae_conv2d_bwd_filter", f)
+            # Conv3x3: dh_j = W3^T * dt + dh (skip connection) [* lrelu'(x0) for j == 0]
+            a = self._conv(hin, C, C, 3, 1, 1)
+            a.dy, a.wt = self.g_t.data_ptr(), net.w(f"{pre}.{idx}.resblock.0.weight")
+            a.dx, a.residual = dnext.data_ptr(), dh.data_ptr()
+            if j == 0:
+                a.dx_epi = _act(SLOPE, x0)
+            self._add(Bw, "vae_conv2d_bwd_data", a)
+            f = self._conv(hin, C, C, 3, 1, 1)
+            f.x, f.x_xf = hin.data_ptr(), hin_xf
+            f.dy, f.dw = self.g_t.data_ptr(), self.g(f"{pre}.{idx}.resblock.0.weight")
+            self._add(Bw, "vae_conv2d_bwd_filter", f)
+            gi = 1 - gi
+        return gi
+
+    # ------------------------------------------------------------------ plan
+    def _build(self):
+        net = self.net
+        h, E, K = net.hidden_dims, net.embedding_dim, net.num_embeddings
+        nh = len(h)
+        B, img = self.B, net.img_size
+        C = h[-1]
+        F = self.fwd_calls
+        # ---------------------------------------------------------------- encoder
+        for i in range(nh):
+            src = self.x if i == 0 else self.enc[i - 1]
+            cin = 3 if i == 0 else h[i - 1]
+            a = L.ConvArgs(dtype=net.dcode, n=B, h=src.shape[2], w=src.shape[3] if i == 0 else src.shape[2], c=cin,
+                           k=h[i], p=self.enc[i].shape[1], q=self.enc[i].shape[2], r=4, stride=2, pad=1)
+            if i == 0:
+                a.h = a.w = img
+                a.x_nchw_f32, a.x = 1, self.x.data_ptr()
+            else:
+                a.x, a.x_xf = src.data_ptr(), _act()
+            a.wt, a.bias = net.w(f"encoder.{i}.0.weight"), net.p(f"encoder.{i}.0.bias")
+            a.y = self.enc[i].data_ptr()
+            self._add(F, "vae_conv2d_fwd", a)
+        a = self._conv(self.enc[-1], C, C, 3, 1, 1)
+        a.x, a.x_xf = self.enc[-1].data_ptr(), _act()
+        a.wt, a.bias = net.w(f"encoder.{nh}.0.weight"), net.p(f"encoder.{nh}.0.bias")
+        a.y = self.e_in.data_ptr()
+        self._add(F, "vae_conv2d_fwd", a)
+        self._res_stack("encoder", nh + 1, self.e_in, self.e_t, self.e_h)
+        ilat = nh + 1 + NRES + 1
+        a = self._conv(self.e_h[-1], C, E, 1, 1, 0)
+        a.x, a.x_xf = self.e_h[-1].data_ptr(), _act()
+        a.wt, a.bias = net.w(f"encoder.{ilat}.0.weight"), net.p(f"encoder.{ilat}.0.bias")
+        a.y = self.latpre.data_ptr()
+        self._add(F, "vae_conv2d_fwd", a)
+        self.n_encode = len(F)
+        # ---------------------------------------------------------------- vector quantizer
+        v = L.VqArgs(dtype=net.dcode, rows=B * self.s * self.s, dim=E, codes=K, beta=self.beta)
+        v.lat, v.lat_xf = self.latpre.data_ptr(), _act()
+        v.codebook = net.p("vq_layer.embedding.weight")
+        v.indices, v.q, v.sse = self.indices.data_ptr(), self.q.data_ptr(), self.vq_sse.data_ptr()
+        v.dq, v.dlat = self.g_q.data_ptr(), self.g_lat.data_ptr()
+        v.loss_grad = None if self.fused_loss else self.vq_grad.data_ptr()
+        v.dcodebook = self.g("vq_layer.embedding.weight")
+        self._add(F, "vae_vq_fwd", v)
+        self.n_decode0 = len(F)
+        # ---------------------------------------------------------------- decoder
+        a = self._conv(self.q, E, C, 3, 1, 1)
+        a.x = self.q.data_ptr()
+        a.wt, a.bias = net.w("decoder.0.0.weight"), net.p("decoder.0.0.bias")
+        a.y = self.d_in.data_ptr()
+        self._add(F, "vae_conv2d_fwd", a)
+        self._res_stack("decoder", 1, self.d_in, self.d_t, self.d_h)
+        r = h[::-1]
+        iup = 1 + NRES + 1
+        src = self.d_h[-1]
+        for i in range(len(r)):
+            last = i == len(r) - 1
+            dst = self.y if last else self.up[i]
+            cout = 3 if last else r[i + 1]
+            a = self._conv(src, r[i], cout, 4, 2, 1, transposed=True)
+            a.x, a.x_xf = src.data_ptr(), _act()
+            a.wt, a.bias = net.w(f"decoder.{iup + i}.0.weight"), net.p(f"decoder.{iup + i}.0.bias")
+            a.y = dst.data_ptr()
+            self._add(F, "vae_convT2d_fwd", a)
+            src = dst
+        # ---------------------------------------------------------------- Tanh + SSE + loss
+        rc = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3)
+        rc.y, rc.target, rc.recon, rc.sse = self.y.data_ptr(), self.x.data_ptr(), self.recon.data_ptr(), self.sse.data_ptr()
+        if self.fused_loss:
+            rc.dy, rc.grad_scale = self.g_y.data_ptr(), 1.0 / (B * 3 * img * img)
+        self._add(F, "vae_recon_fwd", rc)
+        self.n_decode1 = len(F)
+        e = L.ElboArgs(kind=L.LOSS_VQ, batch=B, samples=1, latent=1, img_elems=3 * img * img,
+                       vq_beta=self.beta, vq_elems=float(B * self.s * self.s * E))
+        e.sse, e.out, e.per_img, e.vq_sse = self.sse.data_ptr(), self.out.data_ptr(), self.per_img.data_ptr(), self.vq_sse.data_ptr()
+        if self.fused_loss:
+            self._add(F, "vae_elbo_fwd", e)
+
+        # ================================================================ backward
+        Bw = self.bwd_calls
+        if not self.fused_loss:
+            rb = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3)
+            rb.target, rb.recon = self.x.data_ptr(), self.recon.data_ptr()
+            rb.dy, rb.grad_recon = self.g_y.data_ptr(), self.grad_recon.data_ptr()
+            self._add(Bw, "vae_recon_bwd", rb)
+        ups = [self.d_h[-1]] + self.up                      # inputs of the ConvTs
+        gups = [self.g_h[0]] + self.g_up                    # their gradients (pre-activation)
+        gouts = self.g_up + [self.g_y]
+        for i in reversed(range(len(r))):
+            last = i == len(r) - 1
+            cout = 3 if last else r[i + 1]
+            xin = ups[i]
+            name = f"decoder.{iup + i}.0"
+            a = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
+            a.dy, a.wt = gouts[i].data_ptr(), net.w(name + ".weight")
+            a.dx, a.dx_epi = gups[i].data_ptr(), _act(SLOPE, xin)
+            self._add(Bw, "vae_convT2d_bwd_data", a)
+            f = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
+            f.x, f.x_xf = xin.data_ptr(), _act()
+            f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
+            self._add(Bw, "vae_convT2d_bwd_filter", f)
+        gi = self._res_stack_bwd("decoder", 1, self.d_in, self.d_t, self.d_h, 0)
+        g_din = self.g_h[gi]
+        a = self._conv(self.q, E, C, 3, 1, 1)
+        a.dy, a.wt, a.dx = g_din.data_ptr(), net.w("decoder.0.0.weight"), self.g_q.data_ptr()
+        self._add(Bw, "vae_conv2d_bwd_data", a)
+        f = self._conv(self.q, E, C, 3, 1, 1)
+        f.x, f.dy = self.q.data_ptr(), g_din.data_ptr()
+        f.dw, f.db = self.g("decoder.0.0.weight"), self.g("decoder.0.0.bias")
+        self._add(Bw, "vae_conv2d_bwd_filter", f)
+        self._add(Bw, "vae_vq_bwd", v)
+        # encoder: Conv1x1 -> latents, residual stack, Conv3x3, strided convs
+        a = self._conv(self.e_h[-1], C, E, 1, 1, 0)
+        a.dy, a.wt = self.g_lat.data_ptr(), net.w(f"encoder.{ilat}.0.weight")
+        a.dx, a.dx_epi = self.g_h[0].data_ptr(), _act(SLOPE, self.e_h[-1])
+        self._add(Bw, "vae_conv2d_bwd_data", a)
+        f = self._conv(self.e_h[-1], C, E, 1, 1, 0)
+        f.x, f.x_xf = self.e_h[-1].data_ptr(), _act()
+        f.dy, f.dw, f.db = self.g_lat.data_ptr(), self.g(f"encoder.{ilat}.0.weight"), self.g(f"encoder.{ilat}.0.bias")
+        self._add(Bw, "vae_conv2d_bwd_filter", f)
+        gi = self._res_stack_bwd("encoder", nh + 1, self.e_in, self.e_t, self.e_h, 0)
+        g_ein = self.g_h[gi]
+        a = self._conv(self.enc[-1], C, C, 3, 1, 1)
+        a.dy, a.wt = g_ein.data_ptr(), net.w(f"encoder.{nh}.0.weight")
+        a.dx, a.dx_epi = self.g_enc[-1].data_ptr(), _act(SLOPE, self.enc[-1])
+        self._add(Bw, "vae_conv2d_bwd_data", a)
+        f = self._conv(self.enc[-1], C, C, 3, 1, 1)
+        f.x, f.x_xf = self.enc[-1].data_ptr(), _act()
+        f.dy, f.dw, f.db = g_ein.data_ptr(), self.g(f"encoder.{nh}.0.weight"), self.g(f"encoder.{nh}.0.bias")
+        self._add(Bw, "vae_conv2d_bwd_filter", f)
+        for i in reversed(range(nh)):
+            cin = 3 if i == 0 else h[i - 1]
+            hin = img if i == 0 else self.enc[i - 1].shape[1]
+            mk = lambda: L.ConvArgs(dtype=net.dcode, n=B, h=hin, w=hin, c=cin, k=h[i], p=self.enc[i].shape[1],
+                                    q=self.enc[i].shape[2], r=4, stride=2, pad=1)
+            f = mk()
+            if i == 0:
+                f.x_nchw_f32, f.x = 1, self.x.data_ptr()
+            else:
+                f.x, f.x_xf = self.enc[i - 1].data_ptr(), _act()
+            f.dy, f.dw, f.db = self.g_enc[i].data_ptr(), self.g(f"encoder.{i}.0.weight"), self.g(f"encoder.{i}.0.bias")
+            self._add(Bw, "vae_conv2d_bwd_filter", f)
+            if i > 0:
+                a = mk()
+                a.dy, a.wt = self.g_enc[i].data_ptr(), net.w(f"encoder.{i}.0.weight")
+                a.dx, a.dx_epi = self.g_enc[i - 1].data_ptr(), _act(SLOPE, self.enc[i - 1])
+                self._add(Bw, "vae_conv2d_bwd_data", a)
+
+    # ------------------------------------------------------------------ execution
+    def _run(self, calls, stream):
+        for fn, arg in calls:
+            L.call(fn, arg, stream)
+
+    def begin(self, stream=None):
+        stream = stream if stream is not None else L.stream_ptr()
+        L.call("vae_step_begin", self.zero.data_ptr(), self.zero.numel() * 4, self.step.data_ptr(), stream)
+
+    def forward(self, stream=None):
+        self._run(self.fwd_calls, stream if stream is not None else L.stream_ptr())
+
+    def backward(self, stream=None):
+        self._run(self.bwd_calls, stream if stream is not None else L.stream_ptr())
+
+    def loss_dict(self) -> Dict[str, float]:
+        o = self.out.tolist()
+        return {"loss": o[0], "Reconstruction_Loss": o[1], "VQ_Loss": o[2]}

@@ -1,0 +1,179 @@
+"""VQ-VAE (models/vq_vae.py) on the MI355X kernels: one teacher-forced training step against the
+reference's golden vectors (tests/golden/vq_b4.npz, made by the reference's own VQVAE) and the
+CPU oracle, plus the VectorQuantizer and Tanh/SSE kernels on their own.
+
+Index exactness: the codebook indices must equal the reference's bit for bit on every row whose
+distance gap (second-best minus best, recorded by the reference) exceeds 1e-5 — below that the
+fp32 summation order of z·E decides, and the survey measured ties and order flips at that scale
+(SURVEY.md §8(c)).  The rest of the step is then checked against the oracle teacher-forced with
+the GPU's indices: loss terms within 1e-4 relative (north_star), reconstructions, per-image
+MSE, every parameter gradient (norm within 1e-3), and the Adam update."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import case_inputs, load_case, summary
+
+pytestmark = pytest.mark.gpu
+
+GAP_EXACT = 1e-5
+
+
+def _step(meta, dtype=torch.float32, batch=None, x=None):
+    from vae_amd import _lib as L
+    from vae_amd.engine import FusedAdam
+    from vae_amd.vq import VQNet, VQStepPlan
+    sd, x0, _ = case_inputs(meta)
+    x = x0 if x is None else x
+    kw = meta["ctor"]
+    net = VQNet(embedding_dim=kw["embedding_dim"], num_embeddings=kw["num_embeddings"], dtype=dtype, device="cuda")
+    net.load_reference_state_dict(sd)
+    plan = VQStepPlan(net, x.shape[0], beta=kw["beta"])
+    opt = FusedAdam(net, lr=meta["lr"])
+    plan.x.copy_(x)
+    st = L.stream_ptr()
+    # step_begin zeroes the gradient region and advances the optimizer's step counter
+    L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
+    plan.forward(st)
+    plan.backward(st)
+    torch.cuda.synchronize()
+    return sd, x, net, plan, opt
+
+
+def test_vq_step_matches_reference():
+    from oracle import vae_oracle as O
+    meta, ref = load_case("vq_b4")
+    sd, x, net, plan, opt = _step(meta)
+    idx = plan.indices.cpu()
+    want = torch.from_numpy(ref["indices"])
+    gap = torch.from_numpy(ref["gap"])
+    clear = gap > GAP_EXACT
+    assert torch.equal(idx[clear], want[clear]), int((idx[clear] != want[clear]).sum())
+    n_tie_flips = int((idx != want).sum())
+    if n_tie_flips == 0:
+        for k in ("loss", "Reconstruction_Loss", "VQ_Loss"):
+            v = meta["loss"][k]
+            assert abs(plan.loss_dict()[k] - v) <= 1e-4 * abs(v), (k, plan.loss_dict()[k], v)
+    # teacher-forced oracle on the GPU's codes
+    o = O.train_step("VQVAE", sd, x, M_N=0.0, lr=meta["lr"], vq_beta=meta["ctor"]["beta"], vq_indices=idx)
+    got = plan.loss_dict()
+    for k in ("loss", "Reconstruction_Loss", "VQ_Loss"):
+        assert abs(got[k] - o["loss"][k]) <= 1e-4 * abs(o["loss"][k]), (k, got[k], o["loss"][k])
+    np.testing.assert_allclose(plan.recon.cpu().numpy(), o["recon"].numpy(), rtol=0, atol=1e-4)
+    np.testing.assert_allclose(plan.per_img.cpu().numpy(), o["per_img_mse"].numpy(), rtol=1e-4)
+    grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
+    assert set(grads) == set(o["grads"])
+    for name, gr in o["grads"].items():
+        g = grads[name]
+        err = float((g - gr).norm() / gr.norm().clamp_min(1e-30))
+        assert err < 1e-3, (name, err)
+    # against the golden gradient summaries too when no near-tie row flipped
+    if n_tie_flips == 0:
+        for name in meta["param_names"]:
+            st, rs = summary(grads[name]), ref[f"grad_stats/{name}"]
+            assert abs(st[1] - rs[1]) <= 1e-3 * rs[1], (name, st, rs)
+    # Adam from zero state: lr * g / (|g| + eps) on our gradients
+    before = {k: v.cpu().double() for k, v in net.reference_state_dict().items()}
+    opt.apply(plan.grads)
+    torch.cuda.synchronize()
+    after = {k: v.cpu().double() for k, v in net.reference_state_dict().items()}
+    lr = meta["lr"]
+    for name, g in grads.items():
+        g = g.double()
+        np.testing.assert_allclose(after[name].numpy(), (before[name] - lr * g / (g.abs() + 1e-8)).numpy(),
+                                   rtol=0, atol=1e-6 * lr + 1e-7, err_msg=name)
+
+
+def test_vq_step_bf16_close():
+    """bf16 throughput mode at B=8: loss terms within 2e-2 of the teacher-forced oracle."""
+    from oracle import vae_oracle as O
+    meta, _ = load_case("vq_b4")
+    x = torch.rand(8, 3, 64, 64, generator=torch.Generator().manual_seed(7))
+    sd, x, net, plan, opt = _step(meta, torch.bfloat16, x=x)
+    o = O.train_step("VQVAE", sd, x, M_N=0.0, lr=meta["lr"], vq_beta=meta["ctor"]["beta"],
+                     vq_indices=plan.indices.cpu(), do_adam=False)
+    got = plan.loss_dict()
+    for k, tol in (("loss", 2e-2), ("Reconstruction_Loss", 2e-2), ("VQ_Loss", 5e-2)):
+        assert abs(got[k] - o["loss"][k]) <= tol * abs(o["loss"][k]), (k, got[k], o["loss"][k])
+
+
+@pytest.mark.parametrize("rows,codes,dim", [(1000, 512, 64), (333, 100, 32), (64, 7, 16)])
+def test_vq_kernel_vs_torch(rows, codes, dim):
+    """vae_vq_fwd / vae_vq_bwd against the reference's formulas in torch fp32 (CPU)."""
+    from vae_amd import _lib as L
+    g = torch.Generator().manual_seed(rows + codes)
+    pre = torch.randn(rows, dim, generator=g)
+    E = (torch.rand(codes, dim, generator=g) * 2 - 1) * 0.5
+    E[codes // 2] = E[0]                                   # exact duplicate code: tie -> first index
+    dq = torch.randn(rows, dim, generator=g) * 1e-3
+    beta = 0.25
+    lat_d, E_d, dq_d = pre.cuda(), E.cuda(), dq.cuda()
+    idx = torch.zeros(rows, dtype=torch.int64, device="cuda")
+    q = torch.empty(rows, dim, device="cuda")
+    sse = torch.zeros(1, device="cuda")
+    dlat = torch.empty(rows, dim, device="cuda")
+    dE = torch.zeros(codes, dim, device="cuda")
+    a = L.VqArgs(dtype=L.F32, rows=rows, dim=dim, codes=codes, beta=beta)
+    a.lat, a.lat_xf = lat_d.data_ptr(), L.Xform(kind=L.X_ACT, channels=1, slope=0.01)
+    a.codebook, a.indices, a.q, a.sse = E_d.data_ptr(), idx.data_ptr(), q.data_ptr(), sse.data_ptr()
+    a.dq, a.dlat, a.dcodebook = dq_d.data_ptr(), dlat.data_ptr(), dE.data_ptr()
+    st = L.stream_ptr()
+    L.call("vae_vq_fwd", a, st)
+    L.call("vae_vq_bwd", a, st)
+    torch.cuda.synchronize()
+    # reference formulas (vq_vae.py:24-55) with autograd
+    z = torch.nn.functional.leaky_relu(pre, 0.01).requires_grad_(True)
+    Ew = E.clone().requires_grad_(True)
+    dist = torch.sum(z ** 2, dim=1, keepdim=True) + torch.sum(Ew ** 2, dim=1) - 2 * torch.matmul(z, Ew.t())
+    want = torch.argmin(dist, dim=1)
+    top2 = torch.topk(dist.detach(), 2, dim=1, largest=False).values
+    clear = (top2[:, 1] - top2[:, 0]) > GAP_EXACT
+    got = idx.cpu()
+    assert torch.equal(got[clear], want[clear])
+    assert int((got == codes // 2).sum()) == 0          # the duplicate of code 0 never wins the tie
+    onehot = torch.zeros(rows, codes).scatter_(1, got.view(-1, 1), 1)
+    qq = onehot @ Ew
+    vq_loss = torch.nn.functional.mse_loss(qq.detach(), z) * beta + torch.nn.functional.mse_loss(qq, z.detach())
+    st_q = z + (qq - z).detach()
+    (vq_loss + (st_q * dq).sum()).backward()
+    pre_g = z.grad * torch.where(pre > 0, 1.0, 0.01)
+    np.testing.assert_allclose(q.cpu().numpy(), qq.detach().numpy(), rtol=0, atol=0)
+    assert abs(float(sse) * (1 + beta) / (rows * dim) - float(vq_loss)) <= 1e-5 * float(vq_loss)
+    np.testing.assert_allclose(dlat.cpu().numpy(), pre_g.numpy(), rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(dE.cpu().numpy(), Ew.grad.numpy(), rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_recon_kernel(dtype):
+    """vae_recon_fwd / vae_recon_bwd: tanh, per-image SSE, d/dy of mse(tanh(y), x)."""
+    from vae_amd import _lib as L
+    g = torch.Generator().manual_seed(3)
+    n, hw = 3, 32
+    y = torch.randn(n, hw, hw, 3, generator=g).to(dtype)
+    x = torch.rand(n, 3, hw, hw, generator=g)
+    y_d, x_d = y.cuda(), x.cuda()
+    recon = torch.empty(n, 3, hw, hw, device="cuda")
+    sse = torch.zeros(n, device="cuda")
+    dy = torch.empty(n, hw, hw, 3, dtype=dtype, device="cuda")
+    a = L.ReconArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=3, grad_scale=1.0 / x.numel())
+    a.y, a.target, a.recon, a.sse, a.dy = y_d.data_ptr(), x_d.data_ptr(), recon.data_ptr(), sse.data_ptr(), dy.data_ptr()
+    L.call("vae_recon_fwd", a, L.stream_ptr())
+    torch.cuda.synchronize()
+    yr = y.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    r = torch.tanh(yr)
+    loss = torch.nn.functional.mse_loss(r, x)
+    loss.backward()
+    tolr = 1e-6 if dtype == torch.float32 else 1e-2
+    np.testing.assert_allclose(recon.cpu().numpy(), r.detach().numpy(), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(sse.cpu().numpy(), ((r.detach() - x) ** 2).sum(dim=(1, 2, 3)).numpy(), rtol=1e-5)
+    want_dy = yr.grad.permute(0, 2, 3, 1)
+    np.testing.assert_allclose(dy.float().cpu().numpy(), want_dy.numpy(), rtol=tolr, atol=tolr * float(want_dy.abs().max()))
+    # bwd from a caller-supplied dL/drecon
+    gr = torch.randn(n, 3, hw, hw, generator=g)
+    gr_d = gr.cuda()
+    b = L.ReconArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=3)
+    b.target, b.recon, b.dy, b.grad_recon = x_d.data_ptr(), recon.data_ptr(), dy.data_ptr(), gr_d.data_ptr()
+    L.call("vae_recon_bwd", b, L.stream_ptr())
+    torch.cuda.synchronize()
+    want = (gr * (1 - r.detach() ** 2)).permute(0, 2, 3, 1)
+    np.testing.assert_allclose(dy.float().cpu().numpy(), want.numpy(), rtol=tolr, atol=tolr * float(want.abs().max()))

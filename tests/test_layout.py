@@ -38,3 +38,23 @@ def test_fused_fc_is_contiguous():
     mu, var = lay.by_name["fc_mu.weight"], lay.by_name["fc_var.weight"]
     assert var.offset == mu.offset + mu.numel
     assert lay.total >= 3937635
+
+
+def test_vq_layout_matches_reference_spec_and_roundtrips():
+    from vae_amd.layout import vq_layout, vq_param_spec
+    ospec = O.vq_param_spec()
+    assert [(n, tuple(s), k) for n, s, k in ospec] == [(n, tuple(s), k) for n, s, k in vq_param_spec(3, 64, 512, [128, 256])]
+    sd = O.make_params(ospec, 5)
+    lay = vq_layout(3, 64, 512, [128, 256])
+    assert lay.bns == [] and set(p.name for p in lay.params) == set(sd)
+    flat = torch.zeros(lay.total)
+    lay.load_reference(flat, torch.zeros(0), sd)
+    back = lay.export_reference(flat, None, 0, [n for n, _, _ in ospec])
+    assert list(back) == list(sd)
+    for k in sd:
+        assert torch.equal(back[k], sd[k]), k
+    # every bias directly follows its weight (default_init draws the bias bound from it)
+    names = [p.name for p in lay.params]
+    for i, n in enumerate(names):
+        if n.endswith(".bias"):
+            assert names[i - 1] == n[:-4] + "weight"
