@@ -238,7 +238,7 @@ def main():
         from vae_amd.vq import VQNet, VQStepPlan
         net = VQNet(dtype=dtype, device="cuda", generator=gen)
         plan = VQStepPlan(net, args.batch)
-        opt = FusedAdam(net, lr=0.001)                             # configs/vq_vae.yaml LR
+        opt = FusedAdam(net, lr=0.005)                             # configs/vae/vq_vae.yaml LR
     else:
         net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
         loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]

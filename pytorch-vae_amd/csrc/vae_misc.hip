@@ -336,41 +336,77 @@ int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
 }
 
 // ------------------------------------------------------------------ BatchNorm finalisation
+// One memory round trip: every replica of every statistic a channel needs is loaded up front
+// (64 channels x 4 replica lanes per workgroup, <= 8 replicas per lane), then the 4 lanes of a
+// channel combine through LDS in a fixed order (deterministic) and lane 0 writes the table.
+constexpr int BNF_LANES = 4, BNF_PER = 8;      // replicas <= BNF_LANES * BNF_PER (checked on the host)
+
 __global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) {
+  __shared__ float red[4][BNF_LANES][64];
   const vae_xform& x = a.xf;
   const int C = x.channels;
-  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < C; c += gridDim.x * blockDim.x) {
-    float mean, invstd, var;
-    bn_moments(x, c, mean, invstd, var);
-    const float g = x.gamma[c];
-    if (a.mode == 0) {
-      const float sc = g * invstd;
-      a.table[c] = sc;
-      a.table[C + c] = x.beta[c] - mean * sc;
-      a.table[2 * C + c] = invstd;
-      a.table[3 * C + c] = -mean * invstd;
-      if (x.running_mean) {
-        const float m = x.momentum;
-        const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
-        x.running_mean[c] = (1.f - m) * x.running_mean[c] + m * mean;
-        x.running_var[c] = (1.f - m) * x.running_var[c] + m * unb;
-      }
-    } else {
-      const float inv_m = 1.0f / x.count;
-      const float dgam = rsum(x.dgamma, x, c), dbet = rsum(x.dbeta, x, c);
-      const float A = g * invstd;
-      const float mgx = dgam * inv_m, mg = dbet * inv_m;
-      const float B = -A * invstd * mgx;
-      const float Cc = -A * (mg - mean * invstd * mgx);
-      a.table[c] = A;
-      a.table[C + c] = B;
-      a.table[2 * C + c] = Cc;
-      if (x.dgamma_out) x.dgamma_out[c] += dgam;
-      if (x.dbeta_out) x.dbeta_out[c] += dbet;
-      if (a.db) {
-        const float sum_y = rsum(x.sum, x, c) + x.count * (x.shift ? x.shift[c] : 0.f);
-        a.db[c] += A * dbet + B * sum_y + Cc * x.count;
-      }
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int cc = c < C ? c : 0;
+  const int reps = x.reps > 1 ? x.reps : 1;
+  const long rstr = x.reps > 1 ? x.rstride : 0;
+  const bool bwd = a.mode != 0;
+  const float* arr[4] = {x.sum, x.sumsq, bwd ? x.dgamma : nullptr, bwd ? x.dbeta : nullptr};
+  float v[4][BNF_PER];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int u = 0; u < BNF_PER; ++u) {
+      const int r = rl + BNF_LANES * u;
+      v[k][u] = (arr[k] && r < reps) ? arr[k][r * rstr + cc] : 0.f;
+    }
+  // per-channel parameters, in flight with the replicas (used by lane 0)
+  const float g = x.gamma[cc], be = x.beta[cc], sh = x.shift ? x.shift[cc] : 0.f;
+  const bool run = !bwd && x.running_mean;
+  const float rmean = run ? x.running_mean[cc] : 0.f, rvar = run ? x.running_var[cc] : 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float t = 0.f;
+#pragma unroll
+    for (int u = 0; u < BNF_PER; ++u) t += v[k][u];
+    red[k][rl][cl] = t;
+  }
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  float tot[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) tot[k] = (red[k][0][cl] + red[k][1][cl]) + (red[k][2][cl] + red[k][3][cl]);
+  const float inv_m = 1.0f / x.count;
+  const float s1 = tot[0] * inv_m;
+  const float var = fmaxf(tot[1] * inv_m - s1 * s1, 0.0f);
+  const float mean = s1 + sh;
+  const float invstd = 1.0f / sqrtf(var + x.eps);
+  if (!bwd) {
+    const float sc = g * invstd;
+    a.table[c] = sc;
+    a.table[C + c] = be - mean * sc;
+    a.table[2 * C + c] = invstd;
+    a.table[3 * C + c] = -mean * invstd;
+    if (run) {
+      const float m = x.momentum;
+      const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
+      x.running_mean[c] = (1.f - m) * rmean + m * mean;
+      x.running_var[c] = (1.f - m) * rvar + m * unb;
+    }
+  } else {
+    const float dgam = tot[2], dbet = tot[3];
+    const float A = g * invstd;
+    const float mgx = dgam * inv_m, mg = dbet * inv_m;
+    const float B = -A * invstd * mgx;
+    const float Cc = -A * (mg - mean * invstd * mgx);
+    a.table[c] = A;
+    a.table[C + c] = B;
+    a.table[2 * C + c] = Cc;
+    if (x.dgamma_out) x.dgamma_out[c] += dgam;
+    if (x.dbeta_out) x.dbeta_out[c] += dbet;
+    if (a.db) {
+      const float sum_y = tot[0] + x.count * sh;
+      a.db[c] += A * dbet + B * sum_y + Cc * x.count;
     }
   }
 }
@@ -392,15 +428,24 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
   __shared__ float red[4][4];
   const int B = a.batch, S = a.samples > 0 ? a.samples : 1, D = a.latent;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // kld_b = -0.5 Σ_d (1 + lv - mu^2 - exp(lv))  (one wave per row)
-  for (int b = wv; b < B && a.kind != VAE_LOSS_VQ; b += 4) {
-    float s = 0.f;
-    for (int d = lane; d < D; d += 64) {
-      const float mu = a.mulv[(long)b * 2 * D + d], lv = a.mulv[(long)b * 2 * D + D + d];
-      s += 1.f + lv - mu * mu - expf(lv);
+  // kld_b = -0.5 Σ_d (1 + lv - mu^2 - exp(lv)): 4 threads per row, each a quarter of the latent
+  // dims with all its loads in flight at once (64 rows per pass)
+  if (a.kind != VAE_LOSS_VQ) {
+    const int part = threadIdx.x & 3, per = (D + 3) / 4;
+    for (int b0 = 0; b0 < B; b0 += 64) {
+      const int b = b0 + (threadIdx.x >> 2);
+      float s = 0.f;
+      if (b < B) {
+        const float* mu = a.mulv + (long)b * 2 * D;
+        const float* lv = mu + D;
+        const int d0 = part * per, d1 = min(D, d0 + per);
+#pragma unroll 32
+        for (int d = d0; d < d1; ++d) s += 1.f + lv[d] - mu[d] * mu[d] - expf(lv[d]);
+      }
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      if (part == 0 && b < B) kld_row[b] = -0.5f * s;
     }
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    if (lane == 0) kld_row[b] = -0.5f * s;
   }
   __syncthreads();
   const float inv_img = 1.f / (float)a.img_elems;
@@ -595,7 +640,8 @@ extern "C" int vae_bn_finalize(const vae_bn_args* a, void* stream) {
     return fail(VAE_E_BADARG, "bn_finalize: args");
   if (a->mode != 0 && a->mode != 1) return fail(VAE_E_BADARG, "bn_finalize: mode %d", a->mode);
   if (a->mode == 1 && (!a->xf.dgamma || !a->xf.dbeta)) return fail(VAE_E_BADARG, "bn_finalize: backward sums");
-  const int grid = (a->xf.channels + 255) / 256;
+  if (a->xf.reps > BNF_LANES * BNF_PER) return fail(VAE_E_UNSUPPORTED, "bn_finalize: %d replicas > %d", a->xf.reps, BNF_LANES * BNF_PER);
+  const int grid = (a->xf.channels + 63) / 64;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
   return check_launch("bn_finalize");
 }

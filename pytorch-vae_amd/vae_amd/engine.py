@@ -15,7 +15,8 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
-from .net import StepPlan, VAENet
+from .dp import BucketedAllReduce, broadcast_buffers, plan_buckets
+from .net import VAENet
 
 
 class FusedAdam:
@@ -42,37 +43,44 @@ class FusedAdam:
 
 
 class TrainStep:
-    """One full training step of the VanillaVAE family on fixed-shape device buffers.
+    """One full training step of a plan (VanillaVAE family: net.StepPlan; VQ-VAE: vq.VQStepPlan)
+    on fixed-shape device buffers.
 
     Inputs live in `plan.x` (NCHW fp32 images) and `plan.eps` (N(0,1) noise, the reference's
-    torch.randn_like at vanilla_vae.py:116); write them before calling, or pass tensors."""
+    torch.randn_like at vanilla_vae.py:116); write them before calling, or pass tensors.
+    With more than one rank the backward is cut into segments at gradient-bucket boundaries
+    (dp.plan_buckets); each bucket's RCCL all-reduce is launched as soon as its segment is
+    queued, so it runs on the communication stream while the rest of the backward computes."""
 
-    def __init__(self, net: VAENet, plan: StepPlan, opt: FusedAdam, *, graph: bool = True,
-                 process_group=None):
+    def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
+                 nbuckets: int = 4):
         self.net, self.plan, self.opt = net, plan, opt
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.use_graph = graph
-        self.g_main: Optional[torch.cuda.CUDAGraph] = None
+        self.segments = []                      # (call range) of the backward per bucket
+        if self.world > 1:
+            self.buckets = plan_buckets(plan.bwd_calls, plan.grads, net.layout, nbuckets)
+            self.comm = BucketedAllReduce(plan.grads, self.buckets, process_group)
+        else:
+            self.buckets = [(len(plan.bwd_calls), 0, plan.grads.numel())]
+            self.comm = None
+        self.graphs = []
         self.g_opt: Optional[torch.cuda.CUDAGraph] = None
         self.stream = torch.cuda.Stream(device=net.device)
 
     # -------------------------------------------------------------- eager pieces
-    def _main(self):
+    def _segment(self, k: int):
+        """Segment k of the step: k == 0 also runs step_begin and the forward."""
         p = self.plan
         st = L.stream_ptr()
-        L.call("vae_step_begin", p.zero.data_ptr(), p.zero.numel() * 4, self.opt.step.data_ptr(), st)
-        if p.loss_kind == L.LOSS_BETA_B:
-            p.num_iter.add_(1.0)
-        p.forward(st)
-        p.backward(st)
-
-    def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.plan.grads, op=dist.ReduceOp.AVG, group=self.pg)
-            # BatchNorm running stats are per rank; DDP broadcasts rank 0's buffers each
-            # forward (broadcast_buffers=True), which we mirror after the update.
-            dist.broadcast(self.net.running, src=0, group=self.pg)
+        if k == 0:
+            L.call("vae_step_begin", p.zero.data_ptr(), p.zero.numel() * 4, self.opt.step.data_ptr(), st)
+            if p.loss_kind == L.LOSS_BETA_B:
+                p.num_iter.add_(1.0)
+            p.forward(st)
+        lo = 0 if k == 0 else self.buckets[k - 1][0]
+        p._run(p.bwd_calls[lo:self.buckets[k][0]], st)
 
     def _opt(self):
         self.opt.apply(self.plan.grads, L.stream_ptr())
@@ -84,7 +92,8 @@ class TrainStep:
         state = (self.net.params.clone(), self.net.running.clone(), self.opt.m.clone(), self.opt.v.clone(),
                  self.opt.step.clone(), self.plan.num_iter.clone())
         with torch.cuda.stream(s):
-            self._main()
+            for k in range(len(self.buckets)):
+                self._segment(k)
             self._opt()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -92,9 +101,12 @@ class TrainStep:
         self.net.params.copy_(state[0]); self.net.running.copy_(state[1]); self.opt.m.copy_(state[2])
         self.opt.v.copy_(state[3]); self.opt.step.copy_(state[4]); self.plan.num_iter.copy_(state[5])
         self.net.sync_lowp()
-        self.g_main = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_main, stream=s):
-            self._main()
+        self.graphs = []
+        for k in range(len(self.buckets)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._segment(k)
+            self.graphs.append(g)
         self.g_opt = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_opt, stream=s):
             self._opt()
@@ -105,14 +117,20 @@ class TrainStep:
             self.plan.x.copy_(x)
         if eps is not None:
             self.plan.eps.copy_(eps.reshape(self.plan.eps.shape))
-        if not self.use_graph:
-            self._main()
-            self._allreduce()
-            self._opt()
-        else:
-            if self.g_main is None:
-                self._capture()
-            self.g_main.replay()
-            self._allreduce()
+        if self.use_graph and not self.graphs:
+            self._capture()
+        for k in range(len(self.buckets)):
+            if self.use_graph:
+                self.graphs[k].replay()
+            else:
+                self._segment(k)
+            if self.comm is not None:
+                self.comm.launch(k)
+        if self.comm is not None:
+            self.comm.wait()
+            broadcast_buffers(self.net.running, self.pg)
+        if self.use_graph:
             self.g_opt.replay()
+        else:
+            self._opt()
         self.net.num_batches_tracked += 1

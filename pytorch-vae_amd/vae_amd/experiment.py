@@ -1,0 +1,177 @@
+"""VAEXperiment counterpart (experiment.py:16-391 of the reference) without PyTorch Lightning.
+
+The reference drives the hot path through a LightningModule: `training_step` (experiment.py:45-86)
+calls the model, its `loss_function` with M_N = kld_weight, logs every loss term with
+`.item()` + sync_dist, records per-image MSE for the difficulty sampler and tracks the
+extreme-loss images with 64 more `.item()` calls; `configure_optimizers` (:304-357) builds Adam
+(lr, weight_decay) with ExponentialLR per epoch (or ReduceLROnPlateau when adaptive_lr).
+
+Here the same methods take the same arguments and return the same values, but the step keeps
+everything on the device: the loss terms are returned as tensors (`logged` holds them; the
+caller decides when to synchronise), per-image losses move to the host in one copy, and the
+extreme-image update is a single argmax/argmin.  Lightning (1.5.6 pinned by the reference,
+absent here) is optional: `VAEXperiment` is a plain object whose hooks a Trainer-like loop —
+or `fit()` below — calls.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+from torch import optim
+
+Tensor = torch.Tensor
+
+
+class VAEXperiment:
+    """experiment.py:16 VAEXperiment(vae_model, params) — params are the YAML `exp_params`."""
+
+    def __init__(self, vae_model, params: dict) -> None:
+        self.model = vae_model
+        self.params = params
+        self.curr_device = None
+        self.hold_graph = bool(params.get('retain_first_backpass', False))
+        self.test_output_size = (256, 256)
+        self.datamodule = None                 # optional: .record_img_losses(names, losses)
+        self.logged: Dict[str, Tensor] = {}
+        self.reset_extreme_image_tracking()
+
+    def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
+        return self.model(input, **kwargs)
+
+    __call__ = forward
+
+    def reset_extreme_image_tracking(self):
+        """experiment.py:38-43."""
+        self.extreme_images = {
+            'highest': {'loss': float('-inf'), 'img': None, 'recon': None, 'name': None},
+            'lowest': {'loss': float('inf'), 'img': None, 'recon': None, 'name': None},
+        }
+
+    def log_dict(self, d: Dict[str, Tensor]):
+        """Lightning's log_dict(..., sync_dist=True) without the per-term host sync: values stay
+        device tensors (detached); averaged over ranks when torch.distributed is initialised."""
+        for k, v in d.items():
+            v = v.detach() if torch.is_tensor(v) else torch.tensor(float(v))
+            if torch.distributed.is_available() and torch.distributed.is_initialized():
+                v = v.clone().float()
+                torch.distributed.all_reduce(v)
+                v /= torch.distributed.get_world_size()
+            self.logged[k] = v
+
+    @staticmethod
+    def per_image_mse(recon: Tensor, input: Tensor) -> Tensor:
+        """experiment.py:58-62: mse(recon, input, reduction='none').mean([1,2,3]).  IWAE's
+        [B,S,C,H,W] reconstructions (where the reference's broadcast fails)
+        are scored per image averaged over the samples."""
+        if recon.dim() == 5:
+            return ((recon - input.unsqueeze(1)) ** 2).mean(dim=[1, 2, 3, 4])
+        return F.mse_loss(recon, input, reduction='none').mean(dim=[1, 2, 3])
+
+    def training_step(self, batch, batch_idx, optimizer_idx=0):
+        """experiment.py:45-86."""
+        imgs, labels, img_names = batch
+        self.curr_device = imgs.device
+        results = self.forward(imgs, labels=labels)
+        train_loss = self.model.loss_function(*results, M_N=self.params['kld_weight'],
+                                              optimizer_idx=optimizer_idx, batch_idx=batch_idx)
+        self.log_dict(train_loss)
+        per_img = self.per_image_mse(results[0].detach(), results[1]).cpu()     # one host copy
+        if self.datamodule is not None and hasattr(self.datamodule, "record_img_losses"):
+            self.datamodule.record_img_losses(img_names, per_img)
+        self._track_extremes(per_img, imgs, results[0], img_names)
+        return train_loss['loss']
+
+    def _track_extremes(self, per_img: Tensor, imgs: Tensor, recon: Tensor, names):
+        """experiment.py:65-84 with one argmax / argmin instead of a per-image loop (the first
+        index wins ties, as the reference's strict comparisons do)."""
+        if per_img.numel() == 0:
+            return
+        hi, lo = int(torch.argmax(per_img)), int(torch.argmin(per_img))
+        for key, i, better in (('highest', hi, lambda a, b: a > b), ('lowest', lo, lambda a, b: a < b)):
+            v = float(per_img[i])
+            if better(v, self.extreme_images[key]['loss']):
+                self.extreme_images[key] = {'loss': v, 'img': imgs[i:i + 1].detach().cpu(),
+                                            'recon': recon[i:i + 1].detach().cpu(), 'name': names[i]}
+
+    def validation_step(self, batch, batch_idx, optimizer_idx=0):
+        """experiment.py:122-132 (the models run train-mode BatchNorm)."""
+        imgs, labels, _ = batch
+        self.curr_device = imgs.device
+        with torch.no_grad():
+            results = self.forward(imgs, labels=labels)
+            val_loss = self.model.loss_function(*results, M_N=self.params['kld_weight'],
+                                                optimizer_idx=optimizer_idx, batch_idx=batch_idx)
+        self.log_dict({f"val_{k}": v for k, v in val_loss.items()})
+        return val_loss
+
+    def configure_optimizers(self):
+        """experiment.py:304-357: Adam(lr, weight_decay); ReduceLROnPlateau on val_loss when
+        adaptive_lr, else ExponentialLR(scheduler_gamma) stepped per epoch; a second optimizer
+        for `submodel` when LR_2 is set."""
+        p = self.params
+        optims, scheds = [], []
+        optimizer = optim.Adam(self.model.parameters(), lr=p['LR'], weight_decay=p['weight_decay'])
+        optims.append(optimizer)
+        if p.get('LR_2') is not None and p.get('submodel'):
+            optims.append(optim.Adam(getattr(self.model, p['submodel']).parameters(), lr=p['LR_2']))
+        if p.get('adaptive_lr'):
+            scheduler = optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode='min', factor=0.5, patience=5,
+                                                             threshold=0.00003, threshold_mode='abs', min_lr=1e-7)
+            return {"optimizer": optimizer,
+                    "lr_scheduler": {"scheduler": scheduler, "monitor": "val_loss", "interval": "epoch",
+                                     "frequency": 1}}
+        if p.get('scheduler_gamma') is not None:
+            scheds.append({"scheduler": optim.lr_scheduler.ExponentialLR(optims[0], gamma=p['scheduler_gamma']),
+                           "interval": "epoch"})
+            if p.get('scheduler_gamma_2') is not None and len(optims) > 1:
+                scheds.append({"scheduler": optim.lr_scheduler.ExponentialLR(optims[1], gamma=p['scheduler_gamma_2']),
+                               "interval": "epoch"})
+            return optims, scheds
+        return optims
+
+
+def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=None) -> List[Dict[str, float]]:
+    """Minimal Trainer loop over an iterable of (imgs, labels, names) batches: the reference's
+    Lightning fit() for one optimizer (zero_grad, training_step, backward, step, epoch-interval
+    schedulers).  Returns the per-epoch mean of each logged term (host values, synced once per
+    epoch)."""
+    opt_cfg = experiment.configure_optimizers()
+    sched, plateau = [], None
+    if isinstance(opt_cfg, dict):
+        optims = [opt_cfg["optimizer"]]
+        plateau = opt_cfg["lr_scheduler"]["scheduler"]
+    elif isinstance(opt_cfg, tuple):
+        optims, sched = opt_cfg
+    else:
+        optims = opt_cfg
+    history = []
+    for _ in range(epochs):
+        sums: Dict[str, Tensor] = {}
+        cnt: Dict[str, int] = {}
+
+        def acc():
+            for k, v in experiment.logged.items():
+                sums[k] = sums.get(k, 0) + v.float()
+                cnt[k] = cnt.get(k, 0) + 1
+        for i, batch in enumerate(train_batches):
+            for o in optims:
+                o.zero_grad(set_to_none=True)
+            loss = experiment.training_step(batch, i)
+            loss.backward()
+            optims[0].step()
+            acc()
+        if val_batches is not None:
+            for i, batch in enumerate(val_batches):
+                experiment.validation_step(batch, i)
+                acc()
+        rec = {k: float(v) / cnt[k] for k, v in sums.items()}
+        for s in sched:
+            s["scheduler"].step()
+        if plateau is not None and "val_loss" in rec and math.isfinite(rec["val_loss"]):
+            plateau.step(rec["val_loss"])
+        experiment.reset_extreme_image_tracking()
+        history.append(rec)
+    return history

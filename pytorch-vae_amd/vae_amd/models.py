@@ -6,6 +6,7 @@ Mirrors the reference interface (paths relative to the reference root):
   VanillaVAE              models/vanilla_vae.py:8-173
   BetaVAE                 models/beta_vae.py:8-179  (loss_type 'H' / 'B', per-instance num_iter)
   IWAE                    models/iwae.py:8-188      (num_samples; row-major b*S+s latent order)
+  VQVAE                   models/vq_vae.py:73-219   (VectorQuantizer, residual stacks; vae_amd/vq.py)
   vae_models registry     models/__init__.py:35-56
 
 `forward(x)` runs the HIP encoder/decoder (libvaehip.so) and returns the reference's list
@@ -23,7 +24,7 @@ build plan; sample()/generate() in eval mode raise NotImplemente
 from __future__ import annotations
 
 from abc import abstractmethod
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Union
 
 import torch
 from torch import nn
@@ -266,8 +267,108 @@ class IWAE(_HipVAE):
         return {'loss': loss, 'Reconstruction_Loss': log_p_x_z.mean(), 'KLD': -kld_loss.mean()}
 
 
+class _VQStep(torch.autograd.Function):
+    """VQ-VAE forward on the HIP network; backward = the fused HIP backward seeded with
+    dL/drecon and dL/dvq_loss (straight-through estimator inside, vq_vae.py:53)."""
+
+    @staticmethod
+    def forward(ctx, flat: Tensor, x: Tensor, model: "VQVAE"):
+        plan = model._plan(x.shape[0])
+        st = L.stream_ptr()
+        model.net.sync_lowp()
+        plan.x.copy_(x.detach().to(plan.x.dtype))
+        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, plan.step.data_ptr(), st)
+        plan.forward(st)
+        ctx.plan = plan
+        n = plan.q.numel()
+        vq_loss = plan.vq_sse[0] * ((1.0 + plan.beta) / n)      # commitment*beta + embedding (:47-50)
+        return plan.recon.clone(), vq_loss.clone()
+
+    @staticmethod
+    def backward(ctx, g_recon: Optional[Tensor], g_vq: Optional[Tensor]):
+        plan = ctx.plan
+        if g_recon is None:
+            plan.grad_recon.zero_()
+        else:
+            plan.grad_recon.copy_(g_recon.reshape(plan.grad_recon.shape))
+        if g_vq is None:
+            plan.vq_grad.zero_()
+        else:
+            plan.vq_grad.copy_(g_vq.reshape(1))
+        plan.backward(L.stream_ptr())
+        return plan.grads.clone(), None, None
+
+
+class VQVAE(BaseVAE):
+    """models/vq_vae.py:73-219 on libvaehip (vae_amd/vq.py)."""
+
+    def __init__(self, in_channels: int, embedding_dim: int, num_embeddings: int, hidden_dims: List = None,
+                 beta: float = 0.25, img_size: int = 64, *, dtype: torch.dtype = torch.float32, device=None,
+                 seed: Optional[int] = None, **kwargs) -> None:
+        super().__init__()
+        from .vq import VQNet
+        self.embedding_dim = embedding_dim
+        self.num_embeddings = num_embeddings
+        self.img_size = img_size
+        self.beta = beta
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        self.net = VQNet(in_channels, embedding_dim, num_embeddings, hidden_dims, img_size, dtype, device, gen)
+        self.flat = nn.Parameter(self.net.params)
+        self._plans: Dict[int, Any] = {}
+
+    def _plan(self, batch: int):
+        from .vq import VQStepPlan
+        if batch not in self._plans:
+            self._plans[batch] = VQStepPlan(self.net, batch, beta=self.beta, fused_loss=False)
+        return self._plans[batch]
+
+    def reference_state_dict(self) -> Dict[str, Tensor]:
+        return self.net.reference_state_dict()
+
+    def load_reference_state_dict(self, sd: Dict[str, Tensor]):
+        with torch.no_grad():
+            self.net.load_reference_state_dict(sd)
+
+    def encode(self, input: Tensor) -> List[Tensor]:
+        """vq_vae.py:168-176: the encoder output (after its final LeakyReLU), NCHW."""
+        plan = self._plan(input.shape[0])
+        st = L.stream_ptr()
+        self.net.sync_lowp()
+        plan.x.copy_(input.detach())
+        plan.begin(st)
+        plan._run(plan.fwd_calls[:plan.n_encode], st)
+        return [F.leaky_relu(plan.latpre.float(), 0.01).permute(0, 3, 1, 2).contiguous()]
+
+    def decode(self, z: Tensor) -> Tensor:
+        """vq_vae.py:178-187: decoder on (quantized) latents [B x D x H x W]."""
+        plan = self._plan(z.shape[0])
+        st = L.stream_ptr()
+        self.net.sync_lowp()
+        plan.q.copy_(z.detach().permute(0, 2, 3, 1))
+        plan.begin(st)
+        plan._run(plan.fwd_calls[plan.n_decode0:plan.n_decode1], st)
+        return plan.recon.clone()
+
+    def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
+        recon, vq_loss = _VQStep.apply(self.flat, input, self)
+        return [recon, input, vq_loss]
+
+    def loss_function(self, *args, **kwargs) -> dict:
+        """vq_vae.py:194-211."""
+        recons, input, vq_loss = args[0], args[1], args[2]
+        recons_loss = F.mse_loss(recons, input)
+        loss = recons_loss + vq_loss
+        return {'loss': loss, 'Reconstruction_Loss': recons_loss, 'VQ_Loss': vq_loss}
+
+    def sample(self, num_samples: int, current_device: Union[int, str], **kwargs) -> Tensor:
+        raise Warning('VQVAE sampler is not implemented.')              # vq_vae.py:216
+
+    def generate(self, x: Tensor, **kwargs) -> Tensor:
+        return self.forward(x)[0]
+
+
 # models/__init__.py:35-56: the families on the MI355X path; the others raise on use.
-_ON_PATH = {'VanillaVAE': VanillaVAE, 'BetaVAE': BetaVAE, 'IWAE': IWAE}
+_ON_PATH = {'VanillaVAE': VanillaVAE, 'BetaVAE': BetaVAE, 'IWAE': IWAE, 'VQVAE': VQVAE}
 _REFERENCE_NAMES = ['HVAE', 'LVAE', 'IWAE', 'SWAE', 'MIWAE', 'VQVAE', 'DFCVAE', 'DIPVAE', 'BetaVAE', 'InfoVAE',
                     'WAE_MMD', 'VampVAE', 'GammaVAE', 'MSSIMVAE', 'JointVAE', 'BetaTCVAE', 'FactorVAE',
                     'LogCoshVAE', 'VanillaVAE', 'ConditionalVAE', 'CategoricalVAE', 'Autoencoder']
@@ -276,7 +377,7 @@ _REFERENCE_NAMES = ['HVAE', 'LVAE', 'IWAE', 'SWAE', 'MIWAE', 'VQVAE', 'DFCVAE', 
 def _not_on_path(name):
     def ctor(*args, **kwargs):
         raise NotImplementedError(f"{name} is not on the MI355X training path of this build "
-                                  f"(VanillaVAE, BetaVAE, IWAE are; DESIGN.md §7)")
+                                  f"(VanillaVAE, BetaVAE, IWAE, VQVAE are; DESIGN.md §7)")
     return ctor
 
 

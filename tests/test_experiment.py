@@ -1,0 +1,99 @@
+"""VAEXperiment counterpart (vae_amd/experiment.py) on CPU with a stand-in model that follows the
+BaseVAE contract (forward -> [recons, input, ...], loss_function(*results, M_N=...) -> dict):
+training_step / validation_step / configure_optimizers / fit semantics of experiment.py."""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from vae_amd.experiment import VAEXperiment, fit
+
+
+class TinyAE(nn.Module):
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.enc = nn.Linear(3 * 8 * 8, 16)
+        self.dec = nn.Linear(16, 3 * 8 * 8)
+        with torch.no_grad():
+            for p in self.parameters():
+                p.copy_(torch.randn(p.shape, generator=g) * 0.05)
+
+    def forward(self, x, **kwargs):
+        h = self.enc(x.flatten(1))
+        return [torch.tanh(self.dec(h)).view_as(x), x, h]
+
+    def loss_function(self, *args, **kwargs):
+        recons, x, h = args
+        r = F.mse_loss(recons, x)
+        k = (h ** 2).mean()
+        loss = r + kwargs['M_N'] * k
+        return {'loss': loss, 'Reconstruction_Loss': r.detach(), 'KLD': -k.detach()}
+
+
+class Recorder:
+    def __init__(self):
+        self.calls = []
+
+    def record_img_losses(self, names, losses):
+        self.calls.append((list(names), losses.clone()))
+
+
+def _batch(seed, B=6):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(B, 3, 8, 8, generator=g), torch.zeros(B, dtype=torch.float64), [f"img{seed}_{i}.png" for i in range(B)]
+
+
+PARAMS = {'LR': 0.005, 'weight_decay': 0.0, 'scheduler_gamma': 0.95, 'kld_weight': 0.5, 'manual_seed': 1265}
+
+
+def test_training_step_matches_reference_semantics():
+    m = TinyAE()
+    exp = VAEXperiment(m, dict(PARAMS))
+    rec = Recorder()
+    exp.datamodule = rec
+    batch = _batch(1)
+    loss = exp.training_step(batch, 0)
+    res = m(batch[0])
+    want = m.loss_function(*res, M_N=0.5)
+    assert torch.allclose(loss, want['loss'])
+    assert set(exp.logged) == {'loss', 'Reconstruction_Loss', 'KLD'}
+    per_img = F.mse_loss(res[0], batch[0], reduction='none').mean(dim=[1, 2, 3]).detach()
+    names, got = rec.calls[0]
+    assert names == batch[2] and torch.allclose(got, per_img)
+    i_hi, i_lo = int(per_img.argmax()), int(per_img.argmin())
+    assert exp.extreme_images['highest']['name'] == batch[2][i_hi]
+    assert exp.extreme_images['lowest']['name'] == batch[2][i_lo]
+    assert abs(exp.extreme_images['highest']['loss'] - float(per_img[i_hi])) < 1e-7
+
+
+def test_iwae_shaped_recon_per_image():
+    x = torch.rand(2, 3, 4, 4)
+    r = torch.rand(2, 5, 3, 4, 4)
+    got = VAEXperiment.per_image_mse(r, x)
+    want = ((r - x.unsqueeze(1)) ** 2).mean(dim=[1, 2, 3, 4])
+    assert torch.allclose(got, want)
+
+
+def test_configure_optimizers_variants():
+    m = TinyAE()
+    optims, scheds = VAEXperiment(m, dict(PARAMS)).configure_optimizers()
+    assert isinstance(optims[0], torch.optim.Adam) and optims[0].defaults['lr'] == 0.005
+    assert isinstance(scheds[0]['scheduler'], torch.optim.lr_scheduler.ExponentialLR) and scheds[0]['interval'] == 'epoch'
+    d = VAEXperiment(m, dict(PARAMS, adaptive_lr=True)).configure_optimizers()
+    assert isinstance(d['lr_scheduler']['scheduler'], torch.optim.lr_scheduler.ReduceLROnPlateau)
+    assert d['lr_scheduler']['monitor'] == 'val_loss'
+    p = dict(PARAMS)
+    p['scheduler_gamma'] = None
+    o = VAEXperiment(m, p).configure_optimizers()
+    assert isinstance(o, list) and len(o) == 1
+
+
+def test_fit_steps_and_exponential_lr():
+    m = TinyAE()
+    exp = VAEXperiment(m, dict(PARAMS))
+    batches = [_batch(s) for s in range(3)]
+    before = [p.detach().clone() for p in m.parameters()]
+    hist = fit(exp, batches, epochs=2, val_batches=[_batch(9)])
+    assert len(hist) == 2 and 'val_loss' in hist[0] and 'loss' in hist[0]
+    assert any(not torch.equal(a, b) for a, b in zip(before, m.parameters()))
+    assert hist[1]['loss'] < hist[0]['loss']

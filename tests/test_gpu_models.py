@@ -89,3 +89,49 @@ def test_models_bf16_step_runs_and_trains():
         opt.step()
         first = float(loss) if first is None else first
     assert float(loss) < first
+
+
+def test_vqvae_dropin_forward_loss_backward():
+    """VQVAE through the drop-in (reference forward/loss_function signatures): loss dict against
+    the teacher-forced oracle, flat-parameter gradients through loss.backward()."""
+    from oracle import vae_oracle as O
+    from vae_amd.models import vae_models
+    meta, ref = load_case("vq_b4")
+    sd, x, _ = case_inputs(meta)
+    model = vae_models["VQVAE"](**meta["ctor"], dtype=torch.float32, device="cuda")
+    model.load_reference_state_dict(sd)
+    results = model(x.cuda())
+    assert len(results) == 3
+    losses = model.loss_function(*results, M_N=meta["M_N"], optimizer_idx=0, batch_idx=0)
+    assert set(losses) == {"loss", "Reconstruction_Loss", "VQ_Loss"}
+    plan = model._plan(x.shape[0])
+    o = O.train_step("VQVAE", sd, x, M_N=0.0, lr=meta["lr"], vq_beta=meta["ctor"]["beta"],
+                     vq_indices=plan.indices.cpu(), do_adam=False)
+    for k in ("loss", "Reconstruction_Loss", "VQ_Loss"):
+        assert abs(float(losses[k]) - o["loss"][k]) <= 1e-4 * abs(o["loss"][k]), (k, float(losses[k]), o["loss"][k])
+    model.zero_grad(set_to_none=True)
+    losses["loss"].backward()
+    grads = model.net.layout.export_reference(model.flat.grad.detach())
+    for name, gr in o["grads"].items():
+        err = float((grads[name].cpu() - gr).norm() / gr.norm().clamp_min(1e-30))
+        assert err < 1e-3, (name, err)
+
+
+def test_experiment_training_step_on_gpu_model():
+    """vae_amd.experiment.VAEXperiment.training_step drives the drop-in model (experiment.py:45-86)."""
+    from vae_amd.experiment import VAEXperiment
+    from vae_amd.models import VanillaVAE
+    model = VanillaVAE(3, 128, dtype=torch.float32, device="cuda", seed=1265)
+    exp = VAEXperiment(model, {'LR': 0.005, 'weight_decay': 0.0, 'scheduler_gamma': 0.95, 'kld_weight': 2.5e-4})
+    optims, scheds = exp.configure_optimizers()
+    x = torch.rand(16, 3, 64, 64, device="cuda")
+    batch = (x, torch.zeros(16, dtype=torch.float64), [f"{i}.png" for i in range(16)])
+    losses = []
+    for i in range(4):
+        optims[0].zero_grad(set_to_none=True)
+        loss = exp.training_step(batch, i)
+        loss.backward()
+        optims[0].step()
+        losses.append(float(exp.logged["loss"]))
+    assert losses[-1] < losses[0]
+    assert exp.extreme_images["highest"]["loss"] >= exp.extreme_images["lowest"]["loss"]

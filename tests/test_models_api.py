@@ -12,14 +12,14 @@ def test_registry_names_and_aliases_mirror_reference():
              'VanillaVAE', 'ConditionalVAE', 'CategoricalVAE'}
     assert set(M.vae_models) == names
     assert M.VAE is M.VanillaVAE and M.GaussianVAE is M.VanillaVAE
-    for name in ('VanillaVAE', 'BetaVAE', 'IWAE'):
+    for name in ('VanillaVAE', 'BetaVAE', 'IWAE', 'VQVAE'):
         assert issubclass(M.vae_models[name], M.BaseVAE)
 
 
 def test_families_off_the_path_fail_loudly():
     from vae_amd import models as M
     with pytest.raises(NotImplementedError):
-        M.vae_models['VQVAE'](in_channels=3, embedding_dim=64, num_embeddings=512)
+        M.vae_models['WAE_MMD'](in_channels=3, latent_dim=128)
 
 
 def test_constructor_kwargs_match_reference():
@@ -31,3 +31,6 @@ def test_constructor_kwargs_match_reference():
         assert k in p
     assert 'num_samples' in inspect.signature(M.IWAE.__init__).parameters
     assert list(inspect.signature(M.VanillaVAE.forward).parameters)[:2] == ['self', 'input']
+    q = inspect.signature(M.VQVAE.__init__).parameters
+    for k in ('in_channels', 'embedding_dim', 'num_embeddings', 'hidden_dims', 'beta', 'img_size'):
+        assert k in q                                   # configs/vae/vq_vae.yaml model_params
