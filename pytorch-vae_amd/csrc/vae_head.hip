@@ -133,6 +133,15 @@ __global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
   tile_load(q, ry, n, h0, raw);
   // B fragments: W[co = lane&15][tap][8*(lane>>4) .. +7] (zero for co >= 3)
   const int co = lane & 15, g = lane >> 4;
+  // the epilogue's target pixels, in flight with the tile (no global load after the MFMAs)
+  f32x4v tgv[4];
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    const int grp = wave * 4 + gi, row = grp >> 2, c0 = (grp & 3) * 16;
+    tgv[gi] = co < NCO ? *reinterpret_cast<const f32x4v*>(q.target + (((long)(n / q.samples) * NCO + co) * q.h + h0 + row) * HW +
+                                                         c0 + 4 * g)
+                       : f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
   bf16x8 bw[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -150,6 +159,7 @@ __global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
     const int grp = wave * 4 + gi;                  // 16 groups of 16 pixels
     const int row = grp >> 2, c0 = (grp & 3) * 16;
     f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+    const f32x4v tg = tgv[gi];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int r = t / 3, s = t - 3 * (t / 3);
@@ -163,7 +173,6 @@ __global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) y[i] = tanhf(acc[i] + bco);
       *reinterpret_cast<f32x4v*>(q.recon + (((long)n * NCO + co) * q.h + hh) * HW + w0) = y;
-      const f32x4v tg = *reinterpret_cast<const f32x4v*>(q.target + (((long)img_t * NCO + co) * q.h + hh) * HW + w0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) { const float d = y[i] - tg[i]; sq = fmaf(d, d, sq); }
     }
@@ -243,6 +252,20 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
 #pragma unroll
       for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = ok ? gseed(q, n, c2, hi, wi) : 0.f;
     }
+    // the data epilogue's y (pre-BN) at this lane's pixels x channels of its 4 groups: issued
+    // with the tile so the MFMA phase has no global round trip
+    float yv[4][2][4];
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) {
+      const int grp = wave * 4 + gi, row = grp >> 2, c0 = (grp & 3) * 16;
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t off = (uint32_t)((((n * q.h + h0 + row) * HW + c0 + 4 * g + i) * HC + nf * 16 + li) * 2);
+          yv[gi][nf][i] = q.data ? bf2f(__builtin_amdgcn_raw_buffer_load_b16(ry, off, 0, 0)) : 0.f;
+        }
+    }
     __syncthreads();                    // previous tile's LDS reads done (and tables ready)
     tile_store(q, h0, raw, tile, ta, tb);
 #pragma unroll
@@ -270,15 +293,6 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
         const int grp = wave * 4 + gi;
         const int row = grp >> 2, c0 = (grp & 3) * 16;
         const int hh = h0 + row;
-        // epilogue inputs first: y at this lane's 4 pixels x 2 channels (L2-resident)
-        float yv[2][4];
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t off = (uint32_t)((((n * q.h + hh) * HW + c0 + 4 * g + i) * HC + nf * 16 + li) * 2);
-            yv[nf][i] = bf2f(__builtin_amdgcn_raw_buffer_load_b16(ry, off, 0, 0));
-          }
         f32x4v acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -304,7 +318,7 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
           const int c = nf * 16 + li;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float y = yv[nf][i];
+            const float y = yv[gi][nf][i];
             const float z = fmaf(y, ta[c], tb[c]);
             const float gg = z > 0.f ? acc[nf][i] : acc[nf][i] * q.xf.slope;
             s1[nf] += gg;
@@ -399,28 +413,35 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
   }
 }
 
-// Column sums of a [rows][ld] fp32 slab (first `cols` columns) accumulated into dst, in a fixed
-// row order per column.
-__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, int cols, int ld, float* dst) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;
-  __shared__ float red[4][64];
+// Column sums of the [rows][SLAB_COLS] fp32 slab of per-block filter partials, added into dw
+// (columns < NW) and db (the NCO columns after): 16 columns x 16 row-parts per workgroup, each
+// part's loads issued together, parts combined in a fixed order (deterministic).
+constexpr int RR_COLS = 16, RR_PARTS = 16, RR_UNROLL = 8;
+__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, float* dw, float* db) {
+  __shared__ float red[RR_PARTS][RR_COLS];
+  const int cl = threadIdx.x % RR_COLS, part = threadIdx.x / RR_COLS;
+  const int c = blockIdx.x * RR_COLS + cl;
   float s = 0.f;
-  if (c < cols) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int r = part;
-    for (; r + 12 < rows; r += 16) {
-      a0 += src[(long)r * ld + c];
-      a1 += src[(long)(r + 4) * ld + c];
-      a2 += src[(long)(r + 8) * ld + c];
-      a3 += src[(long)(r + 12) * ld + c];
+  if (c < SLAB_COLS && (c < NW || db)) {
+    for (int r0 = part; r0 < rows; r0 += RR_PARTS * RR_UNROLL) {
+      float v[RR_UNROLL];
+#pragma unroll
+      for (int u = 0; u < RR_UNROLL; ++u) {
+        const int r = r0 + u * RR_PARTS;
+        v[u] = r < rows ? src[(long)r * SLAB_COLS + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < RR_UNROLL; ++u) s += v[u];
     }
-    for (; r < rows; r += 4) a0 += src[(long)r * ld + c];
-    s = (a0 + a1) + (a2 + a3);
   }
-  red[part][threadIdx.x & 63] = s;
+  red[part][cl] = s;
   __syncthreads();
-  if (part == 0 && c < cols) dst[c] += (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+  if (part != 0 || c >= SLAB_COLS) return;
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < RR_PARTS; ++i) t += red[i][cl];
+  if (c < NW) dw[c] += t;
+  else if (db) db[c - NW] += t;
 }
 
 bool head_mfma_ok(const vae_head_args* a) {
@@ -469,14 +490,9 @@ int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStre
   int rc = check_launch("head_bwd_mfma");
   if (rc || !filter) return rc;
   if (slab) {
-    hipLaunchKernelGGL(reduce_rows_kernel, dim3((NW + 63) / 64), dim3(256), 0, st, (const float*)ws, grid, NW,
-                       SLAB_COLS, a->dw);
-    if ((rc = check_launch("reduce_rows dw"))) return rc;
-    if (a->db) {
-      hipLaunchKernelGGL(reduce_rows_kernel, dim3(1), dim3(256), 0, st, (const float*)(ws + NW), grid, NCO,
-                         SLAB_COLS, a->db);
-      rc = check_launch("reduce_rows db");
-    }
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3((SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st, (const float*)ws,
+                       grid, a->dw, a->db);
+    rc = check_launch("reduce_rows");
   }
   return rc;
 }

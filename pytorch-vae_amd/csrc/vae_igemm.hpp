@@ -805,7 +805,7 @@ template <int PER> constexpr int ring_stages() { return PER <= 2 ? 4 : (PER <= 4
 // T: LDS/MFMA type; TA: storage type of the A tensor (fp32 for the NCHW image / d[mu|logvar]);
 // TB: storage type of B (the gathered activation for B_GATHER, weights otherwise).
 // DYA / DYB: the A / B operand may carry a BN_DY transform (its aux tensor is loaded).
-template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM, bool VEC, bool DYA, bool DYB>
+template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM, bool VA, bool VB, bool DYA, bool DYB>
 __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   constexpr int BK = bk_of<T>();
   constexpr int LDK = BK + (sizeof(T) == 4 ? 4 : 8);        // padded LDS row (elements)
@@ -868,10 +868,10 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   const Src<TA> sa = make_src<TA>(p.a_ptr, p.a_bytes, p.a_xf);
   const Src<TB> sb = make_src<TB>(p.b_ptr, p.b_bytes, p.b_xf);
   const PhaseInfo pq = make_phase(p, phase);
-  RowOperand<TA, A_MODE, VEC> ars[A_VM ? 1 : A_PER];
-  ColOperand<TA, A_MODE, VEC> acs[A_VM ? A_PER : 1];
-  RowOperand<TB, B_MODE, VEC> brs[B_VM ? 1 : B_PER];
-  ColOperand<TB, B_MODE, VEC> bcs[B_VM ? B_PER : 1];
+  RowOperand<TA, A_MODE, VA> ars[A_VM ? 1 : A_PER];
+  ColOperand<TA, A_MODE, VA> acs[A_VM ? A_PER : 1];
+  RowOperand<TB, B_MODE, VB> brs[B_VM ? 1 : B_PER];
+  ColOperand<TB, B_MODE, VB> bcs[B_VM ? B_PER : 1];
 #pragma unroll
   for (int i = 0; i < A_PER; ++i) {
     const int o = tid + i * NTHREADS;
@@ -897,8 +897,8 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     const int kb = kt * BK;
     const int kv = kb + (tid % KO) * 8;      // V_K operands: this thread's k (same for all its octets)
     KTap tpa, tpb;
-    if constexpr (!A_VM && VEC) tpa = RowOperand<TA, A_MODE, VEC>::tap(p, pq, p.fd_ach, p.a_xf.channels, a_bn, kv, kend);
-    if constexpr (!B_VM && VEC) tpb = RowOperand<TB, B_MODE, VEC>::tap(p, pq, p.fd_bch, p.b_xf.channels, b_bn, kv, kend);
+    if constexpr (!A_VM && VA) tpa = RowOperand<TA, A_MODE, VA>::tap(p, pq, p.fd_ach, p.a_xf.channels, a_bn, kv, kend);
+    if constexpr (!B_VM && VB) tpb = RowOperand<TB, B_MODE, VB>::tap(p, pq, p.fd_bch, p.b_xf.channels, b_bn, kv, kend);
 #pragma unroll
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
@@ -921,13 +921,13 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     for (int i = 0; i < A_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (A_OCT % NTHREADS == 0 || o < A_OCT) {
-        if constexpr (VEC) {
+        if constexpr (VA) {
           if constexpr (!A_VM) store_vk<T, TA, DYA>(sa, ta, qa[i], As[buf] + (o / KO) * LDK + (o % KO) * 8);
           else store_vm<T, TA, A_MODE, DYA>(sa, ta, qa[i], As[buf] + (o % (BM / 4)) * 4 * LDK + 2 * (o / (BM / 4)), LDK);
           continue;
         }
         float v[8];
-        finish<TA, A_MODE, A_VM, VEC, DYA>(p, sa, ta, qa[i], v);
+        finish<TA, A_MODE, A_VM, VA, DYA>(p, sa, ta, qa[i], v);
         if constexpr (!A_VM) {
           st8(As[buf] + (o / KO) * LDK + (o % KO) * 8, v);
         } else {
@@ -941,13 +941,13 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
     for (int i = 0; i < B_PER; ++i) {
       const int o = tid + i * NTHREADS;
       if (B_OCT % NTHREADS == 0 || o < B_OCT) {
-        if constexpr (VEC) {
+        if constexpr (VB) {
           if constexpr (!B_VM) store_vk<T, TB, DYB>(sb, tb, qb[i], Bs[buf] + (o / KO) * LDK + (o % KO) * 8);
           else store_vm<T, TB, B_MODE, DYB>(sb, tb, qb[i], Bs[buf] + (o % (BN / 4)) * 4 * LDK + 2 * (o / (BN / 4)), LDK);
           continue;
         }
         float v[8];
-        finish<TB, B_MODE, B_VM, VEC, DYB>(p, sb, tb, qb[i], v);
+        finish<TB, B_MODE, B_VM, VB, DYB>(p, sb, tb, qb[i], v);
         if constexpr (!B_VM) {
           st8(Bs[buf] + (o / KO) * LDK + (o % KO) * 8, v);
         } else {

@@ -176,11 +176,11 @@ inline int launch_finalize(const GemmParams& p, hipStream_t st) {
 
 #define VAE_TILE_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VEC, DYA, DYB>), grid, block, lds, st, p); \
+    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VA, VB, DYA, DYB>), grid, block, lds, st, p); \
     return; \
   }
 
-template <class T, class TA, class TB, int AM, int BMD, int EM, bool VEC, bool DYA, bool DYB>
+template <class T, class TA, class TB, int AM, int BMD, int EM, bool VA, bool VB, bool DYA, bool DYB>
 inline void launch_shape(const GemmParams& p, Tile t, hipStream_t st) {
   const dim3 block(NTHREADS);
   const dim3 grid((p.M + t.bm - 1) / t.bm, (p.N + t.bn - 1) / t.bn, p.nphase * p.ksplit);
@@ -218,10 +218,14 @@ inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
 #ifdef VAE_PROBE
   p.probe = vae_probe_buffer();
 #endif
-  const bool vec = operand_vec<AM>(p, p.a_ptr, p.a_xf, (int)sizeof(TA)) &&
-                   operand_vec<100 + BMD>(p, p.b_ptr, p.b_xf, (int)sizeof(TB));
-  if (vec) launch_shape<T, TA, TB, AM, BMD, EM, true, DYA, DYB>(p, t, st);
-  else launch_shape<T, TA, TB, AM, BMD, EM, false, DYA, DYB>(p, t, st);
+  // packed (vector) staging per operand: an operand that cannot be packed (the NCHW image, a
+  // 3-channel tensor or weight matrix) no longer drags the other one onto the per-element path
+  const bool va = operand_vec<AM>(p, p.a_ptr, p.a_xf, (int)sizeof(TA));
+  const bool vb = operand_vec<100 + BMD>(p, p.b_ptr, p.b_xf, (int)sizeof(TB));
+  if (va && vb) launch_shape<T, TA, TB, AM, BMD, EM, true, true, DYA, DYB>(p, t, st);
+  else if (va) launch_shape<T, TA, TB, AM, BMD, EM, true, false, DYA, DYB>(p, t, st);
+  else if (vb) launch_shape<T, TA, TB, AM, BMD, EM, false, true, DYA, DYB>(p, t, st);
+  else launch_shape<T, TA, TB, AM, BMD, EM, false, false, DYA, DYB>(p, t, st);
   int rc = check_launch("igemm");
   if (rc) return rc;
   if (EM != E_ACC && p.slab) return launch_finalize<T, EM>(p, st);
