@@ -209,6 +209,7 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
   __shared__ __attribute__((aligned(16))) uint2 gsA[TPIX];               // [pixel][co0..2, 0] bf16
   __shared__ __attribute__((aligned(16))) __bf16 gsT[4][OWN];            // [co][own pixel]
   __shared__ __attribute__((aligned(16))) __bf16 gst[4][16 * HC];        // per-wave output staging
+  __shared__ __attribute__((aligned(16))) char ytile[OWN * HC * 2];      // raw y of the own pixels
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float r1[4][HC], r2[4][HC], rdb[4][NCO];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -252,22 +253,22 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
 #pragma unroll
       for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = ok ? gseed(q, n, c2, hi, wi) : 0.f;
     }
-    // the data epilogue's y (pre-BN) at this lane's pixels x channels of its 4 groups: issued
-    // with the tile so the MFMA phase has no global round trip
-    float yv[4][2][4];
-#pragma unroll
-    for (int gi = 0; gi < 4; ++gi) {
-      const int grp = wave * 4 + gi, row = grp >> 2, c0 = (grp & 3) * 16;
-#pragma unroll
-      for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t off = (uint32_t)((((n * q.h + h0 + row) * HW + c0 + 4 * g + i) * HC + nf * 16 + li) * 2);
-          yv[gi][nf][i] = q.data ? bf2f(__builtin_amdgcn_raw_buffer_load_b16(ry, off, 0, 0)) : 0.f;
-        }
-    }
     __syncthreads();                    // previous tile's LDS reads done (and tables ready)
     tile_store(q, h0, raw, tile, ta, tb);
+    // raw y (pre-BN) of the own pixels for the data epilogue, from the same registers:
+    // [own pixel][32 ch] bf16, 16-byte chunks XOR-swizzled by (pixel & 3)
+    if (q.data) {
+#pragma unroll
+      for (int j = 0; j < OCT_PER_T; ++j) {
+        const int o = threadIdx.x + 256 * j;
+        if (o >= OCT) continue;
+        const int pix = o >> 2, chk = o & 3;
+        const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+        if (trow < 1 || trow > ROWS || tcol < 1 || tcol > HW) continue;
+        const int own = (trow - 1) * HW + (tcol - 1);
+        *reinterpret_cast<u32x4*>(ytile + own * (HC * 2) + ((chk ^ (own & 3)) << 4)) = raw[j];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int pix = gpix[j];
@@ -318,7 +319,8 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
           const int c = nf * 16 + li;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float y = yv[gi][nf][i];
+            const int own = row * HW + c0 + 4 * g + i;
+            const float y = (float)*reinterpret_cast<const __bf16*>(ytile + own * (HC * 2) + (((c >> 3) ^ (own & 3)) << 4) + (c & 7) * 2);
             const float z = fmaf(y, ta[c], tb[c]);
             const float gg = z > 0.f ? acc[nf][i] : acc[nf][i] * q.xf.slope;
             s1[nf] += gg;
