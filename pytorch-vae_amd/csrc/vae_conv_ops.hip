@@ -30,6 +30,30 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   const int S = a->stride;
   if (a->h % S || a->w % S || a->h / S != a->p || a->w / S != a->q)
     return fail(VAE_E_BADSHAPE, "conv2d_bwd_data: needs h == p*stride (got h=%d p=%d S=%d)", a->h, a->p, S);
+  const long wbytes = (long)a->k * a->r * a->r * a->c * 2;
+  if (S == 1 && a->dtype == VAE_BF16 && a->c % 8 == 0 && a->k % 8 == 0 && a->workspace &&
+      a->workspace_bytes >= 2 * wbytes && !getenv("VAE_NO_DGRAD_FLIP")) {
+    // stride 1: dx = conv(dy, W') with W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] and pad R-1-P — the
+    // forward conv path (k-contiguous weight rows, packed im2col gather of dy) instead of the
+    // phase-gather with k-strided weights.  W' lives at the end of the workspace.
+    char* ws = static_cast<char*>(a->workspace);
+    const long wsoff = ((a->workspace_bytes - wbytes) / 256) * 256;
+    __bf16* wf = reinterpret_cast<__bf16*>(ws + wsoff);
+    int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), wf, a->k, a->r, a->c, (hipStream_t)stream);
+    if (rc) return rc;
+    GemmParams p = base_params();
+    p.M = a->n * a->h * a->w; p.N = a->c; p.K = a->r * a->r * a->k;
+    p.a_ptr = a->dy; p.a_xf = sanitize(a->dy_xf);
+    p.b_ptr = wf; p.b_ld = p.K;
+    p.gn = a->n; p.gh = a->p; p.gw = a->q; p.gc = a->k; p.gp = a->h; p.gq = a->w;
+    p.gr = a->r; p.gs = 1; p.gpad = a->r - 1 - a->pad;
+    p.out = a->dx; p.out_ld = a->c;
+    p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
+    p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
+    p.residual = a->residual;
+    if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
+    return launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, ws, wsoff, (hipStream_t)stream);
+  }
   GemmParams p = base_params();
   if (!make_taps(p, S, a->r, a->pad)) return fail(VAE_E_UNSUPPORTED, "conv2d_bwd_data: stride/kernel");
   p.nphase = S * S;

@@ -354,6 +354,27 @@ __global__ void column_sum(const T* x, long rows, int C, float* out) {
   atomicAdd(out + c, s);
 }
 
+// W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] (bf16): the data gradient of a stride-1 conv as a conv
+__global__ void flip_weights_kernel(const __bf16* w, __bf16* wf, int K, int R, int C) {
+  const long n = (long)K * R * R * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    long t = i / K;
+    const int s = (int)(t % R); t /= R;
+    const int r = (int)(t % R);
+    const int c = (int)(t / R);
+    wf[i] = w[(((long)k * R + (R - 1 - r)) * R + (R - 1 - s)) * C + c];
+  }
+}
+
+inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C, hipStream_t st) {
+  const long n = (long)K * R * R * C;
+  long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(flip_weights_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w, wf, K, R, C);
+  return check_launch("flip_weights");
+}
+
 inline int column_sum_launch(int dtype, const void* dy, long rows, int C, float* db, hipStream_t st) {
   const dim3 grid(64, (C + 63) / 64);
   if (dtype == VAE_F32) hipLaunchKernelGGL(column_sum<float>, grid, dim3(256), 0, st, (const float*)dy, rows, C, db);

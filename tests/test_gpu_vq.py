@@ -177,3 +177,38 @@ def test_recon_kernel(dtype):
     torch.cuda.synchronize()
     want = (gr * (1 - r.detach() ** 2)).permute(0, 2, 3, 1)
     np.testing.assert_allclose(dy.float().cpu().numpy(), want.numpy(), rtol=tolr, atol=tolr * float(want.abs().max()))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("r,pad", [(3, 1), (1, 0)])
+def test_conv_stride1_bwd_data_residual_act(dtype, r, pad):
+    """conv2d_bwd_data at stride 1 (the ResidualLayer convs, vq_vae.py:62-66): dx = W^T * dy + skip,
+    times lrelu'(x_pre) — against torch autograd in fp32 (bf16 runs the flipped-weight conv path)."""
+    from gpu_util import nhwc, to_nchw
+    from vae_amd import _lib as L
+    g = torch.Generator().manual_seed(11 + r)
+    n, hw, c, k = 2, 8, 32, 64
+    x_pre = torch.randn(n, c, hw, hw, generator=g)
+    w = torch.randn(k, c, r, r, generator=g) * 0.1
+    dy = torch.randn(n, k, hw, hw, generator=g)
+    skip = torch.randn(n, c, hw, hw, generator=g)
+    xa = torch.nn.functional.leaky_relu(x_pre, 0.01).requires_grad_(True)
+    y = torch.nn.functional.conv2d(xa, w, None, padding=pad)
+    (y * dy).sum().backward()
+    want = (xa.grad + skip) * torch.where(x_pre > 0, 1.0, 0.01)
+    dev = dict(dtype=dtype)
+    wn = w.permute(0, 2, 3, 1).contiguous().to(device="cuda", **dev)
+    dy_d, skip_d, xp_d = nhwc(dy, dtype), nhwc(skip, dtype), nhwc(x_pre, dtype)
+    dx = torch.empty_like(xp_d)
+    ws = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+    a = L.ConvArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=c, k=k, p=hw, q=hw, r=r, stride=1, pad=pad)
+    a.dy, a.wt, a.dx, a.residual = dy_d.data_ptr(), wn.data_ptr(), dx.data_ptr(), skip_d.data_ptr()
+    a.dx_epi = L.Xform(kind=L.X_ACT, channels=c, slope=0.01)
+    a.dx_epi.aux = xp_d.data_ptr()
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    L.call("vae_conv2d_bwd_data", a, L.stream_ptr())
+    torch.cuda.synchronize()
+    got = to_nchw(dx)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    err = float((got - want).abs().max() / want.abs().max())
+    assert err < tol, err
