@@ -193,7 +193,10 @@ typedef struct vae_head_args {
  *   mode 1 (backward): xf.dgamma/dbeta replicas -> table [3][C]; dL/dgamma, dL/dbeta added to
  *                      xf.dgamma_out / dbeta_out; when db is set, the gradient of the bias of
  *                      the conv feeding the BatchNorm is added in closed form,
- *                      db_c = A*Σg + B*Σy + C*M. */
+ *                      db_c = A*Σg + B*Σy + C*M.
+ *   mode 2 (eval):     table [4][C] from xf.running_mean / running_var (BatchNorm2d in eval
+ *                      mode — validation_step, sample, generate: experiment.py:122-132,
+ *                      vanilla_vae.py:148-173); nothing is updated. */
 typedef struct vae_bn_args {
   int32_t mode;
   vae_xform xf;

@@ -411,6 +411,22 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) {
   }
 }
 
+// Eval-mode BatchNorm: the forward table from the running statistics (torch eval semantics:
+// (y - running_mean) / sqrt(running_var + eps) * gamma + beta).
+__global__ void __launch_bounds__(256) bn_eval_table_kernel(vae_bn_args a) {
+  const vae_xform& x = a.xf;
+  const int C = x.channels;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const float mean = x.running_mean[c];
+  const float invstd = 1.0f / sqrtf(x.running_var[c] + x.eps);
+  const float sc = x.gamma[c] * invstd;
+  a.table[c] = sc;
+  a.table[C + c] = x.beta[c] - mean * sc;
+  a.table[2 * C + c] = invstd;
+  a.table[3 * C + c] = -mean * invstd;
+}
+
 // ------------------------------------------------------------------ reparameterization
 template <class T>
 __global__ void reparam_kernel(int rows, int samples, int D, const float* mulv, const float* eps, T* z) {
@@ -638,7 +654,12 @@ extern "C" int vae_bn_finalize(const vae_bn_args* a, void* stream) {
   if (!a || !a->table || a->xf.channels <= 0 || !a->xf.sum || !a->xf.sumsq || !a->xf.gamma || !a->xf.beta ||
       a->xf.count <= 0.f)
     return fail(VAE_E_BADARG, "bn_finalize: args");
-  if (a->mode != 0 && a->mode != 1) return fail(VAE_E_BADARG, "bn_finalize: mode %d", a->mode);
+  if (a->mode < 0 || a->mode > 2) return fail(VAE_E_BADARG, "bn_finalize: mode %d", a->mode);
+  if (a->mode == 2) {
+    if (!a->xf.running_mean || !a->xf.running_var) return fail(VAE_E_BADARG, "bn_finalize: eval mode needs running statistics");
+    hipLaunchKernelGGL(bn_eval_table_kernel, dim3((a->xf.channels + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
+    return check_launch("bn_finalize(eval)");
+  }
   if (a->mode == 1 && (!a->xf.dgamma || !a->xf.dbeta)) return fail(VAE_E_BADARG, "bn_finalize: backward sums");
   if (a->xf.reps > BNF_LANES * BNF_PER) return fail(VAE_E_UNSUPPORTED, "bn_finalize: %d replicas > %d", a->xf.reps, BNF_LANES * BNF_PER);
   const int grid = (a->xf.channels + 63) / 64;

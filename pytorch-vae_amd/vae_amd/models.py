@@ -18,8 +18,9 @@ gradient of the flat parameter buffer.  Optimizers see one flat nn.Parameter (`m
 `reference_state_dict()` / `load_reference_state_dict()` convert to the reference's keys and
 layouts (vae_amd/layout.py).
 
-Training-mode BatchNorm only: eval-mode inference (running statistics) is the next row of the
-build plan; sample()/generate() in eval mode raise NotImplementedError.
+model.train(): train-mode BatchNorm (batch statistics, running-stat update) and the fused HIP
+backward; model.eval(): eval-mode BatchNorm from the running statistics, forward only
+(validation_step, sample, generate).
 """
 from __future__ import annotations
 
@@ -114,16 +115,32 @@ class _HipVAE(BaseVAE):
         self.flat = nn.Parameter(self.net.params)      # shares storage with the kernels' buffer
         self._plans: Dict[int, StepPlan] = {}
 
-    def _plan(self, batch: int) -> StepPlan:
-        if batch not in self._plans:
-            self._plans[batch] = StepPlan(self.net, batch, loss="iwae" if self.samples > 1 else "vanilla",
-                                          samples=self.samples, fused_loss=False)
-        return self._plans[batch]
+    def _plan(self, batch: int, training: Optional[bool] = None) -> StepPlan:
+        """Launch plan for a batch size: train-mode BatchNorm (batch statistics, running-stat
+        update, backward) or, under model.eval(), eval-mode BatchNorm from the running statistics
+        (forward only)."""
+        training = self.training if training is None else training
+        key = (batch, training)
+        if key not in self._plans:
+            self._plans[key] = StepPlan(self.net, batch, loss="iwae" if self.samples > 1 else "vanilla",
+                                        samples=self.samples, fused_loss=False, training=training)
+        return self._plans[key]
 
-    def _check_train(self, what: str):
-        if not self.training:
-            raise NotImplementedError(f"{what}: eval-mode BatchNorm (running statistics) is not implemented "
-                                      f"on the MI355X path yet (DESIGN.md §7); call model.train()")
+    def _eval_forward(self, input: Tensor, eps: Optional[Tensor]):
+        """model.eval() forward (no autograd): encoder, reparameterization, decoder with running
+        BatchNorm statistics (vanilla_vae.py:119-122 under eval())."""
+        B = input.shape[0]
+        if eps is None:
+            eps = torch.randn(B * self.samples, self.latent_dim, device=input.device)
+        plan = self._plan(B, False)
+        st = L.stream_ptr()
+        self.net.sync_lowp()
+        plan.x.copy_(input.detach().to(plan.x.dtype))
+        plan.eps.copy_(eps.detach().reshape(plan.eps.shape))
+        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, plan.step.data_ptr(), st)
+        plan._run(plan.fwd_calls[:plan.n_decode1], st)
+        D = self.latent_dim
+        return plan.recon.clone(), plan.mulv[:, :D].clone(), plan.mulv[:, D:].clone(), eps
 
     # ---- reference state dict interop (models/vanilla_vae.py parameter names and layouts)
     def reference_state_dict(self) -> Dict[str, Tensor]:
@@ -141,7 +158,6 @@ class _HipVAE(BaseVAE):
         return eps * std + mu
 
     def encode(self, input: Tensor) -> List[Tensor]:
-        self._check_train("encode")
         plan = self._plan(input.shape[0])
         st = L.stream_ptr()
         self.net.sync_lowp()
@@ -152,7 +168,6 @@ class _HipVAE(BaseVAE):
         return [plan.mulv[:, :D].clone(), plan.mulv[:, D:].clone()]
 
     def decode(self, z: Tensor) -> Tensor:
-        self._check_train("decode")
         rows = z.reshape(-1, self.latent_dim).shape[0]
         plan = self._plan(rows // self.samples)
         st = L.stream_ptr()
@@ -163,15 +178,15 @@ class _HipVAE(BaseVAE):
         return plan.recon.clone()
 
     def _run(self, input: Tensor, eps: Optional[Tensor] = None):
-        self._check_train("forward")
+        if not self.training:
+            return self._eval_forward(input, eps)
         B = input.shape[0]
         if eps is None:                                 # torch.randn_like(std), vanilla_vae.py:116
             eps = torch.randn(B * self.samples, self.latent_dim, device=input.device)
         return _VAEStep.apply(self.flat, input, eps, self) + (eps,)
 
     def sample(self, num_samples: int, current_device: int, **kwargs) -> Tensor:
-        """vanilla_vae.py:148-161 (needs eval-mode BatchNorm: next row)."""
-        self._check_train("sample")
+        """vanilla_vae.py:148-161."""
         z = torch.randn(num_samples, self.latent_dim, device=current_device)
         return self.decode(z)
 

@@ -110,9 +110,12 @@ class StepPlan:
 
     def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
-                 capacity_max_iter: float = 1e5, fused_loss: bool = True):
+                 capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True):
         self.net = net
         self.B = batch
+        # training=False: eval-mode BatchNorm (running statistics, nothing updated; the
+        # reference's validation_step / sample / generate under model.eval()) — forward only
+        self.training = training
         # fused_loss: the ELBO runs on the GPU inside the step and seeds the backward itself.
         # False (the BaseVAE drop-in, vae_amd.models): the loss is computed by the caller from
         # recon/mu/log_var and the backward is seeded with dL/drecon (grad_recon) and
@@ -238,9 +241,9 @@ class StepPlan:
         (table + dγ, dβ + the producing conv's bias gradient in closed form)."""
         C = self.net.layout.bn_by_prefix[prefix].channels
         a = L.BnArgs(mode=mode)
-        a.xf = self.bn_xf(prefix, L.X_BN_DY if mode else L.X_BN_ACT, count, running=(mode == 0), table=False)
-        a.table = self.bntab[prefix].data_ptr() + (4 * 4 * C if mode else 0)
-        if mode:
+        a.xf = self.bn_xf(prefix, L.X_BN_DY if mode == 1 else L.X_BN_ACT, count, running=(mode != 1), table=False)
+        a.table = self.bntab[prefix].data_ptr() + (4 * 4 * C if mode == 1 else 0)
+        if mode == 1:
             a.xf.dgamma_out = self.g(prefix + ".weight")
             a.xf.dbeta_out = self.g(prefix + ".bias")
             a.db = self.g(self._bn_prod_bias(prefix))
@@ -272,6 +275,7 @@ class StepPlan:
             return t.shape[0] * t.shape[1] * t.shape[2]
 
         F = self.fwd_calls
+        fmode = 0 if self.training else 2            # bn_finalize: batch statistics / running statistics
         # ---------------------------------------------------------------- encoder
         sp = img
         for i in range(nenc):
@@ -286,9 +290,10 @@ class StepPlan:
             a.wt = net.w(f"encoder.{i}.0.weight")
             a.bias = net.p(f"encoder.{i}.0.bias")
             a.y = self.enc[i].data_ptr()
-            self.fwd_sums(a, enc_pre[i])
+            if self.training:
+                self.fwd_sums(a, enc_pre[i])
             self._add(F, "vae_conv2d_fwd", a)
-            self.bn_finalize(F, enc_pre[i], 0, cnt(self.enc[i]))
+            self.bn_finalize(F, enc_pre[i], fmode, cnt(self.enc[i]))
             sp //= 2
         # ---------------------------------------------------------------- fc_mu | fc_var
         a = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
@@ -323,9 +328,10 @@ class StepPlan:
             a.wt = net.w(dec_w[i] + ".weight")
             a.bias = net.p(dec_w[i] + ".bias")
             a.y = dec_out[i].data_ptr()
-            self.fwd_sums(a, dec_pre[i])
+            if self.training:
+                self.fwd_sums(a, dec_pre[i])
             self._add(F, "vae_convT2d_fwd", a)
-            self.bn_finalize(F, dec_pre[i], 0, cnt(dec_out[i]))
+            self.bn_finalize(F, dec_pre[i], fmode, cnt(dec_out[i]))
             prev, prev_pre = dec_out[i], dec_pre[i]
             sp *= 2
         # ---------------------------------------------------------------- head + SSE
@@ -354,6 +360,8 @@ class StepPlan:
             self._add(F, "vae_elbo_fwd", e)
 
         # ================================================================ backward
+        if not self.training:
+            return
         Bw = self.bwd_calls
         hb = L.HeadArgs(dtype=T, n=BS, h=img, w=img, c=r[-1], samples=self.S)
         hb.x = self.fin.data_ptr()
