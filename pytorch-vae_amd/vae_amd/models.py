@@ -38,7 +38,37 @@ Tensor = torch.Tensor
 
 
 class BaseVAE(nn.Module):
-    """models/base.py:5-28."""
+    """models/base.py:5-28.
+
+    state_dict() / load_state_dict() speak the reference's keys and PyTorch layouts (the one
+    flat nn.Parameter the optimizers see is an implementation detail): a Lightning checkpoint of
+    the experiment (`model.`-prefixed keys, run.py:80-84) has exactly the reference's entries,
+    and a reference-trained checkpoint loads unchanged (checkpoint interop)."""
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        net = getattr(self, "net", None)
+        if net is None:
+            return super()._save_to_state_dict(destination, prefix, keep_vars)
+        for k, v in self.reference_state_dict().items():
+            destination[prefix + k] = v
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
+                              error_msgs):
+        net = getattr(self, "net", None)
+        if net is None:
+            return super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                                 unexpected_keys, error_msgs)
+        expected = list(net.ref_order)
+        mine = {k[len(prefix):]: v for k, v in state_dict.items() if k.startswith(prefix)}
+        for k in expected:
+            if k not in mine:
+                missing_keys.append(prefix + k)
+        for k in mine:
+            if k not in expected and "." in k:
+                unexpected_keys.append(prefix + k)
+        if all(k in mine for k in expected):
+            with torch.no_grad():
+                self.load_reference_state_dict({k: mine[k] for k in expected})
 
     def __init__(self) -> None:
         super().__init__()
