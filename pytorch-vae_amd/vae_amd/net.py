@@ -110,7 +110,8 @@ class StepPlan:
 
     def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
-                 capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True):
+                 capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
+                 concurrent: bool = False):
         self.net = net
         self.B = batch
         # training=False: eval-mode BatchNorm (running statistics, nothing updated; the
@@ -187,6 +188,8 @@ class StepPlan:
         self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
+        # side stream for the weight gradients (run_calls); None: one stream
+        self.side = torch.cuda.Stream(device=dev) if (concurrent and training) else None
         self._build()
 
     # ------------------------------------------------------------------ helpers
@@ -471,11 +474,7 @@ class StepPlan:
 
     # ------------------------------------------------------------------ execution
     def _run(self, calls, stream):
-        for fn, arg in calls:
-            if fn == "vae_reparam_fwd":
-                L.call(fn, *self._reparam, stream)
-            else:
-                L.call(fn, arg, stream)
+        run_calls(self, calls, stream)
 
     def begin(self, stream=None):
         stream = stream if stream is not None else L.stream_ptr()
@@ -501,6 +500,35 @@ class StepPlan:
         o = self.out.tolist()
         third = "KLD"
         return {"loss": o[0], "Reconstruction_Loss": o[1], third: o[2]}
+
+
+# Weight-gradient calls: nothing later in the backward reads their output (only the optimizer),
+# so they run on a side stream, concurrent with the data-gradient chain that is the critical path.
+SIDE_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_linear_bwd_filter"))
+
+
+def run_calls(plan, calls, stream):
+    """Launch a call list on `stream`.  When the plan has a side stream (`plan.side`, and
+    `stream` is the current torch stream), every weight-gradient call waits for the work queued
+    on `stream` before it and runs on the side stream; the side stream is joined back into
+    `stream` at the end of the list.  Recorded inside a HIP graph capture this becomes the
+    graph's fork/join edges, so the replayed graph runs the two chains concurrently."""
+    side = getattr(plan, "side", None)
+    main = torch.cuda.current_stream() if side is not None else None
+    if main is not None and main.cuda_stream != stream:
+        side = None                          # an explicit foreign stream: keep everything on it
+    forked = False
+    for fn, arg in calls:
+        if fn == "vae_reparam_fwd":
+            L.call(fn, *plan._reparam, stream)
+        elif side is not None and fn in SIDE_FNS:
+            side.wait_stream(main)
+            L.call(fn, arg, side.cuda_stream)
+            forked = True
+        else:
+            L.call(fn, arg, stream)
+    if forked:
+        main.wait_stream(side)
 
 
 def bn_reps(channels: int) -> int:

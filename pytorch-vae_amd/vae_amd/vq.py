@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 from .layout import Layout, default_init, vq_layout, vq_param_spec
-from .net import SLOPE, WORKSPACE_BYTES, _pad4
+from .net import SLOPE, WORKSPACE_BYTES, _pad4, run_calls
 
 NRES = 6             # ResidualLayers per stack (vq_vae.py:111, :138)
 
@@ -99,7 +99,7 @@ class VQStepPlan:
 
     loss_kind = L.LOSS_VQ
 
-    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True):
+    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True, concurrent: bool = True):
         self.net, self.B, self.beta, self.fused_loss = net, batch, beta, fused_loss
         dev, T = net.device, net.dtype
         h, E, img = net.hidden_dims, net.embedding_dim, net.img_size
@@ -141,8 +141,10 @@ class VQStepPlan:
         # backward buffers
         self.g_y = torch.empty_like(self.y)
         self.g_up = [torch.empty_like(t) for t in self.up]
-        self.g_h = [torch.empty(*m, **act) for _ in range(2)]       # ping-pong residual-stream grads
-        self.g_t = torch.empty(*m, **act)
+        # residual-stream gradients: a buffer per layer and stack (nothing is reused inside a
+        # backward, so the weight gradients on the side stream never race the data gradients)
+        self.g_h = {st: [torch.empty(*m, **act) for _ in range(NRES + 1)] for st in ("encoder", "decoder")}
+        self.g_t = {st: [torch.empty(*m, **act) for _ in range(NRES)] for st in ("encoder", "decoder")}
         self.g_q = torch.empty_like(self.q)
         self.g_lat = torch.empty_like(self.latpre)
         self.g_enc = [torch.empty_like(t) for t in self.enc]
@@ -156,6 +158,7 @@ class VQStepPlan:
         self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
+        self.side = torch.cuda.Stream(device=dev) if concurrent else None     # weight gradients (run_calls)
         self._build()
 
     # ------------------------------------------------------------------ helpers
@@ -198,19 +201,20 @@ class VQStepPlan:
             b.y = hs[j].data_ptr()
             self._add(F, "vae_conv2d_fwd", b)
 
-    def _res_stack_bwd(self, pre: str, first_idx: int, x0: torch.Tensor, ts, hs, gi: int) -> int:
-        """Backward of the residual stack.  g_h[gi] holds dL/dh_6 on entry; returns the index of
-        the buffer holding dL/dx0 (the gradient w.r.t. the stored pre-activation x0)."""
+    def _res_stack_bwd(self, pre: str, first_idx: int, x0: torch.Tensor, ts, hs) -> torch.Tensor:
+        """Backward of the residual stack.  g_h[pre][NRES] holds dL/dh_6 on entry; returns the
+        buffer holding dL/dx0 (the gradient w.r.t. the stored pre-activation x0)."""
         Bw, net = self.bwd_calls, self.net
         C = x0.shape[3]
+        gh, gt_ = self.g_h[pre], self.g_t[pre]
         for j in reversed(range(NRES)):
             idx = first_idx + j
-            dh, dnext = self.g_h[gi], self.g_h[1 - gi]
+            dh, dnext, gt = gh[j + 1], gh[j], gt_[j]
             hin, hin_xf = (x0, _act()) if j == 0 else (hs[j - 1], L.Xform())
             # Conv1x1: dt = W1^T dh * relu'(t)
             a = self._conv(ts[j], C, C, 1, 1, 0)
             a.dy, a.wt = dh.data_ptr(), net.w(f"{pre}.{idx}.resblock.2.weight")
-            a.dx, a.dx_epi = self.g_t.data_ptr(), _act(0.0, ts[j])
+            a.dx, a.dx_epi = gt.data_ptr(), _act(0.0, ts[j])
             self._add(Bw, "vae_conv2d_bwd_data", a)
             f = self._conv(ts[j], C, C, 1, 1, 0)
             f.x, f.x_xf = ts[j].data_ptr(), _act(0.0)
@@ -218,17 +222,16 @@ class VQStepPlan:
             self._add(Bw, "vae_conv2d_bwd_filter", f)
             # Conv3x3: dh_j = W3^T * dt + dh (skip connection) [* lrelu'(x0) for j == 0]
             a = self._conv(hin, C, C, 3, 1, 1)
-            a.dy, a.wt = self.g_t.data_ptr(), net.w(f"{pre}.{idx}.resblock.0.weight")
+            a.dy, a.wt = gt.data_ptr(), net.w(f"{pre}.{idx}.resblock.0.weight")
             a.dx, a.residual = dnext.data_ptr(), dh.data_ptr()
             if j == 0:
                 a.dx_epi = _act(SLOPE, x0)
             self._add(Bw, "vae_conv2d_bwd_data", a)
             f = self._conv(hin, C, C, 3, 1, 1)
             f.x, f.x_xf = hin.data_ptr(), hin_xf
-            f.dy, f.dw = self.g_t.data_ptr(), self.g(f"{pre}.{idx}.resblock.0.weight")
+            f.dy, f.dw = gt.data_ptr(), self.g(f"{pre}.{idx}.resblock.0.weight")
             self._add(Bw, "vae_conv2d_bwd_filter", f)
-            gi = 1 - gi
-        return gi
+        return gh[0]
 
     # ------------------------------------------------------------------ plan
     def _build(self):
@@ -316,7 +319,7 @@ class VQStepPlan:
             rb.dy, rb.grad_recon = self.g_y.data_ptr(), self.grad_recon.data_ptr()
             self._add(Bw, "vae_recon_bwd", rb)
         ups = [self.d_h[-1]] + self.up                      # inputs of the ConvTs
-        gups = [self.g_h[0]] + self.g_up                    # their gradients (pre-activation)
+        gups = [self.g_h["decoder"][NRES]] + self.g_up     # their gradients (pre-activation)
         gouts = self.g_up + [self.g_y]
         for i in reversed(range(len(r))):
             last = i == len(r) - 1
@@ -331,8 +334,7 @@ class VQStepPlan:
             f.x, f.x_xf = xin.data_ptr(), _act()
             f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
             self._add(Bw, "vae_convT2d_bwd_filter", f)
-        gi = self._res_stack_bwd("decoder", 1, self.d_in, self.d_t, self.d_h, 0)
-        g_din = self.g_h[gi]
+        g_din = self._res_stack_bwd("decoder", 1, self.d_in, self.d_t, self.d_h)
         a = self._conv(self.q, E, C, 3, 1, 1)
         a.dy, a.wt, a.dx = g_din.data_ptr(), net.w("decoder.0.0.weight"), self.g_q.data_ptr()
         self._add(Bw, "vae_conv2d_bwd_data", a)
@@ -344,14 +346,13 @@ class VQStepPlan:
         # encoder: Conv1x1 -> latents, residual stack, Conv3x3, strided convs
         a = self._conv(self.e_h[-1], C, E, 1, 1, 0)
         a.dy, a.wt = self.g_lat.data_ptr(), net.w(f"encoder.{ilat}.0.weight")
-        a.dx, a.dx_epi = self.g_h[0].data_ptr(), _act(SLOPE, self.e_h[-1])
+        a.dx, a.dx_epi = self.g_h["encoder"][NRES].data_ptr(), _act(SLOPE, self.e_h[-1])
         self._add(Bw, "vae_conv2d_bwd_data", a)
         f = self._conv(self.e_h[-1], C, E, 1, 1, 0)
         f.x, f.x_xf = self.e_h[-1].data_ptr(), _act()
         f.dy, f.dw, f.db = self.g_lat.data_ptr(), self.g(f"encoder.{ilat}.0.weight"), self.g(f"encoder.{ilat}.0.bias")
         self._add(Bw, "vae_conv2d_bwd_filter", f)
-        gi = self._res_stack_bwd("encoder", nh + 1, self.e_in, self.e_t, self.e_h, 0)
-        g_ein = self.g_h[gi]
+        g_ein = self._res_stack_bwd("encoder", nh + 1, self.e_in, self.e_t, self.e_h)
         a = self._conv(self.enc[-1], C, C, 3, 1, 1)
         a.dy, a.wt = g_ein.data_ptr(), net.w(f"encoder.{nh}.0.weight")
         a.dx, a.dx_epi = self.g_enc[-1].data_ptr(), _act(SLOPE, self.enc[-1])
@@ -380,8 +381,7 @@ class VQStepPlan:
 
     # ------------------------------------------------------------------ execution
     def _run(self, calls, stream):
-        for fn, arg in calls:
-            L.call(fn, arg, stream)
+        run_calls(self, calls, stream)
 
     def begin(self, stream=None):
         stream = stream if stream is not None else L.stream_ptr()
