@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 5
+#define VAE_ABI_VERSION 6
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -95,6 +95,25 @@ typedef struct vae_xform {
   const float* table;
 } vae_xform;
 
+/* One BatchNorm's per-step finalisation, run once between the kernel that produces its
+ * statistics and the kernels that consume them (vanilla_vae.py:30,56,71 BatchNorm2d in
+ * train mode; torch semantics for the running-statistic update).
+ *   mode 0 (forward):  xf.sum/sumsq replicas -> table [4][C]; running_mean/var updated
+ *                      (momentum, unbiased variance) when set.
+ *   mode 1 (backward): xf.dgamma/dbeta replicas -> table [3][C]; dL/dgamma, dL/dbeta added to
+ *                      xf.dgamma_out / dbeta_out; when db is set, the gradient of the bias of
+ *                      the conv feeding the BatchNorm is added in closed form,
+ *                      db_c = A*Σg + B*Σy + C*M.
+ *   mode 2 (eval):     table [4][C] from xf.running_mean / running_var (BatchNorm2d in eval
+ *                      mode — validation_step, sample, generate: experiment.py:122-132,
+ *                      vanilla_vae.py:148-173); nothing is updated. */
+typedef struct vae_bn_args {
+  int32_t mode;
+  vae_xform xf;
+  float* table;
+  float* db;
+} vae_bn_args;
+
 /* One convolution-family operation.  Geometry is that of the reference layer:
  *   Conv2d:          x [n,h,w,c] -> y [n,p,q,k]
  *   ConvTranspose2d: x [n,h,w,c] -> y [n,p,q,k]   (p = 2h for k3 s2 p1 op1 and k4 s2 p1)
@@ -135,6 +154,13 @@ typedef struct vae_conv_args {
   void* workspace;         /* fp32 scratch for split-K partial slabs (may be NULL: no split
                               of fwd / bwd_data); reused by every call on the stream */
   int64_t workspace_bytes;
+  /* Optional fused BatchNorm finalisation of the statistics this call produces (forward: the
+   * y_sum/y_sumsq of the next BatchNorm; bwd_data: its dx_dgamma/dx_dbeta): the call then also
+   * does what vae_bn_finalize(bn_finalize) would, in its last workgroup when the kernel path
+   * allows (else as a separate launch).  bn_counter: a uint32 that is 0 before the call (the
+   * step's zeroed region) and is left 0. */
+  const struct vae_bn_args* bn_finalize;
+  uint32_t* bn_counter;
 } vae_conv_args;
 
 /* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,
@@ -160,6 +186,13 @@ typedef struct vae_linear_args {
   int32_t samples;         /* rows per mu row (IWAE S; 1 otherwise) */
   void* workspace;         /* as vae_conv_args.workspace */
   int64_t workspace_bytes;
+  /* Optional fused BatchNorm finalisation of the statistics this call produces (forward: the
+   * y_sum/y_sumsq of the next BatchNorm; bwd_data: its dx_dgamma/dx_dbeta): the call then also
+   * does what vae_bn_finalize(bn_finalize) would, in its last workgroup when the kernel path
+   * allows (else as a separate launch).  bn_counter: a uint32 that is 0 before the call (the
+   * step's zeroed region) and is left 0. */
+  const struct vae_bn_args* bn_finalize;
+  uint32_t* bn_counter;
 } vae_linear_args;
 
 /* Final layer of the decoder: Conv2d(C->3, k3, s1, p1) + Tanh (vanilla_vae.py:73-75) and the
@@ -183,26 +216,11 @@ typedef struct vae_head_args {
   void* workspace;         /* bwd (bf16): fp32 scratch for per-workgroup dW/db partials (summed in a
                               fixed order); NULL: atomics straight into dw/db */
   int64_t workspace_bytes;
+  const struct vae_bn_args* bn_finalize;   /* as vae_conv_args.bn_finalize (bwd: final BatchNorm) */
+  uint32_t* bn_counter;
 } vae_head_args;
 
-/* One BatchNorm's per-step finalisation, run once between the kernel that produces its
- * statistics and the kernels that consume them (vanilla_vae.py:30,56,71 BatchNorm2d in
- * train mode; torch semantics for the running-statistic update).
- *   mode 0 (forward):  xf.sum/sumsq replicas -> table [4][C]; running_mean/var updated
- *                      (momentum, unbiased variance) when set.
- *   mode 1 (backward): xf.dgamma/dbeta replicas -> table [3][C]; dL/dgamma, dL/dbeta added to
- *                      xf.dgamma_out / dbeta_out; when db is set, the gradient of the bias of
- *                      the conv feeding the BatchNorm is added in closed form,
- *                      db_c = A*Σg + B*Σy + C*M.
- *   mode 2 (eval):     table [4][C] from xf.running_mean / running_var (BatchNorm2d in eval
- *                      mode — validation_step, sample, generate: experiment.py:122-132,
- *                      vanilla_vae.py:148-173); nothing is updated. */
-typedef struct vae_bn_args {
-  int32_t mode;
-  vae_xform xf;
-  float* table;
-  float* db;
-} vae_bn_args;
+
 
 /* Loss kinds (vanilla_vae.py:124-146, beta_vae.py:129-152, iwae.py:129-160, vq_vae.py:194-211) */
 enum vae_loss_kind { VAE_LOSS_VANILLA = 0, VAE_LOSS_BETA_H = 1, VAE_LOSS_BETA_B = 2, VAE_LOSS_IWAE = 3,

@@ -18,6 +18,8 @@ namespace vae {
 void set_error(const char* fmt, ...);
 int fail(int code, const char* fmt, ...);
 int check_launch(const char* what);
+// vae_bn_finalize as a host call (validation + launch); used by fused-finalisation fallbacks
+int bn_finalize_launch(const vae_bn_args* a, hipStream_t stream);
 // returned by a fast-path launcher whose preconditions do not hold (the caller falls back)
 constexpr int kHeadFallback = 0x7fff0001;
 
@@ -138,5 +140,107 @@ struct XfTable {
     }
   }
 };
+
+// ---------------------------------------------------------------- BatchNorm finalisation
+// The per-step BatchNorm table (vae_bn_args, vaehip.h) for channel groups cg0, cg0+cgs, ... of
+// 64 channels, by one 256-thread workgroup: every replica of every statistic a channel needs is
+// loaded up front (64 channels x 4 replica lanes, <= 8 replicas per lane), the 4 lanes combine
+// through LDS in a fixed order (deterministic) and lane 0 writes the table.  Used by the
+// vae_bn_finalize kernel and by the last workgroup of a producing GEMM (fused finalisation).
+constexpr int BNF_LANES = 4, BNF_PER = 8;      // replicas <= BNF_LANES * BNF_PER (checked on the host)
+
+__device__ __forceinline__ void bn_finalize_block(const vae_bn_args& a, int cg0, int cgs) {
+  __shared__ float red[4][BNF_LANES][64];
+  const vae_xform& x = a.xf;
+  const int C = x.channels;
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int reps = x.reps > 1 ? x.reps : 1;
+  const long rstr = x.reps > 1 ? x.rstride : 0;
+  const bool bwd = a.mode != 0;
+  const float* arr[4] = {x.sum, x.sumsq, bwd ? x.dgamma : nullptr, bwd ? x.dbeta : nullptr};
+  for (int cg = cg0; cg * 64 < C; cg += cgs) {
+    const int c = cg * 64 + cl;
+    const int cc = c < C ? c : 0;
+    float v[4][BNF_PER];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int u = 0; u < BNF_PER; ++u) {
+        const int r = rl + BNF_LANES * u;
+        v[k][u] = (arr[k] && r < reps) ? arr[k][r * rstr + cc] : 0.f;
+      }
+    const float g = x.gamma[cc], be = x.beta[cc], sh = x.shift ? x.shift[cc] : 0.f;
+    const bool run = !bwd && x.running_mean;
+    const float rmean = run ? x.running_mean[cc] : 0.f, rvar = run ? x.running_var[cc] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float t = 0.f;
+#pragma unroll
+      for (int u = 0; u < BNF_PER; ++u) t += v[k][u];
+      red[k][rl][cl] = t;
+    }
+    __syncthreads();
+    if (rl == 0 && c < C) {
+      float tot[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tot[k] = (red[k][0][cl] + red[k][1][cl]) + (red[k][2][cl] + red[k][3][cl]);
+      const float inv_m = 1.0f / x.count;
+      const float s1 = tot[0] * inv_m;
+      const float var = fmaxf(tot[1] * inv_m - s1 * s1, 0.0f);
+      const float mean = s1 + sh;
+      const float invstd = 1.0f / sqrtf(var + x.eps);
+      if (!bwd) {
+        const float sc = g * invstd;
+        a.table[c] = sc;
+        a.table[C + c] = be - mean * sc;
+        a.table[2 * C + c] = invstd;
+        a.table[3 * C + c] = -mean * invstd;
+        if (run) {
+          const float m = x.momentum;
+          const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
+          x.running_mean[c] = (1.f - m) * rmean + m * mean;
+          x.running_var[c] = (1.f - m) * rvar + m * unb;
+        }
+      } else {
+        const float dgam = tot[2], dbet = tot[3];
+        const float A = g * invstd;
+        const float mgx = dgam * inv_m, mg = dbet * inv_m;
+        const float B = -A * invstd * mgx;
+        const float Cc = -A * (mg - mean * invstd * mgx);
+        a.table[c] = A;
+        a.table[C + c] = B;
+        a.table[2 * C + c] = Cc;
+        if (x.dgamma_out) x.dgamma_out[c] += dgam;
+        if (x.dbeta_out) x.dbeta_out[c] += dbet;
+        if (a.db) {
+          const float sum_y = tot[0] + x.count * sh;
+          a.db[c] += A * dbet + B * sum_y + Cc * x.count;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Fused finalisation: called by every workgroup of a grid after its statistics atomics; the
+// last one to arrive (device-scope counter, zeroed by vae_step_begin and re-zeroed here) runs
+// bn_finalize_block for all channels.  Protocol (cdna_hip_programming.md §6 G16): the block's
+// atomics drained at the barrier, agent-scope release, counter RMW, agent-scope acquire in the
+// last block, then plain loads of the replicas.
+__device__ __forceinline__ void bn_finalize_last_block(const vae_bn_args& a, unsigned* counter) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned total = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned old = atomicAdd(counter, 1u);
+    last = old == total - 1;
+    if (last) __threadfence();
+  }
+  __syncthreads();
+  if (!last) return;
+  bn_finalize_block(a, 0, 1);
+  if (threadIdx.x == 0) *counter = 0u;
+}
 
 }  // namespace vae

@@ -336,80 +336,7 @@ int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
 }
 
 // ------------------------------------------------------------------ BatchNorm finalisation
-// One memory round trip: every replica of every statistic a channel needs is loaded up front
-// (64 channels x 4 replica lanes per workgroup, <= 8 replicas per lane), then the 4 lanes of a
-// channel combine through LDS in a fixed order (deterministic) and lane 0 writes the table.
-constexpr int BNF_LANES = 4, BNF_PER = 8;      // replicas <= BNF_LANES * BNF_PER (checked on the host)
-
-__global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) {
-  __shared__ float red[4][BNF_LANES][64];
-  const vae_xform& x = a.xf;
-  const int C = x.channels;
-  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  const int cc = c < C ? c : 0;
-  const int reps = x.reps > 1 ? x.reps : 1;
-  const long rstr = x.reps > 1 ? x.rstride : 0;
-  const bool bwd = a.mode != 0;
-  const float* arr[4] = {x.sum, x.sumsq, bwd ? x.dgamma : nullptr, bwd ? x.dbeta : nullptr};
-  float v[4][BNF_PER];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int u = 0; u < BNF_PER; ++u) {
-      const int r = rl + BNF_LANES * u;
-      v[k][u] = (arr[k] && r < reps) ? arr[k][r * rstr + cc] : 0.f;
-    }
-  // per-channel parameters, in flight with the replicas (used by lane 0)
-  const float g = x.gamma[cc], be = x.beta[cc], sh = x.shift ? x.shift[cc] : 0.f;
-  const bool run = !bwd && x.running_mean;
-  const float rmean = run ? x.running_mean[cc] : 0.f, rvar = run ? x.running_var[cc] : 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float t = 0.f;
-#pragma unroll
-    for (int u = 0; u < BNF_PER; ++u) t += v[k][u];
-    red[k][rl][cl] = t;
-  }
-  __syncthreads();
-  if (rl != 0 || c >= C) return;
-  float tot[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) tot[k] = (red[k][0][cl] + red[k][1][cl]) + (red[k][2][cl] + red[k][3][cl]);
-  const float inv_m = 1.0f / x.count;
-  const float s1 = tot[0] * inv_m;
-  const float var = fmaxf(tot[1] * inv_m - s1 * s1, 0.0f);
-  const float mean = s1 + sh;
-  const float invstd = 1.0f / sqrtf(var + x.eps);
-  if (!bwd) {
-    const float sc = g * invstd;
-    a.table[c] = sc;
-    a.table[C + c] = be - mean * sc;
-    a.table[2 * C + c] = invstd;
-    a.table[3 * C + c] = -mean * invstd;
-    if (run) {
-      const float m = x.momentum;
-      const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
-      x.running_mean[c] = (1.f - m) * rmean + m * mean;
-      x.running_var[c] = (1.f - m) * rvar + m * unb;
-    }
-  } else {
-    const float dgam = tot[2], dbet = tot[3];
-    const float A = g * invstd;
-    const float mgx = dgam * inv_m, mg = dbet * inv_m;
-    const float B = -A * invstd * mgx;
-    const float Cc = -A * (mg - mean * invstd * mgx);
-    a.table[c] = A;
-    a.table[C + c] = B;
-    a.table[2 * C + c] = Cc;
-    if (x.dgamma_out) x.dgamma_out[c] += dgam;
-    if (x.dbeta_out) x.dbeta_out[c] += dbet;
-    if (a.db) {
-      const float sum_y = tot[0] + x.count * sh;
-      a.db[c] += A * dbet + B * sum_y + Cc * x.count;
-    }
-  }
-}
+__global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) { bn_finalize_block(a, blockIdx.x, gridDim.x); }
 
 // Eval-mode BatchNorm: the forward table from the running statistics (torch eval semantics:
 // (y - running_mean) / sqrt(running_var + eps) * gamma + beta).
@@ -650,7 +577,9 @@ extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
   return check_launch("head_bwd_filter");
 }
 
-extern "C" int vae_bn_finalize(const vae_bn_args* a, void* stream) {
+extern "C" int vae_bn_finalize(const vae_bn_args* a, void* stream) { return vae::bn_finalize_launch(a, (hipStream_t)stream); }
+
+int vae::bn_finalize_launch(const vae_bn_args* a, hipStream_t stream) {
   if (!a || !a->table || a->xf.channels <= 0 || !a->xf.sum || !a->xf.sumsq || !a->xf.gamma || !a->xf.beta ||
       a->xf.count <= 0.f)
     return fail(VAE_E_BADARG, "bn_finalize: args");
@@ -674,9 +603,12 @@ extern "C" int vae_head_bwd(const vae_head_args* a, void* stream) {
   if ((!a->coef && !a->grad_recon) || !a->dx || !a->dw) return fail(VAE_E_BADARG, "head_bwd: coef/grad_recon/dx/dw");
   if (p.epi.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta || !p.epi.aux)) return fail(VAE_E_BADARG, "head_bwd: BN epilogue");
   rc = head_bwd_mfma_launch(a, true, true, (hipStream_t)stream);
-  if (rc != kHeadFallback) return rc;
-  if ((rc = vae_head_bwd_data(a, stream))) return rc;
-  return vae_head_bwd_filter(a, stream);
+  if (rc == kHeadFallback) {
+    if ((rc = vae_head_bwd_data(a, stream))) return rc;
+    rc = vae_head_bwd_filter(a, stream);
+  }
+  if (rc || !a->bn_finalize) return rc;
+  return bn_finalize_launch(a->bn_finalize, (hipStream_t)stream);     // the final BatchNorm's backward table
 }
 
 extern "C" int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int32_t latent, const float* mulv,

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -39,6 +39,10 @@ class Xform(ctypes.Structure):
                 ("table", c_void_p)]
 
 
+class BnArgs(ctypes.Structure):
+    _fields_ = [("mode", c_int32), ("xf", Xform), ("table", c_void_p), ("db", c_void_p)]
+
+
 class ConvArgs(ctypes.Structure):
     _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
                 ("k", c_int32), ("p", c_int32), ("q", c_int32), ("r", c_int32), ("stride", c_int32),
@@ -48,7 +52,8 @@ class ConvArgs(ctypes.Structure):
                 ("residual", c_void_p), ("residual_xf", Xform),
                 ("dy", c_void_p), ("dy_xf", Xform), ("dx", c_void_p), ("dx_epi", Xform),
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
-                ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
+                ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -59,7 +64,8 @@ class LinearArgs(ctypes.Structure):
                 ("dx_dbeta", c_void_p), ("sum_reps", c_int32), ("sum_rstride", c_int32),
                 ("dw", c_void_p), ("db", c_void_p),
                 ("mulv", c_void_p), ("eps", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p),
-                ("samples", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
+                ("samples", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p)]
 
 
 class HeadArgs(ctypes.Structure):
@@ -69,7 +75,8 @@ class HeadArgs(ctypes.Structure):
                 ("coef", c_void_p), ("dx", c_void_p), ("dx_epi", Xform), ("dx_dgamma", c_void_p),
                 ("dx_dbeta", c_void_p), ("sum_reps", c_int32), ("sum_rstride", c_int32),
                 ("dw", c_void_p), ("db", c_void_p), ("grad_recon", c_void_p),
-                ("workspace", c_void_p), ("workspace_bytes", c_int64)]
+                ("workspace", c_void_p), ("workspace_bytes", c_int64),
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p)]
 
 
 class ElboArgs(ctypes.Structure):
@@ -91,10 +98,6 @@ class ReconArgs(ctypes.Structure):
     _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
                 ("y", c_void_p), ("target", c_void_p), ("recon", c_void_p), ("sse", c_void_p), ("dy", c_void_p),
                 ("grad_scale", c_float), ("grad_recon", c_void_p)]
-
-
-class BnArgs(ctypes.Structure):
-    _fields_ = [("mode", c_int32), ("xf", Xform), ("table", c_void_p), ("db", c_void_p)]
 
 
 # name -> (argtypes)

@@ -38,6 +38,9 @@ def _written_grad_ptrs(arg) -> List[int]:
             v = getattr(xf, f)
             if v:
                 out.append(int(v))
+    fin = getattr(arg, "bn_finalize", None)  # a BatchNorm finalisation fused into this call
+    if fin:
+        out += _written_grad_ptrs(fin.contents)
     return out
 
 

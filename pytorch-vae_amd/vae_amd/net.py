@@ -111,7 +111,7 @@ class StepPlan:
     def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
                  capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
-                 concurrent: bool = False):
+                 concurrent: bool = False, fuse_bn: bool = False):
         self.net = net
         self.B = batch
         # training=False: eval-mode BatchNorm (running statistics, nothing updated; the
@@ -167,7 +167,7 @@ class StepPlan:
         # BatchNorm has forward sums (Σ, Σ²) and backward sums (Σg·x̂, Σg), each kept in
         # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
         nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
-        nz = net.layout.total + nbn + _pad4(BS) + _pad4(B * 2 * D)
+        nz = net.layout.total + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns))
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
@@ -179,6 +179,7 @@ class StepPlan:
             self.bnbwd[b.prefix] = self.zero[o:o + n].view(2, bn_reps(b.channels), b.channels); o += n
         self.sse = self.zero[o:o + BS]; o += _pad4(BS)
         self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
+        self.counters = self.zero[o:o + 2 * len(net.layout.bns)].view(torch.int32); o += _pad4(2 * len(net.layout.bns))
         # per-BatchNorm coefficient tables, rewritten every step by vae_bn_finalize:
         # forward [4][C] (BN_ACT) then backward [3][C] (BN_DY)
         self.bntab: Dict[str, torch.Tensor] = {
@@ -191,6 +192,13 @@ class StepPlan:
         # side stream for the weight gradients (run_calls); None: one stream
         self.side = torch.cuda.Stream(device=dev) if (concurrent and training) else None
         self._build()
+        if fuse_bn and training:
+            # Off by default: measured 0.81 -> 1.26 ms/step.  The last-workgroup protocol needs an
+            # agent-scope release in every workgroup of the producing GEMM, and that L2 writeback
+            # of the freshly written output costs more than the separate finalisation launch.
+            # one uint32 arrival counter per fused finalisation, inside the zeroed region
+            self._fuse_finalize(self.fwd_calls)
+            self._fuse_finalize(self.bwd_calls)
 
     # ------------------------------------------------------------------ helpers
     def g(self, name: str) -> int:
@@ -251,6 +259,35 @@ class StepPlan:
             a.xf.dbeta_out = self.g(prefix + ".bias")
             a.db = self.g(self._bn_prod_bias(prefix))
         self._add(lst, "vae_bn_finalize", a)
+
+    def _fuse_finalize(self, calls):
+        """Fold every vae_bn_finalize call (modes 0/1) into the call that produced its statistics
+        (the GEMM whose epilogue wrote them): that call's last workgroup then builds the table
+        (vaehip.h bn_finalize), saving a dependent launch per BatchNorm and direction."""
+        out = []
+        nctr = 0
+        for fn, ref in calls:
+            if fn == "vae_bn_finalize" and ref is not None and ref._obj.mode in (0, 1):
+                bn = ref._obj
+                key = bn.xf.sum if bn.mode == 0 else bn.xf.dgamma
+                prod = None
+                for pfn, pref in reversed(out):
+                    a = pref._obj if pref is not None else None
+                    if a is None or not hasattr(a, "bn_counter"):
+                        continue
+                    if bn.mode == 0 and getattr(a, "y_sum", None) == key:
+                        prod = a
+                    elif bn.mode == 1 and getattr(a, "dx_dgamma", None) == key:
+                        prod = a
+                    if prod is not None:
+                        break
+                if prod is not None and not prod.bn_finalize:
+                    prod.bn_finalize = ctypes.pointer(bn)
+                    prod.bn_counter = self.counters.data_ptr() + 4 * nctr
+                    nctr += 1
+                    continue
+            out.append((fn, ref))
+        calls[:] = out
 
     def _add(self, lst, fn, arg):
         if isinstance(arg, (L.ConvArgs, L.LinearArgs, L.HeadArgs)):

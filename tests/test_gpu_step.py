@@ -142,3 +142,32 @@ def test_step_bf16_close(case):
     assert abs(out[0] - meta["loss"]["loss"]) <= 2e-3 * abs(meta["loss"]["loss"])
     assert abs(out[1] - meta["loss"]["Reconstruction_Loss"]) <= 2e-3 * abs(meta["loss"]["Reconstruction_Loss"])
     assert abs(out[2] - meta["loss"]["KLD"]) <= 2e-2 * abs(meta["loss"]["KLD"])
+
+
+def test_step_with_fused_bn_finalize_matches_separate():
+    """StepPlan(fuse_bn=True): every BatchNorm finalisation folded into the last workgroup of the
+    GEMM that produced its statistics (vaehip.h bn_finalize/bn_counter) gives the same step."""
+    from vae_amd import _lib as L
+    from vae_amd.net import StepPlan, VAENet
+    meta, _ = load_case("vanilla_b16")
+    sd, x, eps = case_inputs(meta)
+    outs = []
+    for fuse in (False, True):
+        net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda")
+        net.load_reference_state_dict(sd)
+        plan = StepPlan(net, meta["batch"], loss="vanilla", kld_weight=meta["M_N"], fuse_bn=fuse)
+        if fuse:
+            assert not any(fn == "vae_bn_finalize" for fn, _ in plan.fwd_calls + plan.bwd_calls)
+        plan.x.copy_(x)
+        plan.eps.copy_(eps)
+        st = L.stream_ptr()
+        for _ in range(2):                   # second step: counters were left at zero
+            plan.begin(st)
+            plan.forward(st)
+            plan.backward(st)
+        torch.cuda.synchronize()
+        outs.append((plan.out.cpu().clone(), plan.grads.cpu().clone(), net.running.cpu().clone()))
+    (o0, g0, r0), (o1, g1, r1) = outs
+    assert torch.allclose(o0[:3], o1[:3], rtol=1e-5)
+    assert float((g0 - g1).norm() / g0.norm()) < 1e-4
+    assert torch.allclose(r0, r1, rtol=1e-5, atol=1e-7)
