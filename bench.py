@@ -105,7 +105,7 @@ def kernel_costs(plan, dsz):
     from vae_amd import _lib as L
     out = []
     for fn, ref in plan.fwd_calls + plan.bwd_calls:
-        if fn == "vae_reparam_fwd" or ref is None:
+        if isinstance(ref, tuple) or ref is None:
             out.append((fn, None, 0, 0))
             continue
         a = ref._obj
@@ -128,7 +128,7 @@ def time_kernels(plan, reps=20):
     bracketed by HIP events on the stream it runs on, queued behind a spin kernel so host launch
     latency is not measured; average per launch.  (The calls accumulate into the plan's gradient
     buffers; this runs after the timed region and its loss terms were read.)"""
-    from vae_amd import _lib as L
+    from vae_amd.net import call_one
     st = torch.cuda.current_stream()
     sp = st.cuda_stream
     res = []
@@ -138,10 +138,7 @@ def time_kernels(plan, reps=20):
         torch.cuda._sleep(400000)               # spin: everything below is queued behind it
         e0.record(st)
         for _ in range(reps):
-            if fn == "vae_reparam_fwd":
-                L.call(fn, *plan._reparam, sp)
-            else:
-                L.call(fn, ref, sp)
+            call_one(fn, ref, sp)
         e1.record(st)
         torch.cuda.synchronize()
         res.append((fn, ref, e0.elapsed_time(e1) * 1e3 / reps))   # µs per launch

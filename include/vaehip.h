@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 6
+#define VAE_ABI_VERSION 7
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -154,11 +154,10 @@ typedef struct vae_conv_args {
   void* workspace;         /* fp32 scratch for split-K partial slabs (may be NULL: no split
                               of fwd / bwd_data); reused by every call on the stream */
   int64_t workspace_bytes;
-  /* Optional fused BatchNorm finalisation of the statistics this call produces (forward: the
+  /* Optional BatchNorm finalisation of the statistics this call produces (forward: the
    * y_sum/y_sumsq of the next BatchNorm; bwd_data: its dx_dgamma/dx_dbeta): the call then also
-   * does what vae_bn_finalize(bn_finalize) would, in its last workgroup when the kernel path
-   * allows (else as a separate launch).  bn_counter: a uint32 that is 0 before the call (the
-   * step's zeroed region) and is left 0. */
+   * does what vae_bn_finalize(bn_finalize) would (launched right after its own kernels).
+   * bn_counter: reserved (a zeroed uint32 slot; may be NULL). */
   const struct vae_bn_args* bn_finalize;
   uint32_t* bn_counter;
 } vae_conv_args;
@@ -186,11 +185,10 @@ typedef struct vae_linear_args {
   int32_t samples;         /* rows per mu row (IWAE S; 1 otherwise) */
   void* workspace;         /* as vae_conv_args.workspace */
   int64_t workspace_bytes;
-  /* Optional fused BatchNorm finalisation of the statistics this call produces (forward: the
+  /* Optional BatchNorm finalisation of the statistics this call produces (forward: the
    * y_sum/y_sumsq of the next BatchNorm; bwd_data: its dx_dgamma/dx_dbeta): the call then also
-   * does what vae_bn_finalize(bn_finalize) would, in its last workgroup when the kernel path
-   * allows (else as a separate launch).  bn_counter: a uint32 that is 0 before the call (the
-   * step's zeroed region) and is left 0. */
+   * does what vae_bn_finalize(bn_finalize) would (launched right after its own kernels).
+   * bn_counter: reserved (a zeroed uint32 slot; may be NULL). */
   const struct vae_bn_args* bn_finalize;
   uint32_t* bn_counter;
 } vae_linear_args;
@@ -287,6 +285,8 @@ typedef struct vae_recon_args {
   void* dy;                /* NHWC (dtype) or NULL */
   float grad_scale;
   const float* grad_recon;
+  int32_t ld;              /* channel stride of y and dy (>= c; 0: c) — an 8-channel padded layout keeps
+                              the output convolution on the packed path; dy's pad channels are written 0 */
 } vae_recon_args;
 
 int vae_abi_version(void);
@@ -323,6 +323,18 @@ int vae_vq_bwd(const vae_vq_args* a, void* stream);
 /* --- Tanh output + reconstruction SSE (vq_vae.py:156-160, :203), see vae_recon_args --- */
 int vae_recon_fwd(const vae_recon_args* a, void* stream);
 int vae_recon_bwd(const vae_recon_args* a, void* stream);
+/* --- channel padding for 3-channel layers (the RGB image and the RGB output conv) -----------
+ * The packed GEMM paths need channel counts that are multiples of 8, so the 3-channel tensors
+ * at both ends of the network are carried padded to 8 channels (zeros):
+ *   vae_nchw_to_nhwc_pad: x fp32 NCHW [n][c][h][w] (c <= cp) -> y NHWC [n][h][w][cp] in dtype;
+ *   vae_pad_channels:     dst[r][j] = j < c ? src[r][j] : 0, rows x cp (dtype: both sides;
+ *                         weights in the bf16 copy, biases fp32);
+ *   vae_unpad_accumulate: dst[r][j] += src[r][j] for j < c (fp32; padded weight gradient ->
+ *                         the parameter's gradient). */
+int vae_nchw_to_nhwc_pad(int32_t dtype, int32_t n, int32_t c, int32_t h, int32_t w, int32_t cp, const float* x,
+                         void* y, void* stream);
+int vae_pad_channels(int32_t dtype, int64_t rows, int32_t c, int32_t cp, const void* src, void* dst, void* stream);
+int vae_unpad_accumulate(int64_t rows, int32_t cp, int32_t c, const float* src, float* dst, void* stream);
 /* --- ELBO terms + backward seeds (vanilla_vae.py:124-146 and variants) -------------- */
 int vae_elbo_fwd(const vae_elbo_args* a, void* stream);
 /* --- Adam (experiment.py:308-311; torch.optim.Adam semantics), flat fp32 buffers.

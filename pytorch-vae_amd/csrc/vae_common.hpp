@@ -222,25 +222,4 @@ __device__ __forceinline__ void bn_finalize_block(const vae_bn_args& a, int cg0,
   }
 }
 
-// Fused finalisation: called by every workgroup of a grid after its statistics atomics; the
-// last one to arrive (device-scope counter, zeroed by vae_step_begin and re-zeroed here) runs
-// bn_finalize_block for all channels.  Protocol (cdna_hip_programming.md §6 G16): the block's
-// atomics drained at the barrier, agent-scope release, counter RMW, agent-scope acquire in the
-// last block, then plain loads of the replicas.
-__device__ __forceinline__ void bn_finalize_last_block(const vae_bn_args& a, unsigned* counter) {
-  __shared__ int last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned total = gridDim.x * gridDim.y * gridDim.z;
-    const unsigned old = atomicAdd(counter, 1u);
-    last = old == total - 1;
-    if (last) __threadfence();
-  }
-  __syncthreads();
-  if (!last) return;
-  bn_finalize_block(a, 0, 1);
-  if (threadIdx.x == 0) *counter = 0u;
-}
-
 }  // namespace vae

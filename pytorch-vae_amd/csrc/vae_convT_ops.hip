@@ -21,9 +21,9 @@ extern "C" int vae_convT2d_fwd(const vae_conv_args* a, void* stream) {
   p.out = a->y; p.out_ld = a->k; p.out_phase = 1; p.bias = a->bias; p.sum = a->y_sum; p.sumsq = a->y_sumsq;
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.residual = a->residual; p.res_xf = sanitize(a->residual_xf);
-  if (int rc = attach_finalize(p, a->bn_finalize, a->bn_counter, "convT2d_fwd")) return rc;
-  return launch<A_CONVT, B_KN, E_STORE, false, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
-                                        (hipStream_t)stream);
+  if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "convT2d_fwd")) return rc;
+  return then_finalize(launch<A_CONVT, B_KN, E_STORE, false, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
+                                        (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
 }
 
 // dx[n,h,w,c] = Σ_{r,s,k} dy'[n, h*S-P+r, w*S-P+s, k] · W[c][r][s][k]   (strided conv of dy)
@@ -40,9 +40,9 @@ extern "C" int vae_convT2d_bwd_data(const vae_conv_args* a, void* stream) {
   p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "convT2d_bwd_data: dgamma/dbeta");
-  if (int rc = attach_finalize(p, a->bn_finalize, a->bn_counter, "convT2d_bwd_data")) return rc;
-  return launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
-                                       (hipStream_t)stream);
+  if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "convT2d_bwd_data")) return rc;
+  return then_finalize(launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
+                                       (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
 }
 
 // dW[c][r][s][k] += Σ_{n,h,w} xf(x)[n,h,w,c] · dy'[n, h*S-P+r, w*S-P+s, k];  db[k] += Σ dy'

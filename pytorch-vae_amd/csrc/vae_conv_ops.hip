@@ -17,9 +17,9 @@ extern "C" int vae_conv2d_fwd(const vae_conv_args* a, void* stream) {
   p.out = a->y; p.out_ld = a->k; p.bias = a->bias; p.sum = a->y_sum; p.sumsq = a->y_sumsq;
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.residual = a->residual; p.res_xf = sanitize(a->residual_xf);
-  if (int rc = attach_finalize(p, a->bn_finalize, a->bn_counter, "conv2d_fwd")) return rc;
-  return launch<A_CONV, B_NK, E_STORE, false, false, true>(a->dtype, a->x_nchw_f32 != 0, false, p, a->split_k, a->workspace,
-                                             a->workspace_bytes, (hipStream_t)stream);
+  if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "conv2d_fwd")) return rc;
+  return then_finalize(launch<A_CONV, B_NK, E_STORE, false, false, true>(a->dtype, a->x_nchw_f32 != 0, false, p, a->split_k, a->workspace,
+                                             a->workspace_bytes, (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
 }
 
 // dx[n,h,w,c] = Σ_{r,s,k: h = p*S-P+r} dy'[n,p,q,k] · W[k][r][s][c]  (transposed conv of dy);
@@ -53,8 +53,8 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
     p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
     p.residual = a->residual;
     if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
-    if (int rc2 = attach_finalize(p, a->bn_finalize, a->bn_counter, "conv2d_bwd_data")) return rc2;
-    return launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, ws, wsoff, (hipStream_t)stream);
+    if (int rc2 = check_finalize(a->bn_finalize, a->bn_counter, "conv2d_bwd_data")) return rc2;
+    return then_finalize(launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, ws, wsoff, (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
   }
   GemmParams p = base_params();
   if (!make_taps(p, S, a->r, a->pad)) return fail(VAE_E_UNSUPPORTED, "conv2d_bwd_data: stride/kernel");
@@ -69,9 +69,9 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.residual = a->residual;                                    // + gradient through a skip connection
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
-  if (int rc = attach_finalize(p, a->bn_finalize, a->bn_counter, "conv2d_bwd_data")) return rc;
-  return launch<A_CONVT, B_KN, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
-                                        (hipStream_t)stream);
+  if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "conv2d_bwd_data")) return rc;
+  return then_finalize(launch<A_CONVT, B_KN, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,
+                                        (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
 }
 
 // dW[k][r][s][c] += Σ_{n,p,q} dy'[n,p,q,k] · xf(x)[n, p*S-P+r, q*S-P+s, c];  db[k] += Σ dy'

@@ -94,9 +94,6 @@ struct GemmParams {
   FastDiv fd_ech;            // epilogue transform channel count
   uint32_t out_aux_bytes;    // extent of the out-shaped aux tensor (residual / stored pre-activation)
   unsigned long long* probe; // VAE_PROBE builds: per-block phase timestamps (diagnostics only)
-  // fused BatchNorm finalisation of the sums this GEMM's epilogue produces (the last workgroup
-  // runs it, bn_finalize_last_block); fin_counter NULL: none
-  vae_bn_args fin; unsigned* fin_counter;
 };
 
 // Phase timestamps of one block (VAE_PROBE builds): record = {block id, wall0, wall3, clk0..clk3,
@@ -1160,7 +1157,6 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
         for (int c = tid; c < BN; c += NTHREADS)
           if (n0 + c < p.N) epi_flush_sums<EM>(p, blockIdx.x + blockIdx.z * gridDim.x, n0 + c, red1[c], red2[c]);
       }
-      if (p.fin_counter) bn_finalize_last_block(p.fin, p.fin_counter);
     }
   }
 }
@@ -1270,7 +1266,6 @@ __global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
         if (col < p.N) epi_flush_sums<EM>(p, blockIdx.x, col, a, b);
       }
     }
-    if (p.fin_counter) bn_finalize_last_block(p.fin, p.fin_counter);
   }
 }
 

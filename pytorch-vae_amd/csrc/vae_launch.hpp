@@ -63,18 +63,23 @@ inline bool make_taps(GemmParams& p, int S, int R, int P) {
   return true;
 }
 
-// Attach an optional fused BatchNorm finalisation (vae_conv_args.bn_finalize) to a GEMM whose
-// epilogue produces the statistics; validated like vae_bn_finalize (mode 0 or 1).
-inline int attach_finalize(GemmParams& p, const vae_bn_args* f, uint32_t* counter, const char* what) {
+// The optional BatchNorm finalisation a producing call carries (vae_conv_args.bn_finalize):
+// validated up front, launched right after the GEMM (see vaehip.h; an in-kernel last-workgroup
+// variant measured slower: every workgroup then needs an agent-scope release, and the extra
+// epilogue code and LDS lowered the GEMMs' occupancy).
+inline int check_finalize(const vae_bn_args* f, const uint32_t* counter, const char* what) {
   if (!f) return VAE_OK;
-  if (!counter) return fail(VAE_E_BADARG, "%s: bn_finalize needs bn_counter", what);
+  (void)counter;
   if (f->mode != 0 && f->mode != 1) return fail(VAE_E_BADARG, "%s: fused finalisation mode %d", what, f->mode);
   if (!f->table || f->xf.channels <= 0 || !f->xf.sum || !f->xf.sumsq || !f->xf.gamma || !f->xf.beta || f->xf.count <= 0.f ||
       (f->mode == 1 && (!f->xf.dgamma || !f->xf.dbeta)) || f->xf.reps > BNF_LANES * BNF_PER)
     return fail(VAE_E_BADARG, "%s: bn_finalize args", what);
-  p.fin = *f;
-  p.fin_counter = counter;
   return VAE_OK;
+}
+
+inline int then_finalize(int rc, const vae_bn_args* f, hipStream_t st) {
+  if (rc || !f) return rc;
+  return bn_finalize_launch(f, st);
 }
 
 inline GemmParams base_params() {
@@ -307,15 +312,10 @@ inline int launch_fgemm(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
 #endif
   const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.nphase * p.ksplit);
   const size_t lds = (size_t)(tab_floats(p.a_xf, false) + (EM == E_BNBWD ? tab_floats(p.epi_xf, true) : 0)) * 4;
-  const bool sep_fin = p.fin_counter && !p.slab;          // fgemm's own epilogue does not fuse it
-  unsigned* const ctr = p.fin_counter;
-  if (sep_fin) p.fin_counter = nullptr;
   hipLaunchKernelGGL((fgemm_kernel<T, TA, BM, BN, AM, EM, DYA>), grid, dim3(256), lds, st, p);
   int rc = check_launch("fgemm");
   if (rc) return rc;
   if (p.slab) return launch_finalize<T, EM>(p, st);
-  (void)ctr;
-  if (sep_fin) return bn_finalize_launch(&p.fin, st);
   return VAE_OK;
 }
 

@@ -37,9 +37,9 @@ extern "C" int vae_linear_bwd_data(const vae_linear_args* a, void* stream) {
   p.epi_xf = sanitize(a->dx_epi); p.dgamma = a->dx_dgamma; p.dbeta = a->dx_dbeta;
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "linear_bwd_data: dgamma/dbeta");
-  if (int rc = attach_finalize(p, a->bn_finalize, a->bn_counter, "linear_bwd_data")) return rc;
-  return launch<A_DENSE, B_KN, E_BNBWD, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace, a->workspace_bytes,
-                                              (hipStream_t)stream);
+  if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "linear_bwd_data")) return rc;
+  return then_finalize(launch<A_DENSE, B_KN, E_BNBWD, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace, a->workspace_bytes,
+                                              (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
 }
 
 // dW[n][k] += Σ_m dy[m][n] · xf(x)[m][k];  db[n] += Σ_m dy[m][n]  (ones column)

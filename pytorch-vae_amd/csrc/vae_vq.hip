@@ -148,7 +148,10 @@ __global__ void __launch_bounds__(256) recon_kernel(vae_recon_args a, int bwd) {
   const long pix = (long)blockIdx.x * 256 + threadIdx.x;     // over n*h*w
   const long img = pix / hw, sp = pix - img * hw;
   const T* y = static_cast<const T*>(a.y);
+  const int ld = a.ld > 0 ? a.ld : C;
   float sse = 0.f;
+  if (a.dy)
+    for (int c = C; c < ld; ++c) static_cast<T*>(a.dy)[pix * ld + c] = cvt<T>(0.f);
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const long o = (img * C + c) * hw + sp;                  // NCHW
@@ -156,14 +159,14 @@ __global__ void __launch_bounds__(256) recon_kernel(vae_recon_args a, int bwd) {
     if (bwd) {
       r = a.recon[o];
     } else {
-      r = tanhf(ld_f(y + pix * C + c));
+      r = tanhf(ld_f(y + pix * ld + c));
       a.recon[o] = r;
     }
     const float d = r - a.target[o];
     sse = fmaf(d, d, sse);
     if (a.dy) {
       const float g = a.grad_recon ? a.grad_recon[o] : a.grad_scale * 2.f * d;
-      static_cast<T*>(a.dy)[pix * C + c] = cvt<T>(g * (1.f - r * r));
+      static_cast<T*>(a.dy)[pix * ld + c] = cvt<T>(g * (1.f - r * r));
     }
   }
   if (bwd || !a.sse) return;
@@ -198,6 +201,7 @@ int recon_launch(const vae_recon_args* a, int bwd, hipStream_t st) {
   if (!a || !a->target || !a->recon) return fail(VAE_E_BADARG, "recon: null tensor");
   if (a->n <= 0 || a->h <= 0 || a->w <= 0) return fail(VAE_E_BADSHAPE, "recon: shape");
   if (a->c != 3) return fail(VAE_E_UNSUPPORTED, "recon: %d channels (the output layer is RGB)", a->c);
+  if (a->ld != 0 && a->ld < a->c) return fail(VAE_E_BADARG, "recon: ld %d < c", a->ld);
   if (((long)a->h * a->w) % 256) return fail(VAE_E_UNSUPPORTED, "recon: h*w must be a multiple of 256");
   if (!bwd && !a->y) return fail(VAE_E_BADARG, "recon_fwd: y");
   if (bwd && (!a->grad_recon || !a->dy)) return fail(VAE_E_BADARG, "recon_bwd: grad_recon / dy");
@@ -208,10 +212,63 @@ int recon_launch(const vae_recon_args* a, int bwd, hipStream_t st) {
   return check_launch("recon");
 }
 
+template <class T>
+__global__ void nchw_to_nhwc_pad_kernel(int n, int c, int h, int w, int cp, const float* x, T* y) {
+  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long hw = (long)h * w;
+  if (pix >= (long)n * hw) return;
+  const long img = pix / hw, sp = pix - img * hw;
+  for (int j = 0; j < cp; ++j) y[pix * cp + j] = cvt<T>(j < c ? x[(img * c + j) * hw + sp] : 0.f);
+}
+
+template <class T>
+__global__ void pad_channels_kernel(long rows, int c, int cp, const T* src, T* dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cp) return;
+  const long r = i / cp;
+  const int j = (int)(i - r * cp);
+  dst[i] = j < c ? src[r * c + j] : cvt<T>(0.f);
+}
+
+__global__ void unpad_accumulate_kernel(long rows, int cp, int c, const float* src, float* dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * c) return;
+  const long r = i / c;
+  const int j = (int)(i - r * c);
+  dst[i] += src[r * cp + j];
+}
+
 }  // namespace
 }  // namespace vae
 
 using namespace vae;
+
+extern "C" int vae_nchw_to_nhwc_pad(int32_t dtype, int32_t n, int32_t c, int32_t h, int32_t w, int32_t cp, const float* x,
+                                    void* y, void* stream) {
+  if (!x || !y || n <= 0 || c <= 0 || h <= 0 || w <= 0 || cp < c) return fail(VAE_E_BADARG, "nchw_to_nhwc_pad: args");
+  const long pix = (long)n * h * w;
+  const dim3 grid((unsigned)((pix + 255) / 256));
+  if (dtype == VAE_F32) hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, n, c, h, w, cp, x, (float*)y);
+  else if (dtype == VAE_BF16) hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, n, c, h, w, cp, x, (__bf16*)y);
+  else return fail(VAE_E_BADDTYPE, "nchw_to_nhwc_pad: dtype");
+  return check_launch("nchw_to_nhwc_pad");
+}
+
+extern "C" int vae_pad_channels(int32_t dtype, int64_t rows, int32_t c, int32_t cp, const void* src, void* dst, void* stream) {
+  if (!src || !dst || rows <= 0 || c <= 0 || cp < c) return fail(VAE_E_BADARG, "pad_channels: args");
+  const dim3 grid((unsigned)((rows * cp + 255) / 256));
+  if (dtype == VAE_F32) hipLaunchKernelGGL(pad_channels_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, c, cp, (const float*)src, (float*)dst);
+  else if (dtype == VAE_BF16) hipLaunchKernelGGL(pad_channels_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, c, cp, (const __bf16*)src, (__bf16*)dst);
+  else return fail(VAE_E_BADDTYPE, "pad_channels: dtype");
+  return check_launch("pad_channels");
+}
+
+extern "C" int vae_unpad_accumulate(int64_t rows, int32_t cp, int32_t c, const float* src, float* dst, void* stream) {
+  if (!src || !dst || rows <= 0 || c <= 0 || cp < c) return fail(VAE_E_BADARG, "unpad_accumulate: args");
+  const dim3 grid((unsigned)((rows * c + 255) / 256));
+  hipLaunchKernelGGL(unpad_accumulate_kernel, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, cp, c, src, dst);
+  return check_launch("unpad_accumulate");
+}
 
 extern "C" int vae_vq_fwd(const vae_vq_args* a, void* stream) {
   int rc = vq_check(a, "vq_fwd");

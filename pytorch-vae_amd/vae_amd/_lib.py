@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -97,7 +97,7 @@ class VqArgs(ctypes.Structure):
 class ReconArgs(ctypes.Structure):
     _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
                 ("y", c_void_p), ("target", c_void_p), ("recon", c_void_p), ("sse", c_void_p), ("dy", c_void_p),
-                ("grad_scale", c_float), ("grad_recon", c_void_p)]
+                ("grad_scale", c_float), ("grad_recon", c_void_p), ("ld", c_int32)]
 
 
 # name -> (argtypes)
@@ -128,6 +128,9 @@ _SIGS = {
                       c_float, c_float, c_void_p, c_void_p],
     "vae_cast_bf16": [c_int64, c_void_p, c_void_p, c_void_p],
     "vae_step_begin": [c_void_p, c_int64, c_void_p, c_void_p],
+    "vae_nchw_to_nhwc_pad": [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
+    "vae_pad_channels": [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
+    "vae_unpad_accumulate": [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
 }
 EXPORTED = tuple(_SIGS)
 

@@ -54,11 +54,14 @@ def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4
     params = sorted(layout.params, key=lambda p: p.offset)
     starts = [p.offset for p in params]
     last = [-1] * len(params)
-    for i, (_, ref) in enumerate(calls):
+    for i, (fn, ref) in enumerate(calls):
         if ref is None:
             continue
-        arg = ref._obj if hasattr(ref, "_obj") else ref
-        for ptr in _written_grad_ptrs(arg):
+        if isinstance(ref, tuple):              # scalar-argument entry points
+            ptrs = [ref[4]] if fn == "vae_unpad_accumulate" else []
+        else:
+            ptrs = _written_grad_ptrs(ref._obj if hasattr(ref, "_obj") else ref)
+        for ptr in ptrs:
             off = (ptr - base) // 4
             if not 0 <= off < layout.total:
                 continue

@@ -16,6 +16,7 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -135,6 +136,12 @@ class StepPlan:
         # -------- buffers
         f32 = dict(dtype=torch.float32, device=dev)
         self.x = torch.zeros(B, 3, img, img, **f32)                     # NCHW input (reference layout)
+        # bf16: the image and the first conv's weights carried as 8 zero-padded channels (packed
+        # GEMM operands; vae_nchw_to_nhwc_pad / vae_pad_channels at the start of every step)
+        self.pad_rgb = T == torch.bfloat16 and not os.environ.get("VAE_NO_PAD_RGB")
+        if self.pad_rgb:
+            self.x8 = torch.zeros(B, img, img, 8, dtype=T, device=dev)
+            self.w8 = torch.zeros(h[0] * 9 * 8, dtype=T, device=dev)
         self.eps = torch.zeros(BS, D, **f32)
         self.enc = []
         sp = img
@@ -167,7 +174,8 @@ class StepPlan:
         # BatchNorm has forward sums (Σ, Σ²) and backward sums (Σg·x̂, Σg), each kept in
         # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
         nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
-        nz = net.layout.total + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns))
+        nz = (net.layout.total + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns)) +
+              _pad4(h[0] * 9 * 8))
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
@@ -180,6 +188,7 @@ class StepPlan:
         self.sse = self.zero[o:o + BS]; o += _pad4(BS)
         self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
         self.counters = self.zero[o:o + 2 * len(net.layout.bns)].view(torch.int32); o += _pad4(2 * len(net.layout.bns))
+        self.dw8 = self.zero[o:o + h[0] * 9 * 8]; o += _pad4(h[0] * 9 * 8)       # padded first-conv dW
         # per-BatchNorm coefficient tables, rewritten every step by vae_bn_finalize:
         # forward [4][C] (BN_ACT) then backward [3][C] (BN_DY)
         self.bntab: Dict[str, torch.Tensor] = {
@@ -193,10 +202,10 @@ class StepPlan:
         self.side = torch.cuda.Stream(device=dev) if (concurrent and training) else None
         self._build()
         if fuse_bn and training:
-            # Off by default: measured 0.81 -> 1.26 ms/step.  The last-workgroup protocol needs an
-            # agent-scope release in every workgroup of the producing GEMM, and that L2 writeback
-            # of the freshly written output costs more than the separate finalisation launch.
-            # one uint32 arrival counter per fused finalisation, inside the zeroed region
+            # each BatchNorm finalisation carried by the call that produces its statistics
+            # (vaehip.h bn_finalize).  The library runs it as its own launch right after the
+            # producer: an in-kernel last-workgroup version measured 0.81 -> 1.26 ms/step (an
+            # agent-scope release in every workgroup, and lower GEMM occupancy).
             self._fuse_finalize(self.fwd_calls)
             self._fuse_finalize(self.bwd_calls)
 
@@ -316,18 +325,23 @@ class StepPlan:
 
         F = self.fwd_calls
         fmode = 0 if self.training else 2            # bn_finalize: batch statistics / running statistics
+        if self.pad_rgb:
+            F.append(("vae_nchw_to_nhwc_pad", (T, B, 3, img, img, 8, self.x.data_ptr(), self.x8.data_ptr())))
+            F.append(("vae_pad_channels", (T, h[0] * 9, 3, 8, net.w("encoder.0.0.weight"), self.w8.data_ptr())))
         # ---------------------------------------------------------------- encoder
         sp = img
         for i in range(nenc):
             a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=(3 if i == 0 else h[i - 1]), k=h[i], p=sp // 2, q=sp // 2,
                            r=3, stride=2, pad=1)
-            if i == 0:
+            if i == 0 and self.pad_rgb:
+                a.c, a.x = 8, self.x8.data_ptr()
+            elif i == 0:
                 a.x_nchw_f32 = 1
                 a.x = self.x.data_ptr()
             else:
                 a.x = self.enc[i - 1].data_ptr()
                 a.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]), running=True)
-            a.wt = net.w(f"encoder.{i}.0.weight")
+            a.wt = self.w8.data_ptr() if (i == 0 and self.pad_rgb) else net.w(f"encoder.{i}.0.weight")
             a.bias = net.p(f"encoder.{i}.0.bias")
             a.y = self.enc[i].data_ptr()
             if self.training:
@@ -346,7 +360,7 @@ class StepPlan:
         self._add(F, "vae_linear_fwd", a)
         self.n_encode = len(F)                 # calls of encode(): encoder + fc_mu|fc_var
         self._reparam = (T, BS, self.S, D, self.mulv.data_ptr(), self.eps.data_ptr(), self.z.data_ptr())
-        F.append(("vae_reparam_fwd", None))
+        F.append(("vae_reparam_fwd", self._reparam))
         self.n_decode0 = len(F)                # decode(): decoder_input .. head
         # ---------------------------------------------------------------- decoder_input
         a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
@@ -491,14 +505,19 @@ class StepPlan:
             f = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
             f.dy = self.g_enc[i].data_ptr()
             f.dy_xf = dy_xf
-            if i == 0:
+            if i == 0 and self.pad_rgb:
+                f.c, f.x, f.dw = 8, self.x8.data_ptr(), self.dw8.data_ptr()
+            elif i == 0:
                 f.x_nchw_f32 = 1
                 f.x = self.x.data_ptr()
             else:
                 f.x = self.enc[i - 1].data_ptr()
                 f.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]))
-            f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form in vae_bn_finalize
+            if not (i == 0 and self.pad_rgb):
+                f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form in vae_bn_finalize
             self._add(Bw, "vae_conv2d_bwd_filter", f)
+            if i == 0 and self.pad_rgb:
+                Bw.append(("vae_unpad_accumulate", (h[0] * 9, 8, 3, self.dw8.data_ptr(), self.g("encoder.0.0.weight"))))
             if i > 0:
                 a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
                 a.dy = self.g_enc[i].data_ptr()
@@ -541,7 +560,8 @@ class StepPlan:
 
 # Weight-gradient calls: nothing later in the backward reads their output (only the optimizer),
 # so they run on a side stream, concurrent with the data-gradient chain that is the critical path.
-SIDE_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_linear_bwd_filter"))
+SIDE_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_linear_bwd_filter",
+                      "vae_unpad_accumulate"))     # (follows its padded weight gradient)
 
 
 def run_calls(plan, calls, stream):
@@ -556,16 +576,22 @@ def run_calls(plan, calls, stream):
         side = None                          # an explicit foreign stream: keep everything on it
     forked = False
     for fn, arg in calls:
-        if fn == "vae_reparam_fwd":
-            L.call(fn, *plan._reparam, stream)
-        elif side is not None and fn in SIDE_FNS:
+        if side is not None and fn in SIDE_FNS:
             side.wait_stream(main)
-            L.call(fn, arg, side.cuda_stream)
+            call_one(fn, arg, side.cuda_stream)
             forked = True
         else:
-            L.call(fn, arg, stream)
+            call_one(fn, arg, stream)
     if forked:
         main.wait_stream(side)
+
+
+def call_one(fn, arg, stream):
+    """One entry of a plan's call list (struct argument or scalar-argument tuple) on `stream`."""
+    if isinstance(arg, tuple):
+        L.call(fn, *arg, stream)
+    else:
+        L.call(fn, arg, stream)
 
 
 def bn_reps(channels: int) -> int:

@@ -131,7 +131,17 @@ class VQStepPlan:
         for i in range(len(r) - 1):
             s2 *= 2
             self.up.append(torch.empty(B, s2, s2, r[i + 1], **act))
-        self.y = torch.empty(B, img, img, 3, **act)                 # pre-Tanh output
+        # bf16: the 3-channel ends (image, output conv) carried as 8 zero-padded channels so every
+        # GEMM operand stays on the packed path (vae_pad_channels / vae_unpad_accumulate)
+        self.pad_rgb = T == torch.bfloat16
+        self.cy = 8 if self.pad_rgb else 3
+        r_ = h[::-1]
+        if self.pad_rgb:
+            self.x8 = torch.zeros(B, img, img, 8, **act)
+            self.w8e = torch.zeros(h[0] * 16 * 8, **act)            # encoder.0 [Co][4][4][8]
+            self.w8d = torch.zeros(r_[-1] * 16 * 8, **act)          # output ConvT [Ci][4][4][8]
+            self.b8d = torch.zeros(8, **f32)
+        self.y = torch.empty(B, img, img, self.cy, **act)           # pre-Tanh output
         self.recon = torch.empty(B, 3, img, img, **f32)
         self.grad_recon = None if fused_loss else torch.zeros(B, 3, img, img, **f32)
         self.vq_grad = torch.ones(1, **f32)
@@ -148,12 +158,17 @@ class VQStepPlan:
         self.g_q = torch.empty_like(self.q)
         self.g_lat = torch.empty_like(self.latpre)
         self.g_enc = [torch.empty_like(t) for t in self.enc]
-        nz = net.layout.total + _pad4(B) + 4
+        npad = (h[0] * 16 * 8 + r_[-1] * 16 * 8 + 8) if self.pad_rgb else 0
+        nz = net.layout.total + _pad4(B) + 4 + npad
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
         self.sse = self.zero[o:o + B]; o += _pad4(B)
-        self.vq_sse = self.zero[o:o + 1]
+        self.vq_sse = self.zero[o:o + 1]; o += 4
+        if self.pad_rgb:                                            # padded weight gradients
+            self.dw8e = self.zero[o:o + h[0] * 16 * 8]; o += h[0] * 16 * 8
+            self.dw8d = self.zero[o:o + r_[-1] * 16 * 8]; o += r_[-1] * 16 * 8
+            self.db8d = self.zero[o:o + 8]; o += 8
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
         self.fwd_calls: List = []
@@ -241,6 +256,15 @@ class VQStepPlan:
         B, img = self.B, net.img_size
         C = h[-1]
         F = self.fwd_calls
+        T = net.dcode
+        r = h[::-1]
+        iup = 1 + NRES + 1
+        wout = f"decoder.{iup + len(r) - 1}.0"                      # output ConvT (-> 3 channels)
+        if self.pad_rgb:
+            F.append(("vae_nchw_to_nhwc_pad", (T, B, 3, img, img, 8, self.x.data_ptr(), self.x8.data_ptr())))
+            F.append(("vae_pad_channels", (T, h[0] * 16, 3, 8, net.w("encoder.0.0.weight"), self.w8e.data_ptr())))
+            F.append(("vae_pad_channels", (T, r[-1] * 16, 3, 8, net.w(wout + ".weight"), self.w8d.data_ptr())))
+            F.append(("vae_pad_channels", (L.F32, 1, 3, 8, net.p(wout + ".bias"), self.b8d.data_ptr())))
         # ---------------------------------------------------------------- encoder
         for i in range(nh):
             src = self.x if i == 0 else self.enc[i - 1]
@@ -249,10 +273,15 @@ class VQStepPlan:
                            k=h[i], p=self.enc[i].shape[1], q=self.enc[i].shape[2], r=4, stride=2, pad=1)
             if i == 0:
                 a.h = a.w = img
-                a.x_nchw_f32, a.x = 1, self.x.data_ptr()
+                if self.pad_rgb:
+                    a.c, a.x = 8, self.x8.data_ptr()
+                else:
+                    a.x_nchw_f32, a.x = 1, self.x.data_ptr()
             else:
                 a.x, a.x_xf = src.data_ptr(), _act()
             a.wt, a.bias = net.w(f"encoder.{i}.0.weight"), net.p(f"encoder.{i}.0.bias")
+            if i == 0 and self.pad_rgb:
+                a.wt = self.w8e.data_ptr()
             a.y = self.enc[i].data_ptr()
             self._add(F, "vae_conv2d_fwd", a)
         a = self._conv(self.enc[-1], C, C, 3, 1, 1)
@@ -285,21 +314,21 @@ class VQStepPlan:
         a.y = self.d_in.data_ptr()
         self._add(F, "vae_conv2d_fwd", a)
         self._res_stack("decoder", 1, self.d_in, self.d_t, self.d_h)
-        r = h[::-1]
-        iup = 1 + NRES + 1
         src = self.d_h[-1]
         for i in range(len(r)):
             last = i == len(r) - 1
             dst = self.y if last else self.up[i]
-            cout = 3 if last else r[i + 1]
+            cout = self.cy if last else r[i + 1]
             a = self._conv(src, r[i], cout, 4, 2, 1, transposed=True)
             a.x, a.x_xf = src.data_ptr(), _act()
             a.wt, a.bias = net.w(f"decoder.{iup + i}.0.weight"), net.p(f"decoder.{iup + i}.0.bias")
+            if last and self.pad_rgb:
+                a.wt, a.bias = self.w8d.data_ptr(), self.b8d.data_ptr()
             a.y = dst.data_ptr()
             self._add(F, "vae_convT2d_fwd", a)
             src = dst
         # ---------------------------------------------------------------- Tanh + SSE + loss
-        rc = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3)
+        rc = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3, ld=self.cy)
         rc.y, rc.target, rc.recon, rc.sse = self.y.data_ptr(), self.x.data_ptr(), self.recon.data_ptr(), self.sse.data_ptr()
         if self.fused_loss:
             rc.dy, rc.grad_scale = self.g_y.data_ptr(), 1.0 / (B * 3 * img * img)
@@ -314,7 +343,7 @@ class VQStepPlan:
         # ================================================================ backward
         Bw = self.bwd_calls
         if not self.fused_loss:
-            rb = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3)
+            rb = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3, ld=self.cy)
             rb.target, rb.recon = self.x.data_ptr(), self.recon.data_ptr()
             rb.dy, rb.grad_recon = self.g_y.data_ptr(), self.grad_recon.data_ptr()
             self._add(Bw, "vae_recon_bwd", rb)
@@ -323,17 +352,24 @@ class VQStepPlan:
         gouts = self.g_up + [self.g_y]
         for i in reversed(range(len(r))):
             last = i == len(r) - 1
-            cout = 3 if last else r[i + 1]
+            cout = self.cy if last else r[i + 1]
             xin = ups[i]
             name = f"decoder.{iup + i}.0"
+            padded = last and self.pad_rgb
             a = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
-            a.dy, a.wt = gouts[i].data_ptr(), net.w(name + ".weight")
+            a.dy, a.wt = gouts[i].data_ptr(), (self.w8d.data_ptr() if padded else net.w(name + ".weight"))
             a.dx, a.dx_epi = gups[i].data_ptr(), _act(SLOPE, xin)
             self._add(Bw, "vae_convT2d_bwd_data", a)
             f = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
             f.x, f.x_xf = xin.data_ptr(), _act()
-            f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
+            if padded:
+                f.dy, f.dw, f.db = gouts[i].data_ptr(), self.dw8d.data_ptr(), self.db8d.data_ptr()
+            else:
+                f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
             self._add(Bw, "vae_convT2d_bwd_filter", f)
+            if padded:
+                Bw.append(("vae_unpad_accumulate", (r[-1] * 16, 8, 3, self.dw8d.data_ptr(), self.g(name + ".weight"))))
+                Bw.append(("vae_unpad_accumulate", (1, 8, 3, self.db8d.data_ptr(), self.g(name + ".bias"))))
         g_din = self._res_stack_bwd("decoder", 1, self.d_in, self.d_t, self.d_h)
         a = self._conv(self.q, E, C, 3, 1, 1)
         a.dy, a.wt, a.dx = g_din.data_ptr(), net.w("decoder.0.0.weight"), self.g_q.data_ptr()
@@ -367,12 +403,18 @@ class VQStepPlan:
             mk = lambda: L.ConvArgs(dtype=net.dcode, n=B, h=hin, w=hin, c=cin, k=h[i], p=self.enc[i].shape[1],
                                     q=self.enc[i].shape[2], r=4, stride=2, pad=1)
             f = mk()
-            if i == 0:
+            if i == 0 and self.pad_rgb:
+                f.c, f.x = 8, self.x8.data_ptr()
+            elif i == 0:
                 f.x_nchw_f32, f.x = 1, self.x.data_ptr()
             else:
                 f.x, f.x_xf = self.enc[i - 1].data_ptr(), _act()
             f.dy, f.dw, f.db = self.g_enc[i].data_ptr(), self.g(f"encoder.{i}.0.weight"), self.g(f"encoder.{i}.0.bias")
+            if i == 0 and self.pad_rgb:
+                f.dw = self.dw8e.data_ptr()
             self._add(Bw, "vae_conv2d_bwd_filter", f)
+            if i == 0 and self.pad_rgb:
+                Bw.append(("vae_unpad_accumulate", (h[0] * 16, 8, 3, self.dw8e.data_ptr(), self.g("encoder.0.0.weight"))))
             if i > 0:
                 a = mk()
                 a.dy, a.wt = self.g_enc[i].data_ptr(), net.w(f"encoder.{i}.0.weight")

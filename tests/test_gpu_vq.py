@@ -212,3 +212,18 @@ def test_conv_stride1_bwd_data_residual_act(dtype, r, pad):
     tol = 2e-5 if dtype == torch.float32 else 2e-2
     err = float((got - want).abs().max() / want.abs().max())
     assert err < tol, err
+
+
+def test_vq_bf16_gradients_close_to_oracle():
+    """bf16 VQ-VAE step (padded 8-channel image and output ConvT) against the teacher-forced fp32
+    oracle: gradients of the padded layers and the codebook within 5e-2 relative norm."""
+    from oracle import vae_oracle as O
+    meta, _ = load_case("vq_b4")
+    sd, x, net, plan, opt = _step(meta, torch.bfloat16)
+    o = O.train_step("VQVAE", sd, x, M_N=0.0, lr=meta["lr"], vq_beta=meta["ctor"]["beta"],
+                     vq_indices=plan.indices.cpu(), do_adam=False)
+    grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
+    for name in ("encoder.0.0.weight", "encoder.0.0.bias", "decoder.9.0.weight", "decoder.9.0.bias",
+                 "vq_layer.embedding.weight", "decoder.8.0.weight"):
+        err = float((grads[name] - o["grads"][name]).norm() / o["grads"][name].norm())
+        assert err < 5e-2, (name, err)

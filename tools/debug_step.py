@@ -7,7 +7,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "pytorch-vae_amd"), os.path.join(REPO, "tests")]
 from golden_util import case_inputs, load_case  # noqa: E402
 from vae_amd import _lib as L  # noqa: E402
-from vae_amd.net import StepPlan, VAENet  # noqa: E402
+from vae_amd.net import StepPlan, VAENet, call_one  # noqa: E402
 
 meta, ref = load_case(sys.argv[1] if len(sys.argv) > 1 else "vanilla_b16")
 sd, x, eps = case_inputs(meta)
@@ -22,9 +22,6 @@ L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, step.data_
 torch.cuda.synchronize(); print("step_begin ok", flush=True)
 for i, (fn, arg) in enumerate(plan.fwd_calls + plan.bwd_calls):
     print(f"[{i}] {fn} ...", flush=True)
-    if fn == "vae_reparam_fwd":
-        L.call(fn, *plan._reparam, st)
-    else:
-        L.call(fn, arg, st)
+    call_one(fn, arg, st)
     torch.cuda.synchronize()
 print("all ok", plan.out.tolist())

@@ -30,7 +30,7 @@ def main():
     args = ap.parse_args()
     from vae_amd import _lib as L
     from vae_amd.engine import FusedAdam, TrainStep
-    from vae_amd.net import StepPlan, VAENet
+    from vae_amd.net import StepPlan, VAENet, call_one
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=torch.Generator().manual_seed(0))
     plan = StepPlan(net, args.batch)
@@ -55,10 +55,7 @@ def main():
                 continue
             torch.cuda._sleep(1000)                      # marker kernel (spin_kernel)
             for _ in range(args.reps):
-                if fn == "vae_reparam_fwd":
-                    L.call(fn, *plan._reparam, sp)
-                else:
-                    L.call(fn, ref, sp)
+                call_one(fn, ref, sp)
             groups.append({"launch": i, "fn": fn, "split": s})
             if ref is not None and hasattr(ref._obj, "split_k"):
                 ref._obj.split_k = 0

@@ -32,7 +32,7 @@ def main():
     args = ap.parse_args()
     from vae_amd import _lib as L
     from vae_amd.engine import FusedAdam, TrainStep
-    from vae_amd.net import StepPlan, VAENet
+    from vae_amd.net import StepPlan, VAENet, call_one
     lib = L.load()
     assert "probe" in lib._name, "load the probe build (VAE_HIP_LIB=probe)"
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -59,10 +59,7 @@ def main():
         for rep in range(3):
             buf[8:].zero_()
             torch.cuda.synchronize()
-            if fn == "vae_reparam_fwd":
-                L.call(fn, *plan._reparam, sp)
-            else:
-                L.call(fn, ref, sp)
+            call_one(fn, ref, sp)
             torch.cuda.synchronize()
         r = buf[8:].view(cap, 8).cpu().numpy().astype(np.int64)
         r = r[r[:, 1] != 0]                      # slots written by a block (wall start != 0)
