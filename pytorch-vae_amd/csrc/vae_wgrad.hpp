@@ -224,6 +224,7 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WgradParams p) {
 inline bool wgrad_ok(int dtype, const vae_xform& ux, const vae_xform& vx, long u_elems, long v_elems, int M, int J) {
   if (dtype != VAE_BF16 || getenv("VAE_NO_WGRAD2")) return false;
   if (M % 8 || J % 8) return false;
+  // (J == 8, the padded RGB ends, measured slower too: 536 -> 692 us on the VQ output ConvT)
   if (!getenv("VAE_WGRAD2_ALL") && (M < 64 || J < 64 || u_elems / M < 8192)) return false;
   auto xf_ok2 = [](const vae_xform& x) {
     if (x.kind == VAE_X_BN_ACT || x.kind == VAE_X_BN_DY) return x.table != nullptr;
