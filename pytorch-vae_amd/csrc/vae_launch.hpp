@@ -363,7 +363,56 @@ inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req
   return launch_tiled<__bf16, __bf16, __bf16, AM, BMD, EM, DYA, DYB>(p, t, st);
 }
 
-// Column sums of a plain [rows][C] tensor (bias gradient of a layer whose dy is stored as is)
+// Column sums of a plain [rows][C] tensor (bias gradient of a layer whose dy is stored as is).
+// The tensor is streamed as flat 8-element vectors (C % 8 == 0) or single elements (any C). The
+// block size is a multiple of the number of vector groups per row, and so is the grid stride, so
+// every thread keeps the same channels for its whole loop; partials meet in LDS and each
+// workgroup issues one global atomic per channel (grid capped at one workgroup per CU).
+template <class T, int V>
+__global__ void __launch_bounds__(256) column_sum_flat(const T* x, long nvec, int C, float* out) {
+  extern __shared__ float red[];
+  const int groups = C / V;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) red[c] = 0.f;
+  __syncthreads();
+  const int c0 = (int)(threadIdx.x % groups) * V;
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < nvec; i += 4 * stride) {       // 4 independent loads in flight
+    if constexpr (V == 8) {
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ld8(x + (i + u * stride) * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[u][j];
+    } else {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld_f(x + i + u * stride);
+      acc[0] += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+  }
+  for (; i < nvec; i += stride) {
+    if constexpr (V == 8) {
+      float v[8];
+      ld8(x + i * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    } else {
+      acc[0] += ld_f(x + i);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) atomicAdd(red + c0 + j, acc[j]);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(out + c, red[c]);
+}
+
+// Fallback for widths the flat kernel does not cover (more than 256 vector groups per row)
 template <class T>
 __global__ void column_sum(const T* x, long rows, int C, float* out) {
   const int c = blockIdx.y * 64 + (threadIdx.x & 63);
@@ -395,6 +444,24 @@ inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C,
 }
 
 inline int column_sum_launch(int dtype, const void* dy, long rows, int C, float* db, hipStream_t st) {
+  const int V = (C % 8 == 0 && ((uintptr_t)dy % 16) == 0) ? 8 : 1;   // 16-B aligned vectors
+  const int groups = C / V;
+  if (groups <= 256 && rows > 0) {
+    const int bd = (256 / groups) * groups;
+    const long nvec = rows * (long)(C / V);
+    long blocks = (nvec + (long)bd * 8 - 1) / ((long)bd * 8);      // >= 8 vectors per thread
+    if (blocks > 256) blocks = 256;
+    if (blocks < 1) blocks = 1;
+    const size_t lds = (size_t)C * sizeof(float);
+    if (dtype == VAE_F32) {
+      if (V == 8) hipLaunchKernelGGL((column_sum_flat<float, 8>), dim3((unsigned)blocks), dim3(bd), lds, st, (const float*)dy, nvec, C, db);
+      else hipLaunchKernelGGL((column_sum_flat<float, 1>), dim3((unsigned)blocks), dim3(bd), lds, st, (const float*)dy, nvec, C, db);
+    } else {
+      if (V == 8) hipLaunchKernelGGL((column_sum_flat<__bf16, 8>), dim3((unsigned)blocks), dim3(bd), lds, st, (const __bf16*)dy, nvec, C, db);
+      else hipLaunchKernelGGL((column_sum_flat<__bf16, 1>), dim3((unsigned)blocks), dim3(bd), lds, st, (const __bf16*)dy, nvec, C, db);
+    }
+    return check_launch("column_sum");
+  }
   const dim3 grid(64, (C + 63) / 64);
   if (dtype == VAE_F32) hipLaunchKernelGGL(column_sum<float>, grid, dim3(256), 0, st, (const float*)dy, rows, C, db);
   else hipLaunchKernelGGL(column_sum<__bf16>, grid, dim3(256), 0, st, (const __bf16*)dy, rows, C, db);
