@@ -191,13 +191,34 @@ __device__ __forceinline__ bf16x4v tr16_read(const char* generic_lds_addr) {
 }
 
 // ======================================================================= backward
-// gseed = dL/d(pre-tanh) at one pixel/channel
-__device__ __forceinline__ float gseed(const HeadQ& q, int n, int co, int h, int w) {
-  const long oi = (((long)n * NCO + co) * q.h + h) * HW + w;
-  const float y = q.recon[oi];
-  if (q.grad_recon) return q.grad_recon[oi] * (1.f - y * y);
-  const float t = q.target[(((long)(n / q.samples) * NCO + co) * q.h + h) * HW + w];
-  return q.coef[n] * (y - t) * (1.f - y * y);
+// gseed = dL/d(pre-tanh) at one pixel/channel, split into its loads (issued one tile ahead)
+// and the arithmetic: ld = (recon y, grad_recon or target)
+struct SeedLd { float y[2][NCO], t[2][NCO]; };
+
+__device__ __forceinline__ void seed_load(const HeadQ& q, int tile_i, SeedLd& ld) {
+  const int tiles_per_img = q.h / ROWS;
+  const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * ROWS;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int pix = threadIdx.x + 256 * j;
+    const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+    const int hi = h0 + trow - 1, wi = tcol - 1;
+    const bool ok = pix < TPIX && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+#pragma unroll
+    for (int co = 0; co < NCO; ++co) {
+      const long oi = (((long)n * NCO + co) * q.h + hi) * HW + wi;
+      ld.y[j][co] = ok ? q.recon[oi] : 0.f;
+      ld.t[j][co] = !ok ? 0.f
+                        : q.grad_recon ? q.grad_recon[oi]
+                                       : q.target[(((long)(n / q.samples) * NCO + co) * q.h + hi) * HW + wi];
+    }
+  }
+}
+
+__device__ __forceinline__ float gseed(const HeadQ& q, int n, const SeedLd& ld, int j, int co) {
+  const float y = ld.y[j][co];
+  if (q.grad_recon) return ld.t[j][co] * (1.f - y * y);
+  return q.coef[n] * (y - ld.t[j][co]) * (1.f - y * y);   // 0 outside the image (y = t = 0)
 }
 
 constexpr int NW = NCO * 9 * HC;        // 864 weight-gradient entries
@@ -235,22 +256,25 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
   float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, dbp[NCO] = {0.f, 0.f, 0.f};
 
   head_tables(q.xf, ta, tb, tp, tq);
+  // software pipeline: the raw y tile and the seed inputs of the next tile are loaded while
+  // this tile's MFMAs run (one workgroup per CU leaves no other wave to hide the latency)
+  u32x4 raw[OCT_PER_T];
+  SeedLd sld;
+  if ((int)blockIdx.x < q.tiles) {
+    const int n0 = blockIdx.x / tiles_per_img;
+    tile_load(q, ry, n0, (blockIdx.x - n0 * tiles_per_img) * ROWS, raw);
+    seed_load(q, blockIdx.x, sld);
+  }
   for (int tile_i = blockIdx.x; tile_i < q.tiles; tile_i += gridDim.x) {
     const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * ROWS;
-    u32x4 raw[OCT_PER_T];
-    tile_load(q, ry, n, h0, raw);
     // gseed over the halo tile: threads walk pixels (2 per thread)
     float gv[2][NCO];
     int gpix[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int pix = threadIdx.x + 256 * j;
-      gpix[j] = pix;
-      const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
-      const int hi = h0 + trow - 1, wi = tcol - 1;
-      const bool ok = pix < TPIX && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+      gpix[j] = threadIdx.x + 256 * j;
 #pragma unroll
-      for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = ok ? gseed(q, n, c2, hi, wi) : 0.f;
+      for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = gseed(q, n, sld, j, c2);
     }
     __syncthreads();                    // previous tile's LDS reads done (and tables ready)
     tile_store(q, h0, raw, tile, ta, tb);
@@ -285,6 +309,14 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
       }
     }
     __syncthreads();
+    {
+      const int nx = tile_i + gridDim.x;
+      if (nx < q.tiles) {
+        const int n1 = nx / tiles_per_img;
+        tile_load(q, ry, n1, (nx - n1 * tiles_per_img) * ROWS, raw);
+        seed_load(q, nx, sld);
+      }
+    }
 
     if (q.data) {
       // ---- dact for this wave's 4 groups of 16 pixels, N = 32 channels (2 n-frags)
