@@ -18,6 +18,8 @@
 //            K = the tile's 256 pixels; the act operand is read transposed (ds_read_b64_tr_b16)
 //            from the same LDS tile; per-block partials go to a slab summed by vae_reduce_rows
 //            (fixed order: deterministic, and no same-address atomics).
+#include <stdlib.h>
+
 #include "vae_common.hpp"
 
 namespace vae {
@@ -510,7 +512,18 @@ int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
 // Persistent grid of the backward: one workgroup per CU.  Swept on MI355X (B=64 step):
 // 128 -> 78.7 us, 192 -> 61.7, 256 -> 45.6, 512 -> 50.5, 1024 -> 61.4 (more blocks means more
 // filter partials to reduce and more halo re-reads; fewer leaves CUs idle).
+// Re-swept with the tile-ahead loads: 192 -> 50.4 us, 256 -> 38.5, 320 -> 55.6, 384 -> 49.8,
+// 512 -> 43.9 (scripts/gpu_headgrid.sh): 256 divides the 1024 tiles of B=64 evenly.
 constexpr int kHeadGrid = 256;
+// VAE_HEAD_GRID overrides it (tuning sweeps only; read once)
+int head_grid() {
+  static const int g = [] {
+    const char* e = getenv("VAE_HEAD_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : kHeadGrid;
+  }();
+  return g;
+}
 
 // data / filter: which halves of the backward to run.  The filter half writes per-block partials
 // into the caller's workspace (when large enough) and reduces them into dw/db in fixed order.
@@ -519,7 +532,7 @@ int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStre
   if (data && a->dx_epi.kind != VAE_X_BN_ACT) return kHeadFallback;   // the fused epilogue is BatchNorm+LReLU
   HeadQ q = head_q(a);
   q.data = data; q.filter = filter;
-  const int grid = q.tiles < kHeadGrid ? q.tiles : kHeadGrid;
+  const int grid = q.tiles < head_grid() ? q.tiles : head_grid();
   const long need = (long)grid * SLAB_COLS * 4;
   float* ws = static_cast<float*>(a->workspace);
   const bool slab = filter && ws && a->workspace_bytes >= need;
