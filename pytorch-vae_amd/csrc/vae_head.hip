@@ -127,13 +127,13 @@ __global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
   __shared__ __attribute__((aligned(16))) char tile[TPIX * HC * 2];
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float red[4];
+  __shared__ __attribute__((aligned(16))) float wsh[NCO * 9 * HC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int tiles_per_img = q.h / ROWS;
   const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x - n * tiles_per_img) * ROWS;
   const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
   u32x4 raw[OCT_PER_T];
   tile_load(q, ry, n, h0, raw);
-  // B fragments: W[co = lane&15][tap][8*(lane>>4) .. +7] (zero for co >= 3)
   const int co = lane & 15, g = lane >> 4;
   // the epilogue's target pixels, in flight with the tile (no global load after the MFMAs)
   f32x4v tgv[4];
@@ -144,15 +144,26 @@ __global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
                                                          c0 + 4 * g)
                        : f32x4v{0.f, 0.f, 0.f, 0.f};
   }
-  bf16x8 bw[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bw[t][j] = (__bf16)(co < NCO ? q.wt[(co * 9 + t) * HC + 8 * g + j] : 0.f);
+  // the 864 weights: one coalesced pass into LDS (per-lane scattered scalar loads of the
+  // fragments cost ~72 vector-memory instructions per wave)
+  for (int i = threadIdx.x; i < NCO * 9 * HC; i += 256) wsh[i] = q.wt[i];
   const float bco = co < NCO ? q.bias[co] : 0.f;
   head_tables(q.xf, ta, tb, tp, tq);
   __syncthreads();
   tile_store(q, h0, raw, tile, ta, tb);
+  // B fragments: W[co = lane&15][tap][8*(lane>>4) .. +7] (zero for co >= 3)
+  bf16x8 bw[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int wr = (co < NCO ? co : 0) * 9 + t;   // rows co >= 3 read row 0, then zeroed
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(&wsh[wr * HC + 8 * g]);
+    const f32x4 w1 = *reinterpret_cast<const f32x4*>(&wsh[wr * HC + 8 * g + 4]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bw[t][j] = (__bf16)(co < NCO ? w0[j] : 0.f);
+      bw[t][4 + j] = (__bf16)(co < NCO ? w1[j] : 0.f);
+    }
+  }
   __syncthreads();
   float sq = 0.f;
 #pragma unroll
