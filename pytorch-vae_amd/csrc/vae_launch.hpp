@@ -422,24 +422,27 @@ __global__ void column_sum(const T* x, long rows, int C, float* out) {
   atomicAdd(out + c, s);
 }
 
-// W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] (bf16): the data gradient of a stride-1 conv as a conv
-__global__ void flip_weights_kernel(const __bf16* w, __bf16* wf, int K, int R, int C) {
-  const long n = (long)K * R * R * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int k = (int)(i % K);
-    long t = i / K;
-    const int s = (int)(t % R); t /= R;
-    const int r = (int)(t % R);
-    const int c = (int)(t / R);
-    wf[i] = w[(((long)k * R + (R - 1 - r)) * R + (R - 1 - s)) * C + c];
+// W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] (bf16): the data gradient of a stride-1 conv as a conv.
+// Per tap a [K][C] -> [C][K] transpose through a 32x33 LDS tile, so reads and writes are both
+// 64-byte row segments (an element-wise gather reads with a stride of R*R*C elements).
+__global__ void __launch_bounds__(256) flip_weights_kernel(const __bf16* w, __bf16* wf, int K, int RR, int C) {
+  __shared__ float t[32][33];
+  const int tap = blockIdx.z, k0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int j = ty; j < 32; j += 8) {
+    const int k = k0 + j, c = c0 + tx;
+    t[j][tx] = (k < K && c < C) ? (float)w[((long)k * RR + tap) * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int c = c0 + j, k = k0 + tx;
+    if (c < C && k < K) wf[((long)c * RR + (RR - 1 - tap)) * K + k] = (__bf16)t[tx][j];
   }
 }
 
 inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C, hipStream_t st) {
-  const long n = (long)K * R * R * C;
-  long blocks = (n + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(flip_weights_kernel, dim3((unsigned)blocks), dim3(256), 0, st, w, wf, K, R, C);
+  const dim3 grid((C + 31) / 32, (K + 31) / 32, R * R);
+  hipLaunchKernelGGL(flip_weights_kernel, grid, dim3(256), 0, st, w, wf, K, R * R, C);
   return check_launch("flip_weights");
 }
 
