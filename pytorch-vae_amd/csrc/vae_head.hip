@@ -245,22 +245,14 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
   __shared__ __attribute__((aligned(16))) char ytile[OWN * HC * 2];      // raw y of the own pixels
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float r1[4][HC], r2[4][HC], rdb[4][NCO];
+  __shared__ float wsh[NCO * 9 * HC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int tiles_per_img = q.h / ROWS;
   const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
 
-  // dgrad B fragments: B[k = tap*4 + co][n = c] = W[co][tap][c], k-step ks, n-frag nf
-  bf16x8 bd[2][2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-    for (int nf = 0; nf < 2; ++nf)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int tap = ks * 8 + 2 * g + (j >> 2), c2 = j & 3, c = nf * 16 + li;
-        bd[ks][nf][j] = (__bf16)(tap < 9 && c2 < NCO ? q.wt[(c2 * 9 + tap) * HC + c] : 0.f);
-      }
+  // the 864 weights through LDS in one coalesced pass (built into fragments after the prologue)
+  for (int i = threadIdx.x; i < NCO * 9 * HC; i += 256) wsh[i] = q.wt[i];
   // filter accumulators: this wave's n-frags f = wave + 4*i (18 n-frags of 16 over (tap, c))
   constexpr int NFW = 5;
   f32x4v accw[NFW];
@@ -278,6 +270,18 @@ __global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
     tile_load(q, ry, n0, (blockIdx.x - n0 * tiles_per_img) * ROWS, raw);
     seed_load(q, blockIdx.x, sld);
   }
+  __syncthreads();
+  // dgrad B fragments: B[k = tap*4 + co][n = c] = W[co][tap][c], k-step ks, n-frag nf
+  bf16x8 bd[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = ks * 8 + 2 * g + (j >> 2), c2 = j & 3, c = nf * 16 + li;
+        bd[ks][nf][j] = (__bf16)(tap < 9 && c2 < NCO ? wsh[(c2 * 9 + tap) * HC + c] : 0.f);
+      }
   for (int tile_i = blockIdx.x; tile_i < q.tiles; tile_i += gridDim.x) {
     const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * ROWS;
     // gseed over the halo tile: threads walk pixels (2 per thread)
