@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: train images/sec of the VanillaVAE training step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|f32] [--arch vanilla|betaH|iwae]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|f32] [--arch vanilla|betaH|iwae|vq]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+With --gpus N > 1 and no RANK in the environment, this process starts the N rank processes
+itself (before anything touches the GPU) and waits for them; rank r runs on device
+r % device_count.  Ranks on distinct devices exchange gradients over RCCL; when there are
+fewer devices than ranks (a 1-GPU box) they share devices and fall back to gloo, because RCCL
+needs one device per rank.  --selftest replaces the training step with a CPU stand-in (the
+gradient exchange only) to check the launcher, the barrier/max-over-ranks timing and the
+output line without a GPU (tests/test_bench_launcher.py).
 
 Workload (BASELINE.json configs[1]): VanillaVAE latent_dim=128, 64x64x3 synthetic images, batch 64
 per GPU (weak scaling, data parallel over ranks, RCCL gradient all-reduce), bf16 MFMA with fp32
@@ -24,6 +32,8 @@ import glob
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,10 +58,49 @@ def parse():
     ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae", "vq"],
                     help="vq: BASELINE.json configs[4], VQ-VAE B=128 (pass --batch 128)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--concurrent", action="store_true",
+                    help="weight gradients on a side stream beside the data-gradient chain (measured slower "
+                         "for VanillaVAE: 0.88 vs 0.77 ms, the graph's per-call fork/join edges)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernel-breakdown", action="store_true", help="print per-kernel times to stderr")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU stand-in step (launcher / timing / output contract check; no GPU)")
     return ap.parse_args()
+
+
+# ----------------------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """Start n rank processes of this script (torchrun-style env) and wait for them.  Runs in a
+    parent that never touched the GPU; if one rank fails the others are stopped (by PID)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 # ----------------------------------------------------------------------------- kernels
@@ -212,18 +261,85 @@ def cpu_baseline(batch, seconds, arch="vanilla"):
 
 
 # ----------------------------------------------------------------------------- main
+def timed_loop(step, args, distributed, sync):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + device sync on both
+    sides; returns the max over ranks of the timed region (seconds)."""
+    for _ in range(args.warmup):
+        step()
+    sync()
+    if distributed:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    if distributed:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def selftest(args, distributed):
+    """The launcher / timing / output contract without a GPU: the step is a gloo all-reduce of a
+    gradient-sized buffer (3,937,635 fp32, VanillaVAE) — the only cross-rank work of the real step."""
+    if distributed:
+        dist.init_process_group("gloo")
+    rank, world = (dist.get_rank(), dist.get_world_size()) if distributed else (0, 1)
+    grads = torch.full((3937635,), float(rank + 1))
+
+    def step():
+        if distributed:
+            dist.all_reduce(grads)
+            grads.div_(world)
+
+    elapsed = timed_loop(step, args, distributed, lambda: None)
+    if rank == 0:
+        print(json.dumps({"metric": "selftest (CPU stand-in step: gradient all-reduce only)",
+                          "value": round(world * args.batch * args.steps / elapsed, 1), "unit": "images/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                          "selftest": True, "grad_mean_ok": bool(torch.allclose(grads, torch.full_like(grads, (world + 1) / 2))),
+                          "config": {"workload": "selftest", "per_gpu_batch": args.batch,
+                                     "global_batch": world * args.batch, "parallelism": f"dp{world}"}}), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "RANK" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))          # parent: never touches the GPU
     distributed = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    if args.selftest:
+        return selftest(args, distributed)
+    ndev = max(1, torch.cuda.device_count())
+    comm = "none"
     if distributed:
         local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world_env = int(os.environ["WORLD_SIZE"])
+        dev = local % ndev
+        torch.cuda.set_device(dev)
+        if world_env > ndev:
+            # fewer devices than ranks: RCCL cannot place two ranks on one device
+            dist.init_process_group("gloo")
+            comm = f"gloo ({world_env} ranks on {ndev} device(s))"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            comm = "rccl"
         rank, world = dist.get_rank(), dist.get_world_size()
     else:
         rank, world = 0, 1
         torch.cuda.set_device(0)
-    from vae_amd import _lib as L
+    from vae_amd import _lib as L  # noqa: F401
     from vae_amd.engine import FusedAdam, TrainStep
     from vae_amd.net import StepPlan, VAENet
 
@@ -234,14 +350,14 @@ def main():
     if args.arch == "vq":
         from vae_amd.vq import VQNet, VQStepPlan
         net = VQNet(dtype=dtype, device="cuda", generator=gen)
-        plan = VQStepPlan(net, args.batch)
+        plan = VQStepPlan(net, args.batch, concurrent=args.concurrent)
         opt = FusedAdam(net, lr=0.005)                             # configs/vae/vq_vae.yaml LR
     else:
         net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
         loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
         kld = {"vanilla": 1e-8, "betaH": 2.5e-4, "iwae": 2.5e-4}[args.arch]
         lr = {"vanilla": 0.005, "betaH": 0.005, "iwae": 0.007}[args.arch]
-        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S)
+        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S, concurrent=args.concurrent)
         opt = FusedAdam(net, lr=lr)
     # synthetic data resident in HBM (per-rank seed 1265+rank): U[0,1) images, N(0,1) eps
     g = torch.Generator(device="cuda").manual_seed(1265 + rank)
@@ -250,25 +366,8 @@ def main():
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
     step = TrainStep(net, plan, opt, graph=not args.no_graph)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    loss_terms = plan.out.tolist()
+    elapsed = timed_loop(step, args, distributed, torch.cuda.synchronize)
+    loss_terms = step.loss_terms()                  # rank mean (sync_dist) when distributed
     finite = all(math.isfinite(v) for v in loss_terms)
 
     if rank != 0:
@@ -328,7 +427,8 @@ def main():
                                 f"{'VanillaVAE' if args.arch == 'vanilla' else args.arch} latent_dim=128 "
                                 f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}"),
                    "per_gpu_batch": args.batch, "global_batch": world * args.batch,
-                   "parallelism": f"dp{world}", "graph": not args.no_graph},
+                   "parallelism": f"dp{world}", "graph": not args.no_graph, "comm": comm,
+                   "devices_used": min(world, ndev)},
         "elbo": {"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1],
                  ("VQ_Loss" if args.arch == "vq" else "KLD"): loss_terms[2], "finite": finite},
         "sum_kernel_us_isolated": round(step_kernel_us, 1),

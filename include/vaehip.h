@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 7
+#define VAE_ABI_VERSION 8
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -160,6 +160,11 @@ typedef struct vae_conv_args {
    * bn_counter: reserved (a zeroed uint32 slot; may be NULL). */
   const struct vae_bn_args* bn_finalize;
   uint32_t* bn_counter;
+  /* Optional bf16 copy of wt with its first and last axes swapped ([k][r][s][c] of a
+   * ConvTranspose2d's [c][r][s][k], [c][r][s][k] of a Conv2d's [k][r][s][c]): the k-contiguous
+   * weight rows the bf16 convT2d_fwd / conv2d_bwd_data GEMMs read (vae_swap_axes).  NULL: the
+   * call builds it at the end of the workspace first (one extra launch). */
+  const void* wt_t;
 } vae_conv_args;
 
 /* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,
@@ -341,10 +346,22 @@ int vae_elbo_fwd(const vae_elbo_args* a, void* stream);
  *     step/lr are device scalars so the call can be replayed from a graph.  When
  *     p_lowp != NULL the updated parameters are also written as bf16 (weight copies). --- */
 int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v,
-                  const int32_t* step, const float* lr, float beta1, float beta2, float eps,
+                  const int32_t* step, const float* lr, double beta1, double beta2, float eps,
                   float weight_decay, void* p_lowp, void* stream);
 /* --- fp32 -> bf16 copy (weight copies when the optimizer is not vae_adam_step) -------- */
 int vae_cast_bf16(int64_t n, const float* src, void* dst, void* stream);
+/* --- swapped-axes bf16 weight copies (vae_conv_args.wt_t), several tensors per launch:
+ *     dst[b][t][a] = bf16(src[a][t][b]), src fp32 [a][rs][b] (the master weights), dst bf16
+ *     [b][rs][a].  A ConvTranspose2d weight [c][r][s][k] gives the [k][r][s][c] rows its bf16
+ *     forward GEMM reads; a Conv2d weight [k][r][s][c] the [c][r][s][k] rows of its data
+ *     gradient.  Replaces the per-call rebuild at the end of the workspace. ------------ */
+#define VAE_SWAP_MAX 16
+typedef struct vae_swap_desc {
+  const void* src;
+  void* dst;
+  int32_t a, rs, b;
+} vae_swap_desc;
+int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* stream);
 /* --- start of a training step: zero `bytes` at `zero` and ++*step ------------------ */
 int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream);
 

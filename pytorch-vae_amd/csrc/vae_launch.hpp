@@ -2,6 +2,7 @@
 // setup, slab workspace and the finalize pass.  Included by the entry-point translation units.
 #pragma once
 #include "vae_fgemm.hpp"
+#include "vae_cgemm.hpp"
 #include <stdlib.h>
 
 #ifdef VAE_PROBE
@@ -422,10 +423,11 @@ __global__ void column_sum(const T* x, long rows, int C, float* out) {
   atomicAdd(out + c, s);
 }
 
-// W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] (bf16): the data gradient of a stride-1 conv as a conv.
-// Per tap a [K][C] -> [C][K] transpose through a 32x33 LDS tile, so reads and writes are both
-// 64-byte row segments (an element-wise gather reads with a stride of R*R*C elements).
-__global__ void __launch_bounds__(256) flip_weights_kernel(const __bf16* w, __bf16* wf, int K, int RR, int C) {
+// W'[c][t'][k] = W[k][t][c] (bf16) with t' = t (swap) or RR-1-t (flip: the data gradient of a
+// stride-1 conv as a conv).  Per tap a [K][C] -> [C][K] transpose through a 32x33 LDS tile, so
+// reads and writes are both 64-byte row segments (an element-wise gather reads with a stride of
+// R*R*C elements).
+__global__ void __launch_bounds__(256) flip_weights_kernel(const __bf16* w, __bf16* wf, int K, int RR, int C, int flip) {
   __shared__ float t[32][33];
   const int tap = blockIdx.z, k0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -434,16 +436,123 @@ __global__ void __launch_bounds__(256) flip_weights_kernel(const __bf16* w, __bf
     t[j][tx] = (k < K && c < C) ? (float)w[((long)k * RR + tap) * C + c] : 0.f;
   }
   __syncthreads();
+  const int tap2 = flip ? RR - 1 - tap : tap;
   for (int j = ty; j < 32; j += 8) {
     const int c = c0 + j, k = k0 + tx;
-    if (c < C && k < K) wf[((long)c * RR + (RR - 1 - tap)) * K + k] = (__bf16)t[tx][j];
+    if (c < C && k < K) wf[((long)c * RR + tap2) * K + k] = (__bf16)t[tx][j];
   }
 }
 
-inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C, hipStream_t st) {
+inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C, hipStream_t st, int flip = 1) {
   const dim3 grid((C + 31) / 32, (K + 31) / 32, R * R);
-  hipLaunchKernelGGL(flip_weights_kernel, grid, dim3(256), 0, st, w, wf, K, R * R, C);
+  hipLaunchKernelGGL(flip_weights_kernel, grid, dim3(256), 0, st, w, wf, K, R * R, C, flip);
   return check_launch("flip_weights");
+}
+
+// ------------------------------------------------------------------ bf16 conv-GEMM (vae_cgemm.hpp)
+// Eligible: bf16 NHWC operands with channel counts % 8 (16-byte chunks never straddle a tap),
+// 16-byte aligned tensors, k-contiguous weight rows, and a transform / epilogue pair the kernel
+// is instantiated for.  VAE_NO_CGEMM=1 keeps everything on the generic kernel (A/B timing).
+inline bool cg_ok(const GemmParams& p, int em) {
+  if (getenv("VAE_NO_CGEMM")) return false;
+  if (p.g_nchw || p.ones_col >= 0 || p.gc % 8 || p.N % 8 || p.out_ld % 8 || p.b_ld % 8) return false;
+  if (!aligned(p.a_ptr, 16) || !aligned(p.b_ptr, 16) || !aligned(p.out, 16)) return false;
+  const int k = p.a_xf.kind;
+  if (em == E_STORE && k == VAE_X_BN_DY) return false;
+  if (em == E_BNBWD && k == VAE_X_BN_ACT) return false;
+  if ((k == VAE_X_BN_ACT || k == VAE_X_BN_DY) && (p.a_xf.channels != p.gc || p.a_xf.channels > MAXC)) return false;
+  if (k == VAE_X_BN_DY && !aligned(p.a_xf.aux, 16)) return false;
+  if (p.residual && !aligned(p.residual, 16)) return false;
+  if (em == E_BNBWD && p.epi_xf.kind != VAE_X_NONE) {
+    if (!aligned(p.epi_xf.aux, 16) || p.epi_xf.channels % 8) return false;
+  }
+  return true;
+}
+
+struct CgTile { int bm, bn; };
+
+// Largest tile that still gives every CU ~2 workgroups; split-K (slabs + igemm_finalize) when
+// even the smallest leaves the chip half empty and K is deep.
+inline CgTile cg_pick(long M, long N, int nphase) {
+  const CgTile c[] = {{128, 128}, {64, 64}, {64, 32}, {32, 64}, {32, 32}};
+  for (const CgTile& t : c) {
+    if (t.bm > 32 && M < t.bm) continue;
+    if (t.bn > 32 && N < t.bn) continue;
+    if (tile_blocks(M, N, nphase, Tile{t.bm, t.bn}) >= 2 * kCUs) return t;
+  }
+  return CgTile{32, 32};
+}
+
+template <int BM, int BN> constexpr int cg_bk() { return BM >= 128 ? 64 : 128; }
+
+template <int AM, int XA, int EM>
+inline void cg_launch_tile(const GemmParams& p, CgTile t, hipStream_t st) {
+  const size_t lds = (size_t)((XA == VAE_X_BN_ACT || XA == VAE_X_BN_DY ? 3 * tab_stride(p.a_xf.channels) : 0) +
+                              (EM == E_BNBWD ? 4 * tab_stride(p.epi_xf.channels) : 0)) * 4;
+#define VAE_CG_CASE(BM_, BN_) \
+  if (t.bm == BM_ && t.bn == BN_) { \
+    const unsigned nb = (unsigned)(((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.nphase * p.ksplit); \
+    hipLaunchKernelGGL((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM>), dim3(nb), dim3(256), lds, st, p); \
+    return; \
+  }
+  VAE_CG_CASE(128, 128)
+  VAE_CG_CASE(64, 64)
+  VAE_CG_CASE(64, 32)
+  VAE_CG_CASE(32, 64)
+  VAE_CG_CASE(32, 32)
+#undef VAE_CG_CASE
+}
+
+// Plan tile + split-K and launch (GemmParams as for launch_tiled; B must be k-contiguous rows)
+template <int AM, int EM>
+inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipStream_t st) {
+  if (p.M <= 0 || p.N <= 0) return VAE_OK;
+  finish_divs(p);
+  const long ab = a_elems<AM>(p) * 2, bb = (long)(p.N - 1) * p.b_ld * 2 + (long)p.b_ld * 2;
+  if (ab <= 0 || bb <= 0 || ab >= (1l << 31) || bb >= (1l << 31))
+    return fail(VAE_E_UNSUPPORTED, "cgemm: operand of %ld / %ld bytes (buffer addressing needs < 2 GiB)", ab, bb);
+  p.a_bytes = (uint32_t)ab;
+  p.b_bytes = (uint32_t)bb;
+  const long ob = out_elems(p) * 2;
+  if (ob >= (1l << 31)) return fail(VAE_E_UNSUPPORTED, "cgemm: output of %ld bytes", ob);
+  p.out_aux_bytes = (uint32_t)ob;
+#ifdef VAE_PROBE
+  p.probe = vae_probe_buffer();
+#endif
+  const CgTile t = cg_pick(p.M, p.N, p.nphase);
+  const int bk = t.bm >= 128 ? 64 : 128;
+  int kmax = p.K;
+  if (AM == A_CONVT) {
+    kmax = 0;
+    for (int ph = 0; ph < p.nphase; ++ph) {
+      const int k = p.ntap_h[ph / p.gs] * p.ntap_w[ph % p.gs] * p.gc;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  const int ktiles = (kmax + bk - 1) / bk;
+  const long blocks = tile_blocks(p.M, p.N, p.nphase, Tile{t.bm, t.bn});
+  int split = split_req > 0 ? split_req : 1;
+  if (split_req <= 0 && blocks < kCUs && ktiles >= 4) {
+    split = (int)((2 * kCUs + blocks - 1) / blocks);
+    if (split > ktiles / 2) split = ktiles / 2;
+  }
+  if (split > 1 && (!ws || (long)split * p.M * p.N * p.nphase * 4 > ws_bytes)) split = 1;
+  p.ksplit = split < 1 ? 1 : split;
+  p.slab = p.ksplit > 1 ? static_cast<float*>(ws) : nullptr;
+  switch (p.a_xf.kind) {
+    case VAE_X_NONE: cg_launch_tile<AM, VAE_X_NONE, EM>(p, t, st); break;
+    case VAE_X_ACT: cg_launch_tile<AM, VAE_X_ACT, EM>(p, t, st); break;
+    case VAE_X_BN_ACT:
+      if constexpr (EM == E_STORE) cg_launch_tile<AM, VAE_X_BN_ACT, EM>(p, t, st);
+      break;
+    case VAE_X_BN_DY:
+      if constexpr (EM == E_BNBWD) cg_launch_tile<AM, VAE_X_BN_DY, EM>(p, t, st);
+      break;
+  }
+  int rc = check_launch("cgemm");
+  if (rc) return rc;
+  if (p.slab) return launch_finalize<__bf16, EM>(p, st);
+  return VAE_OK;
 }
 
 inline int column_sum_launch(int dtype, const void* dy, long rows, int C, float* db, hipStream_t st) {

@@ -465,18 +465,22 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
 // ---------------------------------------------------------------------------- Adam
 template <bool LOWP>
 __global__ void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, const int* step, const float* lr, float b1, float b2, float eps,
+                            float* __restrict__ v, const int* step, const float* lr, double b1, double b2, float eps,
                             float wd, __bf16* __restrict__ lowp) {
-  const float t = (float)(*step);
-  const float bc1 = 1.f - powf(b1, t), bc2 = 1.f - powf(b2, t);
-  const float step_size = *lr / bc1;
-  const float bc2s = sqrtf(bc2);
+  // torch.optim.Adam (single-tensor path): the scalars it derives from the Python-float
+  // hyper-parameters (1 - beta, bias corrections, step size) are formed in double and rounded
+  // once, as torch does — 1 - 0.999f in fp32 would be 1.3e-5 off 1 - 0.999
+  const double t = (double)(*step);
+  const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2), b2f = (float)b2;
+  const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
+  const float step_size = (float)((double)*lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float gi = g[i];
     float pi = p[i];
     if (wd != 0.f) gi = fmaf(wd, pi, gi);
-    const float mi = m[i] + (1.f - b1) * (gi - m[i]);                 // lerp (torch Adam)
-    const float vi = fmaf(v[i], b2, (1.f - b2) * gi * gi);
+    const float mi = m[i] + omb1 * (gi - m[i]);                       // lerp (torch Adam)
+    const float vi = v[i] * b2f + omb2 * gi * gi;                     // mul_(beta2).addcmul_(g, g, 1-beta2)
     const float den = sqrtf(vi) / bc2s + eps;
     pi = pi - step_size * (mi / den);
     m[i] = mi; v[i] = vi; p[i] = pi;
@@ -637,7 +641,7 @@ extern "C" int vae_elbo_fwd(const vae_elbo_args* a, void* stream) {
 }
 
 extern "C" int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v, const int32_t* step,
-                             const float* lr, float beta1, float beta2, float eps, float weight_decay, void* p_lowp,
+                             const float* lr, double beta1, double beta2, float eps, float weight_decay, void* p_lowp,
                              void* stream) {
   if (n <= 0) return VAE_OK;
   if (!p || !g || !m || !v || !step || !lr) return fail(VAE_E_BADARG, "adam_step: null");
@@ -664,4 +668,61 @@ extern "C" int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* st
   hipLaunchKernelGGL(step_begin_kernel, dim3(grid_for(n16 > 0 ? n16 : 1)), dim3(256), 0, (hipStream_t)stream,
                      (f32x4*)zero, n16, (unsigned char*)zero + n16 * 16, ntail, (int*)step);
   return check_launch("step_begin");
+}
+
+// ------------------------------------------------------------------ swapped-axes weight copies
+// dst[b][t][a] = bf16(src[a][t][b]) for up to VAE_SWAP_MAX tensors in one launch: the k-contiguous
+// B operands of the bf16 ConvTranspose2d forward / Conv2d data-gradient GEMMs (vaehip.h wt_t),
+// refreshed from the fp32 master right after the optimizer step.  One workgroup = one 32x32
+// (a, b) tile of one tap through a padded LDS tile (both sides 64-byte segments).
+namespace {
+struct SwapBatch {
+  vae_swap_desc d[VAE_SWAP_MAX];
+  int tiles0[VAE_SWAP_MAX + 1];      // first workgroup of each descriptor
+  int count;
+};
+
+__global__ void __launch_bounds__(256) swap_axes_kernel(const SwapBatch sb) {
+  __shared__ float t[32][33];
+  int i = 0;
+  while (i + 1 < sb.count && (int)blockIdx.x >= sb.tiles0[i + 1]) ++i;
+  const vae_swap_desc d = sb.d[i];
+  int blk = blockIdx.x - sb.tiles0[i];
+  const int nb = (d.b + 31) / 32, na = (d.a + 31) / 32;
+  const int bt = blk % nb; blk /= nb;
+  const int at = blk % na;
+  const int tap = blk / na;
+  const int a0 = at * 32, b0 = bt * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* src = static_cast<const float*>(d.src);
+  __bf16* dst = static_cast<__bf16*>(d.dst);
+  for (int j = ty; j < 32; j += 8) {
+    const int a = a0 + j, b = b0 + tx;
+    t[j][tx] = (a < d.a && b < d.b) ? src[((long)a * d.rs + tap) * d.b + b] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int b = b0 + j, a = a0 + tx;
+    if (a < d.a && b < d.b) dst[((long)b * d.rs + tap) * d.a + a] = (__bf16)t[tx][j];
+  }
+}
+}  // namespace
+
+extern "C" int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* stream) {
+  if (count <= 0) return VAE_OK;
+  if (count > VAE_SWAP_MAX || !descs) return fail(VAE_E_BADARG, "swap_axes: count %d (max %d)", count, VAE_SWAP_MAX);
+  SwapBatch sb;
+  memset(&sb, 0, sizeof(sb));
+  int tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    const vae_swap_desc& d = descs[i];
+    if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0) return fail(VAE_E_BADARG, "swap_axes: descriptor %d", i);
+    sb.d[i] = d;
+    sb.tiles0[i] = tiles;
+    tiles += ((d.a + 31) / 32) * ((d.b + 31) / 32) * d.rs;
+  }
+  sb.tiles0[count] = tiles;
+  sb.count = count;
+  hipLaunchKernelGGL(swap_axes_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, sb);
+  return check_launch("swap_axes");
 }

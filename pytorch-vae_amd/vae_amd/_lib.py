@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -53,7 +53,7 @@ class ConvArgs(ctypes.Structure):
                 ("dy", c_void_p), ("dy_xf", Xform), ("dx", c_void_p), ("dx_epi", Xform),
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
                 ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
-                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p)]
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("wt_t", c_void_p)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -100,6 +100,12 @@ class ReconArgs(ctypes.Structure):
                 ("grad_scale", c_float), ("grad_recon", c_void_p), ("ld", c_int32)]
 
 
+class SwapDesc(ctypes.Structure):
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("a", c_int32), ("rs", c_int32), ("b", c_int32)]
+
+
+SWAP_MAX = 16
+
 # name -> (argtypes)
 _SIGS = {
     "vae_abi_version": [],
@@ -124,10 +130,11 @@ _SIGS = {
     "vae_vq_bwd": [POINTER(VqArgs), c_void_p],
     "vae_recon_fwd": [POINTER(ReconArgs), c_void_p],
     "vae_recon_bwd": [POINTER(ReconArgs), c_void_p],
-    "vae_adam_step": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_float,
-                      c_float, c_float, c_void_p, c_void_p],
+    "vae_adam_step": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_double,
+                      ctypes.c_double, c_float, c_float, c_void_p, c_void_p],
     "vae_cast_bf16": [c_int64, c_void_p, c_void_p, c_void_p],
     "vae_step_begin": [c_void_p, c_int64, c_void_p, c_void_p],
+    "vae_swap_axes": [c_int32, c_void_p, c_void_p],
     "vae_nchw_to_nhwc_pad": [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vae_pad_channels": [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vae_unpad_accumulate": [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],

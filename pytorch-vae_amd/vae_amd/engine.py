@@ -40,6 +40,8 @@ class FusedAdam:
                self.v.data_ptr(), self.step.data_ptr(), self.lr.data_ptr(), self.betas[0], self.betas[1], self.eps,
                self.weight_decay, net.lowp.data_ptr() if net.lowp is not None else None,
                stream if stream is not None else L.stream_ptr())
+        if getattr(net, "swap_descs", None) is not None:
+            net.refresh_swaps(stream)
 
 
 class TrainStep:
@@ -61,7 +63,13 @@ class TrainStep:
         self.segments = []                      # (call range) of the backward per bucket
         if self.world > 1:
             self.buckets = plan_buckets(plan.bwd_calls, plan.grads, net.layout, nbuckets)
-            self.comm = BucketedAllReduce(plan.grads, self.buckets, process_group)
+            # the last bucket also carries the loss terms (plan.metrics sits right after the
+            # gradients): their rank mean is the reference's log_dict(sync_dist=True) at no extra
+            # collective (experiment.py:55)
+            e, s, _ = self.buckets[-1]
+            mo = plan.metrics.data_ptr() - plan.zero.data_ptr()
+            self.buckets[-1] = (e, s, mo // 4 + plan.metrics.numel())
+            self.comm = BucketedAllReduce(plan.zero, self.buckets, process_group)
         else:
             self.buckets = [(len(plan.bwd_calls), 0, plan.grads.numel())]
             self.comm = None
@@ -79,6 +87,8 @@ class TrainStep:
             if p.loss_kind == L.LOSS_BETA_B:
                 p.num_iter.add_(1.0)
             p.forward(st)
+            if self.world > 1:
+                p.metrics.copy_(p.out)
         lo = 0 if k == 0 else self.buckets[k - 1][0]
         p._run(p.bwd_calls[lo:self.buckets[k][0]], st)
 
@@ -134,3 +144,8 @@ class TrainStep:
         else:
             self._opt()
         self.net.num_batches_tracked += 1
+
+    def loss_terms(self):
+        """[loss, Reconstruction_Loss, KLD|VQ_Loss] of the last step: the mean over ranks with more
+        than one (what the reference logs, experiment.py:55), else this rank's."""
+        return (self.plan.metrics if self.world > 1 else self.plan.out)[:3].tolist()

@@ -97,7 +97,8 @@ class VAEXperiment:
                                             'recon': recon[i:i + 1].detach().cpu(), 'name': names[i]}
 
     def validation_step(self, batch, batch_idx, optimizer_idx=0):
-        """experiment.py:122-132 (the models run train-mode BatchNorm)."""
+        """experiment.py:122-132.  Lightning calls it with the model in eval mode (BatchNorm on the
+        running statistics, nothing updated); fit() below does the same."""
         imgs, labels, _ = batch
         self.curr_device = imgs.device
         with torch.no_grad():
@@ -164,9 +165,16 @@ def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=No
             optims[0].step()
             acc()
         if val_batches is not None:
-            for i, batch in enumerate(val_batches):
-                experiment.validation_step(batch, i)
-                acc()
+            was_training = getattr(experiment.model, "training", True)
+            if hasattr(experiment.model, "eval"):
+                experiment.model.eval()            # Lightning's validation loop: model.eval()
+            try:
+                for i, batch in enumerate(val_batches):
+                    experiment.validation_step(batch, i)
+                    acc()
+            finally:
+                if was_training and hasattr(experiment.model, "train"):
+                    experiment.model.train()
         rec = {k: float(v) / cnt[k] for k, v in sums.items()}
         for s in sched:
             s["scheduler"].step()

@@ -59,9 +59,27 @@ class VAENet:
         self.lowp = (torch.zeros(self.layout.total, dtype=torch.bfloat16, device=self.device)
                      if dtype == torch.bfloat16 else None)
         self.num_batches_tracked = 0
+        self._init_swaps()
         self.sync_lowp()
 
     # ------------------------------------------------------------------ state
+    def _init_swaps(self):
+        """bf16 mode: swapped-axes copies (vaehip.h wt_t) of the weights the bf16 GEMMs read
+        transposed — every ConvTranspose2d (its forward) and every Conv2d with a data gradient
+        (encoder blocks 1..) — refreshed with the bf16 copy (sync_lowp / FusedAdam.apply)."""
+        self.wt_t: Dict[str, int] = {}
+        self.swap_descs = None
+        if self.lowp is None:
+            return
+        names = ([f"encoder.{i}.0.weight" for i in range(1, len(self.hidden_dims))] +
+                 [f"decoder.{i}.0.weight" for i in range(len(self.hidden_dims) - 1)] + ["final_layer.0.weight"])
+        self.swap_descs, self.lowp_t = make_swaps(self.layout, self.params, names, self.device, self.wt_t)
+
+    def refresh_swaps(self, stream=None):
+        if self.swap_descs is not None:
+            L.call("vae_swap_axes", len(self.swap_descs), ctypes.byref(self.swap_descs),
+                   stream if stream is not None else L.stream_ptr())
+
     @property
     def dcode(self) -> int:
         return L.dtype_code(self.dtype)
@@ -70,6 +88,7 @@ class VAENet:
         """Refresh the bf16 weight copy from the fp32 master (bf16 mode only)."""
         if self.lowp is not None:
             L.call("vae_cast_bf16", self.params.numel(), self.params.data_ptr(), self.lowp.data_ptr(), L.stream_ptr())
+            self.refresh_swaps()
 
     def load_reference_state_dict(self, sd: Dict[str, torch.Tensor]):
         self.layout.load_reference(self.params, self.running, {k: v.to(self.device) for k, v in sd.items()})
@@ -174,11 +193,14 @@ class StepPlan:
         # BatchNorm has forward sums (Σ, Σ²) and backward sums (Σg·x̂, Σg), each kept in
         # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
         nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
-        nz = (net.layout.total + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns)) +
+        nz = (_pad4(net.layout.total) + 4 + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns)) +
               _pad4(h[0] * 9 * 8))
         self.zero = torch.zeros(nz, **f32)
         o = 0
-        self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
+        self.grads = self.zero[o:o + net.layout.total]; o += _pad4(net.layout.total)
+        # loss terms averaged over ranks (experiment.py:55 log_dict(sync_dist=True)): copied from
+        # `out` after the forward and reduced together with the last gradient bucket (engine.py)
+        self.metrics = self.zero[o:o + 4]; o += 4
         self.bnfwd: Dict[str, torch.Tensor] = {}     # [2][reps][C]: Σ(y-shift), Σ(y-shift)²
         self.bnbwd: Dict[str, torch.Tensor] = {}     # [2][reps][C]: Σg·x̂ (dγ), Σg (dβ)
         for b in net.layout.bns:
@@ -380,6 +402,7 @@ class StepPlan:
             if prev_pre is not None:
                 a.x_xf = self.bn_xf(prev_pre, L.X_BN_ACT, cnt(prev), running=True)
             a.wt = net.w(dec_w[i] + ".weight")
+            a.wt_t = net.wt_t.get(dec_w[i] + ".weight")
             a.bias = net.p(dec_w[i] + ".bias")
             a.y = dec_out[i].data_ptr()
             if self.training:
@@ -523,6 +546,7 @@ class StepPlan:
                 a.dy = self.g_enc[i].data_ptr()
                 a.dy_xf = dy_xf
                 a.wt = net.w(f"encoder.{i}.0.weight")
+                a.wt_t = net.wt_t.get(f"encoder.{i}.0.weight")
                 a.dx = self.g_enc[i - 1].data_ptr()
                 a.dx_epi = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]), aux=self.enc[i - 1])
                 self.bwd_sums(a, enc_pre[i - 1])
@@ -592,6 +616,28 @@ def call_one(fn, arg, stream):
         L.call(fn, *arg, stream)
     else:
         L.call(fn, arg, stream)
+
+
+def make_swaps(layout: Layout, params: torch.Tensor, names, device, out: Dict[str, int]):
+    """Descriptor array for vae_swap_axes over the named conv / convT weights (native
+    [a][r][s][b] -> bf16 [b][r][s][a]) and the bf16 buffer holding the copies; `out` maps
+    each name to its copy's device pointer."""
+    specs = [layout.by_name[n] for n in names if n in layout.by_name]
+    if len(specs) > L.SWAP_MAX:
+        raise ValueError(f"{len(specs)} swapped weights > {L.SWAP_MAX} per vae_swap_axes launch")
+    sizes = [(s.numel + 63) // 64 * 64 for s in specs]
+    buf = torch.zeros(max(1, sum(sizes)), dtype=torch.bfloat16, device=device)
+    descs = (L.SwapDesc * len(specs))()
+    o = 0
+    for i, (spec, n) in enumerate(zip(specs, sizes)):
+        a, r, r2, b = spec.native_shape
+        d = descs[i]
+        d.src = params.data_ptr() + 4 * spec.offset
+        d.dst = buf.data_ptr() + 2 * o
+        d.a, d.rs, d.b = a, r * r2, b
+        out[spec.name] = d.dst
+        o += n
+    return descs, buf
 
 
 def bn_reps(channels: int) -> int:

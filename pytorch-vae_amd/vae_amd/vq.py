@@ -159,10 +159,11 @@ class VQStepPlan:
         self.g_lat = torch.empty_like(self.latpre)
         self.g_enc = [torch.empty_like(t) for t in self.enc]
         npad = (h[0] * 16 * 8 + r_[-1] * 16 * 8 + 8) if self.pad_rgb else 0
-        nz = net.layout.total + _pad4(B) + 4 + npad
+        nz = _pad4(net.layout.total) + 4 + _pad4(B) + 4 + npad
         self.zero = torch.zeros(nz, **f32)
         o = 0
-        self.grads = self.zero[o:o + net.layout.total]; o += net.layout.total
+        self.grads = self.zero[o:o + net.layout.total]; o += _pad4(net.layout.total)
+        self.metrics = self.zero[o:o + 4]; o += 4                  # rank-averaged loss terms (engine.py)
         self.sse = self.zero[o:o + B]; o += _pad4(B)
         self.vq_sse = self.zero[o:o + 1]; o += 4
         if self.pad_rgb:                                            # padded weight gradients

@@ -97,3 +97,31 @@ def test_fit_steps_and_exponential_lr():
     assert len(hist) == 2 and 'val_loss' in hist[0] and 'loss' in hist[0]
     assert any(not torch.equal(a, b) for a, b in zip(before, m.parameters()))
     assert hist[1]['loss'] < hist[0]['loss']
+
+
+class TinyBN(TinyAE):
+    """TinyAE with a BatchNorm on the code (running statistics change only in train mode)."""
+
+    def __init__(self):
+        super().__init__()
+        self.bn = nn.BatchNorm1d(16)
+        self.modes = []
+
+    def forward(self, x, **kwargs):
+        self.modes.append(self.training)
+        h = self.bn(self.enc(x.flatten(1)))
+        return [torch.tanh(self.dec(h)).view_as(x), x, h]
+
+
+def test_fit_validates_in_eval_mode():
+    """Lightning's validation loop runs the model under eval(): BatchNorm uses its running
+    statistics and does not update them (the reference's val_loss, experiment.py:122-132)."""
+    m = TinyBN()
+    exp = VAEXperiment(m, dict(PARAMS))
+    fit(exp, [_batch(0)], epochs=1)
+    rm, rv = m.bn.running_mean.clone(), m.bn.running_var.clone()
+    m.modes.clear()
+    fit(exp, [], epochs=1, val_batches=[_batch(5), _batch(6)])
+    assert m.modes == [False, False]
+    assert torch.equal(rm, m.bn.running_mean) and torch.equal(rv, m.bn.running_var)
+    assert m.training                           # back in train mode afterwards
