@@ -58,9 +58,10 @@ def parse():
     ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae", "vq"],
                     help="vq: BASELINE.json configs[4], VQ-VAE B=128 (pass --batch 128)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--concurrent", action="store_true",
-                    help="weight gradients on a side stream beside the data-gradient chain (measured slower "
-                         "for VanillaVAE: 0.88 vs 0.77 ms, the graph's per-call fork/join edges)")
+    ap.add_argument("--concurrent", choices=["auto", "on", "off"], default="auto",
+                    help="weight gradients on a side stream beside the data-gradient chain; auto = on for "
+                         "VQ-VAE (r1: 9.96 -> 8.51 ms), off for the VanillaVAE family (measured 0.88 vs 0.77 ms: "
+                         "the graph's per-call fork/join edges cost more than the overlap gains)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernel-breakdown", action="store_true", help="print per-kernel times to stderr")
@@ -350,14 +351,14 @@ def main():
     if args.arch == "vq":
         from vae_amd.vq import VQNet, VQStepPlan
         net = VQNet(dtype=dtype, device="cuda", generator=gen)
-        plan = VQStepPlan(net, args.batch, concurrent=args.concurrent)
+        plan = VQStepPlan(net, args.batch, concurrent=args.concurrent != "off")
         opt = FusedAdam(net, lr=0.005)                             # configs/vae/vq_vae.yaml LR
     else:
         net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
         loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
         kld = {"vanilla": 1e-8, "betaH": 2.5e-4, "iwae": 2.5e-4}[args.arch]
         lr = {"vanilla": 0.005, "betaH": 0.005, "iwae": 0.007}[args.arch]
-        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S, concurrent=args.concurrent)
+        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S, concurrent=args.concurrent == "on")
         opt = FusedAdam(net, lr=lr)
     # synthetic data resident in HBM (per-rank seed 1265+rank): U[0,1) images, N(0,1) eps
     g = torch.Generator(device="cuda").manual_seed(1265 + rank)
