@@ -102,7 +102,9 @@ template <int BM, int BN, int BK> struct CgSmem {
   static constexpr int BYTES = LOOP > EPI ? LOOP : EPI;
 };
 
-template <int BM, int BN, int BK, int AM, int XA, int EM>
+// OR ("one round"): every workgroup's K slice fits the register ring (host-checked), so the
+// prologue requests all of it and the loop never refills.
+template <int BM, int BN, int BK, int AM, int XA, int EM, bool OR>
 __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
   using WG = CgWaves<BM, BN>;
   constexpr int TM = WG::TM, TN = WG::TN, WTM = TM * 16, WTN = TN * 16;
@@ -239,7 +241,11 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
   }
   Stage ring[NS];
 #pragma unroll
-  for (int u = 0; u < NS; ++u) issue(kt0 + u, ring[u]);
+  for (int u = 0; u < NS; ++u) {
+    // one round: only the slice's own steps (the first store then waits for all of them — they
+    // were requested together); ring mode: every slot, so vmcnt stays exact across the loop
+    if (!OR || kt0 + u < kt1) issue(kt0 + u, ring[u]);
+  }
   if (a_tab) {
     const int C = p.a_xf.channels;
 #pragma unroll
@@ -317,16 +323,27 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
   // step kt+NS (loads past the K range read zeros through the buffer resource)
   // (loads are issued on every path, so the compiler's vmcnt bookkeeping stays exact across
   // the loop back-edge; only the LDS work of steps past the slice's end is skipped)
-  int buf = 0;
-  for (int kb = kt0; kb < kt1; kb += NS) {
+  if constexpr (OR) {
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
-      const bool live = kb + u < kt1;
-      if (live) store(buf, ring[u]);
-      __syncthreads();
-      issue(kb + u + NS, ring[u]);
-      if (live) compute(buf);
-      buf ^= 1;
+      if (kt0 + u < kt1) {
+        store(u & 1, ring[u]);
+        __syncthreads();
+        compute(u & 1);
+      }
+    }
+  } else {
+    int buf = 0;
+    for (int kb = kt0; kb < kt1; kb += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const bool live = kb + u < kt1;
+        if (live) store(buf, ring[u]);
+        __syncthreads();
+        issue(kb + u + NS, ring[u]);
+        if (live) compute(buf);
+        buf ^= 1;
+      }
     }
   }
   // probe marks: 1 = K loop done, 2 = epilogue loads landed, 3 = end
@@ -339,6 +356,23 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
 #endif
 
   // ------------------------------------------------------------------ epilogue through LDS
+  // E_STORE statistics straight from the accumulators (rows outside M accumulated zeros): lane
+  // holds rows 4g..4g+3 of column l&15 of each fragment -> 2 butterfly steps per column fragment
+  __shared__ float fpart[CgWaves<BM, BN>::WM][2][BN];
+  const bool frag_sums = EM == E_STORE && p.sum != nullptr && p.slab == nullptr;
+  if (frag_sums) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { a1 += acc[i][j][e]; a2 = fmaf(acc[i][j][e], acc[i][j][e], a2); }
+      a1 += __shfl_xor(a1, 16); a2 += __shfl_xor(a2, 16);
+      a1 += __shfl_xor(a1, 32); a2 += __shfl_xor(a2, 32);
+      if (lane < 16) { fpart[wm][0][wn * WTN + j * 16 + lane] = a1; fpart[wm][1][wn * WTN + j * 16 + lane] = a2; }
+    }
+  }
   __syncthreads();                                   // every wave is done with the K tiles
   float* Cs = reinterpret_cast<float*>(smem);        // [BM][BN+4]
   constexpr int LDC = BN + 4;
@@ -433,9 +467,7 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
       for (int e = 0; e < 8; ++e) {
         float y = v[e] + bias[e];
         if (has_res) y += ract ? lrelu(ax[e], p.res_xf.slope) : ax[e];
-        o[e] = y;
-        s1[e] = fmaf(w, v[e], s1[e]);
-        s2[e] = fmaf(w * v[e], v[e], s2[e]);
+        o[e] = y;                                  // (statistics: fpart, from the accumulators)
       }
     } else {
       const int ek = p.epi_xf.kind;
@@ -463,7 +495,16 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
       pp[e] = *reinterpret_cast<uint32_t*>(&h);
     }
   }
-  if (epi_wants_sums<EM>(p)) {
+  if (frag_sums) {
+    for (int c = tid; c < BN; c += 256) {
+      if (n0 + c < p.N) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < CgWaves<BM, BN>::WM; ++w) { t1 += fpart[w][0][c]; t2 += fpart[w][1][c]; }
+        epi_flush_sums<EM>(p, (int)blockIdx.x, n0 + c, t1, t2);
+      }
+    }
+  } else if (EM == E_BNBWD && epi_wants_sums<EM>(p)) {
     // lanes l, l+EC, l+2EC, ... of a wave hold the same 8 columns: butterfly over the lane
     // bits above EC, then one partial per wave and column in LDS (no atomics), summed in wave order
     float* part = Cs;                                // [4 waves][2][BN] (Cs was read above)

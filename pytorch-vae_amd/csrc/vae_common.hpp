@@ -222,4 +222,106 @@ __device__ __forceinline__ void bn_finalize_block(const vae_bn_args& a, int cg0,
   }
 }
 
+// ---------------------------------------------------------------- per-channel transform tables
+// Views into LDS, sized by the real channel count of each transform (rounded up to 4 so vector
+// reads of 4 consecutive channels stay 16-byte aligned):
+//   BN_ACT: v = lrelu(t*a + b)   BN_DY: v = a*t + b*aux + c   epilogue BN_ACT: x̂ = y*p + q
+struct Tab {
+  float *a, *b, *c, *p, *q;
+};
+
+__host__ __device__ inline int tab_pad(int c) { return (c + 3) & ~3; }
+// Each table row is followed by 8 zero entries (the "zero slot" at index tab_pad(C)): a packed
+// group that is out of range points its channel there, so any transform maps it to exactly 0.
+__host__ __device__ inline int tab_stride(int c) { return tab_pad(c) + 8; }
+
+// A BatchNorm table built by the consuming workgroup from the producer's replicated statistics
+// (no vae_bn_finalize launch): all 256 threads call it in uniform control flow.  Every replica
+// element is loaded in one round (reps * C <= 1024 per statistic, C dividing 256 or a multiple
+// of it: host-checked, bn_fast_ok), partials meet in LDS and are summed in a fixed order, so
+// every workgroup of every consumer derives bit-identical coefficients.
+__host__ __device__ inline bool bn_fast_ok(const vae_xform& x) {
+  const int C = x.channels, R = x.reps > 1 ? x.reps : 1;
+  if (C <= 0 || R * C > 1024 || (x.reps > 1 && x.rstride < C)) return false;
+  return C <= 256 ? (256 % C == 0) : (C % 256 == 0);
+}
+
+__device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, bool update_running) {
+  __shared__ float scr[4][256];
+  const int C = x.channels, R = x.reps > 1 ? x.reps : 1, tid = threadIdx.x;
+  const long rs = x.reps > 1 ? x.rstride : 0;
+  const bool dy = x.kind == VAE_X_BN_DY;
+  const int total = R * C;
+  float v[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int f = tid + 256 * k;
+    const bool ok = f < total;
+    const int r = ok ? f / C : 0, c = ok ? f - r * C : 0;
+    const long o = (long)r * rs + c;
+    v[0][k] = ok ? x.sum[o] : 0.f;
+    v[1][k] = ok ? x.sumsq[o] : 0.f;
+    v[2][k] = (ok && dy) ? x.dgamma[o] : 0.f;
+    v[3][k] = (ok && dy) ? x.dbeta[o] : 0.f;
+  }
+  // channel totals: C <= 256 -> every element of a thread is channel tid % C; C = 256k -> the
+  // thread's elements are channels tid + 256j, each complete after summing its replicas
+  float tot[2][4];
+  int nch = 1;
+  if (C <= 256) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) scr[a][tid] = (v[a][0] + v[a][1]) + (v[a][2] + v[a][3]);
+    __syncthreads();
+    if (tid < C) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        float acc = 0.f;
+        for (int j = tid; j < 256; j += C) acc += scr[a][j];
+        tot[0][a] = acc;
+      }
+    }
+    __syncthreads();                            // scr is free for the next table of this workgroup
+    nch = tid < C ? 1 : 0;
+  } else {
+    const int per = C / 256;                    // channels per thread (2 for C = 512)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc += ((k % per) == j && k / per < R) ? v[a][k] : 0.f;
+        tot[j][a] = acc;
+      }
+    nch = per;
+  }
+  for (int j = 0; j < nch && j < 2; ++j) {
+    const int ch = C <= 256 ? tid : tid + 256 * j;
+    const float inv_m = 1.0f / x.count;
+    const float s1 = tot[j][0] * inv_m;
+    const float var = fmaxf(tot[j][1] * inv_m - s1 * s1, 0.0f);
+    const float mean = s1 + (x.shift ? x.shift[ch] : 0.0f);
+    const float invstd = 1.0f / sqrtf(var + x.eps);
+    const float g = x.gamma[ch];
+    if (x.kind == VAE_X_BN_ACT) {
+      const float sc = g * invstd;
+      t.a[ch] = sc;
+      t.b[ch] = x.beta[ch] - mean * sc;
+      if (epi) { t.p[ch] = invstd; t.q[ch] = -mean * invstd; }
+      if (update_running && x.running_mean) {
+        const float m = x.momentum;
+        const float unb = x.count > 1.f ? var * x.count / (x.count - 1.f) : var;
+        x.running_mean[ch] = (1.f - m) * x.running_mean[ch] + m * mean;
+        x.running_var[ch] = (1.f - m) * x.running_var[ch] + m * unb;
+      }
+    } else {
+      const float A = g * invstd;
+      const float mg = tot[j][3] * inv_m, mgx = tot[j][2] * inv_m;
+      t.a[ch] = A;
+      t.b[ch] = -A * invstd * mgx;
+      t.c[ch] = -A * (mg - mean * invstd * mgx);
+    }
+  }
+}
+
 }  // namespace vae

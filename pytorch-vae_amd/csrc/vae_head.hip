@@ -66,7 +66,13 @@ __device__ __forceinline__ int act_off(int trow, int tcol, int chunk) {
 __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
 
 // Per-channel BN coefficients in LDS (from vae_bn_finalize's table when present).
-__device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq) {
+// Without a precomputed table the workgroup reduces the producer's replicated statistics itself
+// (tab_build; `update_running`: this workgroup also applies the running-statistic update).
+__device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq, bool update_running = false) {
+  if (xf.kind == VAE_X_BN_ACT && !xf.table && xf.channels == HC && bn_fast_ok(xf)) {
+    tab_build(xf, Tab{ta, tb, nullptr, tp, tq}, true, update_running);
+    return;
+  }
   for (int c = threadIdx.x; c < HC; c += blockDim.x) {
     if (xf.kind != VAE_X_BN_ACT) { ta[c] = 1.f; tb[c] = 0.f; tp[c] = 0.f; tq[c] = 0.f; continue; }
     if (xf.table) {
@@ -148,7 +154,7 @@ __global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
   // fragments cost ~72 vector-memory instructions per wave)
   for (int i = threadIdx.x; i < NCO * 9 * HC; i += 256) wsh[i] = q.wt[i];
   const float bco = co < NCO ? q.bias[co] : 0.f;
-  head_tables(q.xf, ta, tb, tp, tq);
+  head_tables(q.xf, ta, tb, tp, tq, blockIdx.x == 0);
   __syncthreads();
   tile_store(q, h0, raw, tile, ta, tb);
   // B fragments: W[co = lane&15][tap][8*(lane>>4) .. +7] (zero for co >= 3)

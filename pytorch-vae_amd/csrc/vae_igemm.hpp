@@ -140,18 +140,8 @@ __device__ __forceinline__ PhaseInfo make_phase(const GemmParams& p, int phase) 
 }
 
 // ------------------------------------------------------------------ per-channel tables
-// Views into dynamic LDS, sized by the real channel count of each transform (rounded up to 4
-// so vector reads of 4 consecutive channels stay 16-byte aligned):
-//   BN_ACT: v = lrelu(t*a + b)   BN_DY: v = a*t + b*aux + c   epilogue BN_ACT: x̂ = y*p + q
-struct Tab {
-  float *a, *b, *c, *p, *q;
-};
-
-__host__ __device__ inline int tab_pad(int c) { return (c + 3) & ~3; }
-// Each table row is followed by 8 zero entries (the "zero slot" at index tab_pad(C)): a packed
-// group that is out of range points its channel there, so any transform maps it to exactly 0.
-__host__ __device__ inline int tab_stride(int c) { return tab_pad(c) + 8; }
-
+// Fill a transform table (vae_common.hpp Tab): a copy of vae_bn_finalize's precomputed table, or
+// built by this workgroup from the producer's replicated statistics (tab_build).
 __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bool update_running) {
   if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return;
   if (threadIdx.x < 8) {
@@ -171,6 +161,10 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
       if (dy) t.c[ch] = v2;
       else if (epi) { t.p[ch] = v2; t.q[ch] = v3; }
     }
+    return;
+  }
+  if (blockDim.x == 256 && bn_fast_ok(x)) {
+    tab_build(x, t, epi, update_running);
     return;
   }
   for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {

@@ -474,10 +474,12 @@ struct CgTile { int bm, bn; };
 // Largest tile that still gives every CU ~2 workgroups; split-K (slabs + igemm_finalize) when
 // even the smallest leaves the chip half empty and K is deep.
 inline CgTile cg_pick(long M, long N, int nphase) {
-  const CgTile c[] = {{128, 128}, {64, 64}, {64, 32}, {32, 64}, {32, 32}};
+  const CgTile c[] = {{128, 128}, {128, 32}, {64, 64}, {64, 32}, {32, 64}, {32, 32}};
   for (const CgTile& t : c) {
     if (t.bm > 32 && M < t.bm) continue;
     if (t.bn > 32 && N < t.bn) continue;
+    // 128 x 32 only for the long thin maps (>= 8 workgroups per CU at 64 x 32)
+    if (t.bm == 128 && t.bn == 32 && tile_blocks(M, N, nphase, Tile{64, 32}) < 8 * kCUs) continue;
     if (tile_blocks(M, N, nphase, Tile{t.bm, t.bn}) >= 2 * kCUs) return t;
   }
   return CgTile{32, 32};
@@ -485,17 +487,18 @@ inline CgTile cg_pick(long M, long N, int nphase) {
 
 template <int BM, int BN> constexpr int cg_bk() { return BM >= 128 ? 64 : 128; }
 
-template <int AM, int XA, int EM>
+template <int AM, int XA, int EM, bool OR>
 inline void cg_launch_tile(const GemmParams& p, CgTile t, hipStream_t st) {
   const size_t lds = (size_t)((XA == VAE_X_BN_ACT || XA == VAE_X_BN_DY ? 3 * tab_stride(p.a_xf.channels) : 0) +
                               (EM == E_BNBWD ? 4 * tab_stride(p.epi_xf.channels) : 0)) * 4;
 #define VAE_CG_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
     const unsigned nb = (unsigned)(((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.nphase * p.ksplit); \
-    hipLaunchKernelGGL((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM>), dim3(nb), dim3(256), lds, st, p); \
+    hipLaunchKernelGGL((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM, OR>), dim3(nb), dim3(256), lds, st, p); \
     return; \
   }
   VAE_CG_CASE(128, 128)
+  VAE_CG_CASE(128, 32)
   VAE_CG_CASE(64, 64)
   VAE_CG_CASE(64, 32)
   VAE_CG_CASE(32, 64)
@@ -539,16 +542,25 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   if (split > 1 && (!ws || (long)split * p.M * p.N * p.nphase * 4 > ws_bytes)) split = 1;
   p.ksplit = split < 1 ? 1 : split;
   p.slab = p.ksplit > 1 ? static_cast<float*>(ws) : nullptr;
+  // one-round kernels when every slice's K-steps fit the ring of the chosen instantiation
+  const int kps = (ktiles + p.ksplit - 1) / p.ksplit;
+  const bool dy = p.a_xf.kind == VAE_X_BN_DY;
+  const int KCt = bk / 8, RPPt = 256 / KCt;
+  const int loads = ((t.bm + RPPt - 1) / RPPt) * (dy ? 2 : 1) + (t.bn + RPPt - 1) / RPPt;
+  const int ns = 20 / loads < 2 ? 2 : (20 / loads > 8 ? 8 : 20 / loads);   // == cg_stages<loads>()
+  const bool one = kps <= ns;
+#define VAE_CG_XA(XA_) (one ? cg_launch_tile<AM, XA_, EM, true>(p, t, st) : cg_launch_tile<AM, XA_, EM, false>(p, t, st))
   switch (p.a_xf.kind) {
-    case VAE_X_NONE: cg_launch_tile<AM, VAE_X_NONE, EM>(p, t, st); break;
-    case VAE_X_ACT: cg_launch_tile<AM, VAE_X_ACT, EM>(p, t, st); break;
+    case VAE_X_NONE: VAE_CG_XA(VAE_X_NONE); break;
+    case VAE_X_ACT: VAE_CG_XA(VAE_X_ACT); break;
     case VAE_X_BN_ACT:
-      if constexpr (EM == E_STORE) cg_launch_tile<AM, VAE_X_BN_ACT, EM>(p, t, st);
+      if constexpr (EM == E_STORE) VAE_CG_XA(VAE_X_BN_ACT);
       break;
     case VAE_X_BN_DY:
-      if constexpr (EM == E_BNBWD) cg_launch_tile<AM, VAE_X_BN_DY, EM>(p, t, st);
+      if constexpr (EM == E_BNBWD) VAE_CG_XA(VAE_X_BN_DY);
       break;
   }
+#undef VAE_CG_XA
   int rc = check_launch("cgemm");
   if (rc) return rc;
   if (p.slab) return launch_finalize<__bf16, EM>(p, st);

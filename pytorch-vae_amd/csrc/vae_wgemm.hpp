@@ -1,0 +1,526 @@
+// bf16 weight-gradient GEMM of the conv / transposed-conv layers for every tile size.
+//
+//   dW[m][r][s][j] += Σ_{n,hu,wu} U'[n,hu,wu,m] · V'[n, hu*S-P+r, wu*S-P+s, j]
+//
+//   Conv2d bwd_filter:          U = dy (output grid), V = x  (input grid);  m = k,  j = c
+//   ConvTranspose2d bwd_filter: U = x  (input grid),  V = dy (output grid); m = c,  j = k
+//   (U', V' = the stored tensors with their per-channel transforms, template parameters XU / XV.)
+//
+// Both operands are NHWC with the reduction index (pixels) outermost: every pixel row goes
+// global -> registers -> (transform) -> LDS as whole 16-byte chunks in its natural
+// [pixel][channel] order, and the MFMA operand fragments are read back column-major with
+// ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 of a 4x16
+// block; lane i receives column i) — the K = pixel direction needs no transposing store.
+//
+// Why beside vae_wgrad.hpp's 128x128 kernel: the VanillaVAE layers have 32-512 channels and
+// 256-65536 pixels, so one tile size cannot fill the chip; here BM x BJ is 32x32 .. 128x128,
+// the pixel range is split over workgroups until ~2 per CU, the register ring keeps ~20 loads
+// in flight (one memory round trip per workgroup for most layers, tools/kprobe.py), the
+// BatchNorm tables are built in-kernel from the producers' replicated statistics, and the
+// first workgroup publishes dL/dgamma, dL/dbeta and the closed-form conv-bias gradient of the
+// BatchNorm whose backward it applies (vae_bn_finalize mode 1's work).
+//
+// LDS rows: 64 B (BM 32), 160 B (64), 288 B (128): the four 32-byte row segments a 16-lane
+// transposed read touches fall in distinct bank groups.
+#pragma once
+#include "vae_cgemm.hpp"
+
+namespace vae {
+
+struct WgParams {
+  const void* u; vae_xform u_xf; uint32_t u_bytes;   // [n][hu][wu][M]
+  const void* v; vae_xform v_xf; uint32_t v_bytes;   // [n][hv][wv][J]
+  int n, hu, wu, M;
+  int hv, wv, J;
+  int R, S, P;
+  int kper;                          // pixels per K slice (multiple of 32)
+  float* dw;                         // [M][R][R][J] fp32, accumulated
+  float* db;                         // closed-form bias gradient (first workgroup; with u/v BN_DY extras)
+  int dy_is_v;                       // which operand carries the BN_DY transform (bias gradient of its conv)
+  FastDiv fd_wu, fd_hu, fd_r;
+};
+
+template <int BM> constexpr int wg_rs() { return BM == 32 ? 64 : (BM == 64 ? 160 : 288); }
+
+typedef __bf16 __attribute__((ext_vector_type(4))) __attribute__((address_space(3))) wgm_lds_bf16x4;
+typedef __bf16 wgm_bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ wgm_bf16x4 wgm_tr_read(const char* generic_lds_addr) {
+  const uint32_t off = (uint32_t)(uintptr_t)generic_lds_addr;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((wgm_lds_bf16x4*)(uintptr_t)off);
+}
+
+template <int BM, int BJ, int XU, int XV>
+__global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
+  constexpr int KP = 32;                               // pixels per K-step
+  constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
+  constexpr int CU = BM / 8, CV = BJ / 8;              // 16-byte chunks per pixel row
+  constexpr int RPU = 256 / CU, RPV = 256 / CV;        // pixel rows per pass
+  constexpr int UPT = RPU >= KP ? 1 : KP / RPU, VPT = RPV >= KP ? 1 : KP / RPV;
+  constexpr bool DU = XU == VAE_X_BN_DY, DV = XV == VAE_X_BN_DY;
+  constexpr bool BU = XU == VAE_X_BN_ACT || DU, BV = XV == VAE_X_BN_ACT || DV;
+  constexpr int LOADS = UPT * (DU ? 2 : 1) + VPT * (DV ? 2 : 1);
+  constexpr int NS = cg_stages<LOADS>();
+  constexpr int WTM = BM / 2, WTJ = BJ / 2;            // 2 x 2 waves
+  constexpr int TM = WTM / 16, TJ = WTJ / 16;
+
+  __shared__ __attribute__((aligned(16))) char Us[2][KP * RSU];
+  __shared__ __attribute__((aligned(16))) char Vs[2][KP * RSV];
+  extern __shared__ float tabs[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int gm = (p.M + BM - 1) / BM, gj = (p.J + BJ - 1) / BJ;
+  const int per_slice = gm * gj * p.R * p.R;
+  const int slice = blockIdx.x / per_slice;
+  int t = blockIdx.x - slice * per_slice;
+  const int tj = t % gj; t /= gj;
+  const int tmi = t % gm;
+  const int tap = t / gm;
+  const int r = (int)p.fd_r.div(tap), s = tap - r * p.R;
+  const int m0 = tmi * BM, j0 = tj * BJ;
+  const long npix = (long)p.n * p.hu * p.wu;
+  const long k0 = (long)slice * p.kper;
+  const long k1 = min(npix, k0 + p.kper);
+  const int nsteps = (int)((k1 - k0 + KP - 1) / KP);
+
+  // per-thread chunk coordinates (all of a thread's rows share the chunk column)
+  const int cu = tid % CU, ru0 = tid / CU, cv = tid % CV, rv0 = tid / CV;
+  const int chu = m0 + cu * 8, chv = j0 + cv * 8;
+  const bool cu_ok = chu < p.M && ru0 < KP, cv_ok = chv < p.J && rv0 < KP;
+  const Src<__bf16> su = make_src<__bf16>(p.u, p.u_bytes, p.u_xf);
+  const Src<__bf16> sv = make_src<__bf16>(p.v, p.v_bytes, p.v_xf);
+
+  struct Stage {
+    uint32_t u[UPT][4], uy[DU ? UPT : 1][4];
+    uint32_t v[VPT][4], vy[DV ? VPT : 1][4];
+    uint32_t oku, okv;
+  };
+  auto issue = [&](int step, Stage& st) {
+    const long kb = k0 + (long)step * KP;
+    uint32_t oku = 0u, okv = 0u;
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const long pix = kb + ru0 + i * RPU;
+      const bool in = cu_ok && pix < k1;
+      oku |= (uint32_t)in << i;
+      const uint32_t off = in ? (uint32_t)((pix * p.M + chu) * 2) : kOOB;
+      bload<16>(su.x, off, st.u[i]);
+      if constexpr (DU) bload<16>(su.y, off, st.uy[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const long pix = kb + rv0 + i * RPV;
+      const bool in = cv_ok && pix < k1;
+      const uint32_t pp = in ? (uint32_t)pix : 0u;
+      const uint32_t q = p.fd_wu.div(pp);
+      const int wu_i = (int)(pp - q * (uint32_t)p.wu);
+      const uint32_t nn = p.fd_hu.div(q);
+      const int hu_i = (int)(q - nn * (uint32_t)p.hu);
+      const int hv_i = hu_i * p.S - p.P + r, wv_i = wu_i * p.S - p.P + s;
+      const bool vin = in && (uint32_t)hv_i < (uint32_t)p.hv && (uint32_t)wv_i < (uint32_t)p.wv;
+      okv |= (uint32_t)vin << i;
+      const uint32_t off = vin ? (uint32_t)(((((long)nn * p.hv + hv_i) * p.wv + wv_i) * p.J + chv) * 2) : kOOB;
+      bload<16>(sv.x, off, st.v[i]);
+      if constexpr (DV) bload<16>(sv.y, off, st.vy[i]);
+    }
+    st.oku = oku; st.okv = okv;
+  };
+
+  // tables: U transform [3][stride_u], V transform [3][stride_v]
+  const int cau = tab_stride(p.u_xf.channels), cav = tab_stride(p.v_xf.channels);
+  const Tab tu{tabs, tabs + cau, tabs + 2 * cau, nullptr, nullptr};
+  float* q0 = tabs + (BU ? 3 * cau : 0);
+  const Tab tv{q0, q0 + cav, q0 + 2 * cav, nullptr, nullptr};
+
+  Stage ring[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) issue(u, ring[u]);
+  if constexpr (BU) tab_fill(p.u_xf, tu, false, false);
+  if constexpr (BV) tab_fill(p.v_xf, tv, false, false);
+  if (blockIdx.x == 0) {
+    // the BatchNorm whose backward this call applies: dL/dgamma, dL/dbeta (+ conv bias) once
+    const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
+    if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
+  }
+  __syncthreads();
+
+  f32x4 acc[TM][TJ];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto store = [&](int buf, const Stage& st) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int row = ru0 + i * RPU;
+      if (row < KP) {
+        uint4 w;
+        if constexpr (XU == VAE_X_NONE) {
+          w = uint4{st.u[i][0], st.u[i][1], st.u[i][2], st.u[i][3]};
+        } else {
+          const int ch = ((st.oku >> i) & 1u) ? chu : su.zs;   // out of range -> 0 after the transform
+          w = cg_xform<XU>(st.u[i], st.uy[DU ? i : 0], tu, ch, su.slope);
+        }
+        *reinterpret_cast<uint4*>(Us[buf] + row * RSU + cu * 16) = w;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int row = rv0 + i * RPV;
+      if (row < KP) {
+        uint4 w;
+        if constexpr (XV == VAE_X_NONE) {
+          w = uint4{st.v[i][0], st.v[i][1], st.v[i][2], st.v[i][3]};
+        } else {
+          const int ch = ((st.okv >> i) & 1u) ? chv : sv.zs;
+          w = cg_xform<XV>(st.v[i], st.vy[DV ? i : 0], tv, ch, sv.slope);
+        }
+        *reinterpret_cast<uint4*>(Vs[buf] + row * RSV + cv * 16) = w;
+      }
+    }
+  };
+  // transposed-read addresses: lane 4q+p of 16-lane group g reads pixel rows 8g+4h+q, channels
+  // c0 + 4p .. +3 of the fragment's 16 (byte offsets within a buffer)
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  int aoff[TM][2], boff[TJ][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) aoff[i][h] = row * RSU + (wm * WTM + i * 16 + 4 * p4) * 2;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) boff[j][h] = row * RSV + (wn * WTJ + j * 16 + 4 * p4) * 2;
+  }
+  auto compute = [&](int buf) {
+    bf16x8 af[TM], bfr[TJ];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const wgm_bf16x4 a0 = wgm_tr_read(Us[buf] + aoff[i][0]), a1 = wgm_tr_read(Us[buf] + aoff[i][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+    }
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const wgm_bf16x4 b0 = wgm_tr_read(Vs[buf] + boff[j][0]), b1 = wgm_tr_read(Vs[buf] + boff[j][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bfr[j][e] = b0[e]; bfr[j][4 + e] = b1[e]; }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  };
+
+  // main loop (vae_cgemm.hpp: loads issued on every path, LDS work skipped past the slice)
+  int buf = 0;
+  for (int kb = 0; kb < nsteps; kb += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const bool live = kb + u < nsteps;
+      if (live) store(buf, ring[u]);
+      __syncthreads();
+      issue(kb + u + NS, ring[u]);
+      if (live) compute(buf);
+      buf ^= 1;
+    }
+  }
+  // D[m][j]: lane holds rows 4g + e of fragment i, column li of fragment j
+  const long rowstride = (long)p.R * p.R * p.J;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int jj = j0 + wn * WTJ + j * 16 + li;
+      if (jj >= p.J) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int mm = m0 + wm * WTM + i * 16 + 4 * g + e;
+        if (mm < p.M) atomicAdd(p.dw + mm * rowstride + (long)tap * p.J + jj, acc[i][j][e]);
+      }
+    }
+}
+
+// All R x R taps in one workgroup (small tiles): the U tile of a K-step is loaded and
+// transformed once and reused by every tap (per-tap workgroups did it R*R times), V is gathered
+// per tap from the pixel decomposition computed once per row.  Accumulators: R*R x the
+// (BM/2 x BJ/2) wave tile.
+template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : cg_stages<LOADS>(); }
+
+template <int BM, int BJ, int XU, int XV, int RR>
+__global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
+  constexpr int TAPS = RR * RR;
+  constexpr int KP = 32;
+  constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
+  constexpr int CU = BM / 8, CV = BJ / 8;
+  constexpr int RPU = 256 / CU, RPV = 256 / CV;
+  constexpr int UPT = RPU >= KP ? 1 : KP / RPU, VPT = RPV >= KP ? 1 : KP / RPV;
+  constexpr bool DU = XU == VAE_X_BN_DY, DV = XV == VAE_X_BN_DY;
+  constexpr bool BU = XU == VAE_X_BN_ACT || DU, BV = XV == VAE_X_BN_ACT || DV;
+  constexpr int LOADS = UPT * (DU ? 2 : 1) + TAPS * VPT * (DV ? 2 : 1);
+  constexpr int NS = wgt_stages<LOADS>();
+  constexpr int WTM = BM / 2, WTJ = BJ / 2;
+  constexpr int TM = WTM / 16, TJ = WTJ / 16;
+
+  __shared__ __attribute__((aligned(16))) char Us[2][KP * RSU];
+  __shared__ __attribute__((aligned(16))) char Vs[2][TAPS][KP * RSV];
+  extern __shared__ float tabs[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int gm = (p.M + BM - 1) / BM, gj = (p.J + BJ - 1) / BJ;
+  const int per_slice = gm * gj;
+  const int slice = blockIdx.x / per_slice;
+  const int t0 = blockIdx.x - slice * per_slice;
+  const int tj = t0 % gj, tmi = t0 / gj;
+  const int m0 = tmi * BM, j0 = tj * BJ;
+  const long npix = (long)p.n * p.hu * p.wu;
+  const long k0 = (long)slice * p.kper;
+  const long k1 = min(npix, k0 + p.kper);
+  const int nsteps = (int)((k1 - k0 + KP - 1) / KP);
+
+  const int cu = tid % CU, ru0 = tid / CU, cv = tid % CV, rv0 = tid / CV;
+  const int chu = m0 + cu * 8, chv = j0 + cv * 8;
+  const bool cu_ok = chu < p.M && ru0 < KP, cv_ok = chv < p.J && rv0 < KP;
+  const Src<__bf16> su = make_src<__bf16>(p.u, p.u_bytes, p.u_xf);
+  const Src<__bf16> sv = make_src<__bf16>(p.v, p.v_bytes, p.v_xf);
+
+  struct Stage {
+    uint32_t u[UPT][4], uy[DU ? UPT : 1][4];
+    uint32_t v[TAPS][VPT][4], vy[DV ? TAPS : 1][DV ? VPT : 1][4];
+    uint32_t oku, okv[TAPS];
+  };
+  auto issue = [&](int step, Stage& st) {
+    const long kb = k0 + (long)step * KP;
+    uint32_t oku = 0u;
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const long pix = kb + ru0 + i * RPU;
+      const bool in = cu_ok && pix < k1;
+      oku |= (uint32_t)in << i;
+      const uint32_t off = in ? (uint32_t)((pix * p.M + chu) * 2) : kOOB;
+      bload<16>(su.x, off, st.u[i]);
+      if constexpr (DU) bload<16>(su.y, off, st.uy[i]);
+    }
+    st.oku = oku;
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) st.okv[t] = 0u;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const long pix = kb + rv0 + i * RPV;
+      const bool in = cv_ok && pix < k1;
+      const uint32_t pp = in ? (uint32_t)pix : 0u;
+      const uint32_t q = p.fd_wu.div(pp);
+      const int wu_i = (int)(pp - q * (uint32_t)p.wu);
+      const uint32_t nn = p.fd_hu.div(q);
+      const int hu_i = (int)(q - nn * (uint32_t)p.hu);
+      const int hb = hu_i * p.S - p.P, wb = wu_i * p.S - p.P;
+      const long nbase = (long)nn * p.hv;
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        const int hv_i = hb + t / RR, wv_i = wb + t % RR;
+        const bool vin = in && (uint32_t)hv_i < (uint32_t)p.hv && (uint32_t)wv_i < (uint32_t)p.wv;
+        st.okv[t] |= (uint32_t)vin << i;
+        const uint32_t off = vin ? (uint32_t)((((nbase + hv_i) * p.wv + wv_i) * p.J + chv) * 2) : kOOB;
+        bload<16>(sv.x, off, st.v[t][i]);
+        if constexpr (DV) bload<16>(sv.y, off, st.vy[t][i]);
+      }
+    }
+  };
+
+  const int cau = tab_stride(p.u_xf.channels), cav = tab_stride(p.v_xf.channels);
+  const Tab tu{tabs, tabs + cau, tabs + 2 * cau, nullptr, nullptr};
+  float* q0 = tabs + (BU ? 3 * cau : 0);
+  const Tab tv{q0, q0 + cav, q0 + 2 * cav, nullptr, nullptr};
+
+  Stage ring[NS];
+#pragma unroll
+  for (int u = 0; u < NS; ++u) issue(u, ring[u]);
+  if constexpr (BU) tab_fill(p.u_xf, tu, false, false);
+  if constexpr (BV) tab_fill(p.v_xf, tv, false, false);
+  if (blockIdx.x == 0) {
+    const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
+    if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
+  }
+  __syncthreads();
+
+  f32x4 acc[TAPS][TM][TJ];
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto store = [&](int buf, const Stage& st) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int row = ru0 + i * RPU;
+      if (row < KP) {
+        uint4 w;
+        if constexpr (XU == VAE_X_NONE) {
+          w = uint4{st.u[i][0], st.u[i][1], st.u[i][2], st.u[i][3]};
+        } else {
+          const int ch = ((st.oku >> i) & 1u) ? chu : su.zs;
+          w = cg_xform<XU>(st.u[i], st.uy[DU ? i : 0], tu, ch, su.slope);
+        }
+        *reinterpret_cast<uint4*>(Us[buf] + row * RSU + cu * 16) = w;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int row = rv0 + i * RPV;
+        if (row < KP) {
+          uint4 w;
+          if constexpr (XV == VAE_X_NONE) {
+            w = uint4{st.v[t][i][0], st.v[t][i][1], st.v[t][i][2], st.v[t][i][3]};
+          } else {
+            const int ch = ((st.okv[t] >> i) & 1u) ? chv : sv.zs;
+            w = cg_xform<XV>(st.v[t][i], st.vy[DV ? t : 0][DV ? i : 0], tv, ch, sv.slope);
+          }
+          *reinterpret_cast<uint4*>(Vs[buf][t] + row * RSV + cv * 16) = w;
+        }
+      }
+  };
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  int aoff[TM][2], boff[TJ][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q4;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) aoff[i][h] = row * RSU + (wm * WTM + i * 16 + 4 * p4) * 2;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) boff[j][h] = row * RSV + (wn * WTJ + j * 16 + 4 * p4) * 2;
+  }
+  auto compute = [&](int buf) {
+    bf16x8 af[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const wgm_bf16x4 a0 = wgm_tr_read(Us[buf] + aoff[i][0]), a1 = wgm_tr_read(Us[buf] + aoff[i][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+    }
+#pragma unroll
+    for (int t = 0; t < TAPS; ++t) {
+      bf16x8 bfr[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const wgm_bf16x4 b0 = wgm_tr_read(Vs[buf][t] + boff[j][0]), b1 = wgm_tr_read(Vs[buf][t] + boff[j][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bfr[j][e] = b0[e]; bfr[j][4 + e] = b1[e]; }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+    }
+  };
+
+  int buf = 0;
+  for (int kb = 0; kb < nsteps; kb += NS) {
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+      const bool live = kb + u < nsteps;
+      if (live) store(buf, ring[u]);
+      __syncthreads();
+      issue(kb + u + NS, ring[u]);
+      if (live) compute(buf);
+      buf ^= 1;
+    }
+  }
+  const long rowstride = (long)TAPS * p.J;
+#pragma unroll
+  for (int t = 0; t < TAPS; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int jj = j0 + wn * WTJ + j * 16 + li;
+        if (jj >= p.J) continue;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int mm = m0 + wm * WTM + i * 16 + 4 * g + e;
+          if (mm < p.M) atomicAdd(p.dw + mm * rowstride + (long)t * p.J + jj, acc[t][i][j][e]);
+        }
+      }
+}
+
+// ------------------------------------------------------------------ host
+inline bool wg2_ok(int dtype, const vae_xform& ux, const vae_xform& vx, long u_elems, long v_elems, int M, int J,
+                   const void* u, const void* v) {
+  if (dtype != VAE_BF16 || getenv("VAE_NO_WGEMM")) return false;
+  if (M % 8 || J % 8) return false;
+  if (u_elems * 2 >= (1l << 31) || v_elems * 2 >= (1l << 31)) return false;
+  if (((uintptr_t)u & 15) || ((uintptr_t)v & 15)) return false;
+  auto ok = [](const vae_xform& x) {
+    if (x.kind == VAE_X_BN_DY && ((uintptr_t)x.aux & 15)) return false;
+    if (x.kind == VAE_X_BN_ACT || x.kind == VAE_X_BN_DY) return x.channels <= MAXC;
+    return true;
+  };
+  return ok(ux) && ok(vx);
+}
+
+template <int BM, int BJ, int XU, int XV>
+inline void wg2_launch_k(const WgParams& p, unsigned blocks, hipStream_t st) {
+  const bool bu = XU == VAE_X_BN_ACT || XU == VAE_X_BN_DY, bv = XV == VAE_X_BN_ACT || XV == VAE_X_BN_DY;
+  const size_t lds = (size_t)((bu ? 3 * tab_stride(p.u_xf.channels) : 0) + (bv ? 3 * tab_stride(p.v_xf.channels) : 0)) * 4;
+  if constexpr (BM == 32) {
+    // 32 x 32 tiles of 3x3 kernels: every tap in one workgroup (the grid was sized without the
+    // tap factor); larger tiles / kernels would exceed the LDS and register budget
+    if (p.R == 3) { hipLaunchKernelGGL((wgemm_taps_kernel<BM, BJ, XU, XV, 3>), dim3(blocks), dim3(256), lds, st, p); return; }
+  }
+  hipLaunchKernelGGL((wgemm_kernel<BM, BJ, XU, XV>), dim3(blocks), dim3(256), lds, st, p);
+}
+
+template <int BM, int BJ, int XU>
+inline void wg2_launch_v(const WgParams& p, unsigned blocks, hipStream_t st) {
+  switch (p.v_xf.kind) {
+    case VAE_X_NONE: wg2_launch_k<BM, BJ, XU, VAE_X_NONE>(p, blocks, st); break;
+    case VAE_X_ACT: wg2_launch_k<BM, BJ, XU, VAE_X_ACT>(p, blocks, st); break;
+    case VAE_X_BN_ACT: wg2_launch_k<BM, BJ, XU, VAE_X_BN_ACT>(p, blocks, st); break;
+    default: wg2_launch_k<BM, BJ, XU, VAE_X_BN_DY>(p, blocks, st); break;
+  }
+}
+
+template <int BM, int BJ>
+inline void wg2_launch_u(const WgParams& p, unsigned blocks, hipStream_t st) {
+  switch (p.u_xf.kind) {
+    case VAE_X_NONE: wg2_launch_v<BM, BJ, VAE_X_NONE>(p, blocks, st); break;
+    case VAE_X_ACT: wg2_launch_v<BM, BJ, VAE_X_ACT>(p, blocks, st); break;
+    case VAE_X_BN_ACT: wg2_launch_v<BM, BJ, VAE_X_BN_ACT>(p, blocks, st); break;
+    default: wg2_launch_v<BM, BJ, VAE_X_BN_DY>(p, blocks, st); break;
+  }
+}
+
+inline int wg2_launch(WgParams p, hipStream_t st) {
+  p.fd_wu = make_fastdiv(p.wu);
+  p.fd_hu = make_fastdiv(p.hu);
+  p.fd_r = make_fastdiv(p.R);
+  const long npix = (long)p.n * p.hu * p.wu;
+  p.u_bytes = (uint32_t)(npix * p.M * 2);
+  p.v_bytes = (uint32_t)((long)p.n * p.hv * p.wv * p.J * 2);
+  // tile: square, the largest whose both sides fit the channel counts
+  const int mn = p.M < p.J ? p.M : p.J;
+  const int T = mn >= 128 ? 128 : (mn >= 64 ? 64 : 32);
+  const bool taps_in_block = T == 32 && p.R == 3;
+  const long tiles = (long)((p.M + T - 1) / T) * ((p.J + T - 1) / T) * (taps_in_block ? 1 : p.R * p.R);
+  const long ksteps = (npix + 31) / 32;
+  // K slices: ~2 workgroups per CU, >= 4 K-steps per slice
+  long split = (2 * kCUs + tiles - 1) / tiles;
+  if (split > ksteps / 4) split = ksteps / 4;
+  if (split < 1) split = 1;
+  p.kper = (int)(((ksteps + split - 1) / split) * 32);
+  split = (npix + p.kper - 1) / p.kper;
+  const unsigned blocks = (unsigned)(tiles * split);
+  if (T == 128) wg2_launch_u<128, 128>(p, blocks, st);
+  else if (T == 64) wg2_launch_u<64, 64>(p, blocks, st);
+  else wg2_launch_u<32, 32>(p, blocks, st);
+  return check_launch("wgemm");
+}
+
+}  // namespace vae

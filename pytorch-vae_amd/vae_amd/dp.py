@@ -32,12 +32,13 @@ def _written_grad_ptrs(arg) -> List[int]:
             v = getattr(arg, f)
             if v:
                 out.append(int(v))
-    xf = getattr(arg, "xf", None)            # vae_bn_args (mode 1): dγ, dβ outputs
-    if xf is not None:
-        for f in _XF_GRAD_FIELDS:
-            v = getattr(xf, f)
-            if v:
-                out.append(int(v))
+    for name in ("xf", "dy_xf"):             # vae_bn_args (mode 1) / a weight-gradient call's
+        xf = getattr(arg, name, None)        # BN_DY transform: dγ, dβ outputs
+        if xf is not None:
+            for f in _XF_GRAD_FIELDS:
+                v = getattr(xf, f)
+                if v:
+                    out.append(int(v))
     fin = getattr(arg, "bn_finalize", None)  # a BatchNorm finalisation fused into this call
     if fin:
         out += _written_grad_ptrs(fin.contents)

@@ -131,7 +131,7 @@ class StepPlan:
     def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
                  capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
-                 concurrent: bool = False, fuse_bn: bool = False):
+                 concurrent: bool = False, fuse_bn: bool = False, bn_in_consumer: bool = True):
         self.net = net
         self.B = batch
         # training=False: eval-mode BatchNorm (running statistics, nothing updated; the
@@ -142,6 +142,12 @@ class StepPlan:
         # recon/mu/log_var and the backward is seeded with dL/drecon (grad_recon) and
         # dL/d[mu|log_var] (written into dmulv) instead.
         self.fused_loss = fused_loss
+        # bn_in_consumer: no vae_bn_finalize launches in training — every kernel that applies a
+        # BatchNorm reduces the producer's replicated statistics itself (vae_common.hpp
+        # tab_build); the forward consumer's first workgroup updates the running statistics and
+        # the weight-gradient call's first workgroup writes dL/dgamma, dL/dbeta and the conv
+        # bias gradient (closed form).  Eval mode keeps vae_bn_finalize (running statistics).
+        self.bn_in_consumer = bn_in_consumer and training
         self.S = samples if loss == "iwae" else 1
         self.loss_kind = {"vanilla": L.LOSS_VANILLA, "betaH": L.LOSS_BETA_H, "betaB": L.LOSS_BETA_B,
                           "iwae": L.LOSS_IWAE}[loss]
@@ -240,7 +246,9 @@ class StepPlan:
         return prefix[:-2] + ".0.bias"          # "encoder.3.1" -> "encoder.3.0.bias"
 
     def bn_xf(self, prefix: str, kind: int, count: int, aux=None, running: bool = False,
-              table: bool = True) -> L.Xform:
+              table: Optional[bool] = None) -> L.Xform:
+        if table is None:
+            table = not self.bn_in_consumer
         net = self.net
         C = net.layout.bn_by_prefix[prefix].channels
         s = self.bnfwd[prefix]
@@ -277,10 +285,24 @@ class StepPlan:
         arg.dx_dgamma, arg.dx_dbeta = s[0].data_ptr(), s[1].data_ptr()
         arg.sum_reps, arg.sum_rstride = s.shape[1], s.shape[2]
 
+    def bwd_extras(self, arg, prefix: str):
+        """bn_in_consumer: the weight-gradient call of the conv feeding BatchNorm `prefix` also
+        publishes that BatchNorm's dL/dgamma, dL/dbeta and the conv's bias gradient (what
+        vae_bn_finalize mode 1 did)."""
+        if not self.bn_in_consumer:
+            return
+        xf = arg.dy_xf
+        xf.dgamma_out = self.g(prefix + ".weight")
+        xf.dbeta_out = self.g(prefix + ".bias")
+        arg.dy_xf = xf
+        arg.db = self.g(self._bn_prod_bias(prefix))
+
     def bn_finalize(self, lst, prefix: str, mode: int, count: int):
         """Queue vae_bn_finalize for one BatchNorm: mode 0 after the conv producing its input
         (table + running statistics), mode 1 after the kernel producing its backward sums
         (table + dγ, dβ + the producing conv's bias gradient in closed form)."""
+        if self.bn_in_consumer and mode in (0, 1):
+            return
         C = self.net.layout.bn_by_prefix[prefix].channels
         a = L.BnArgs(mode=mode)
         a.xf = self.bn_xf(prefix, L.X_BN_DY if mode == 1 else L.X_BN_ACT, count, running=(mode != 1), table=False)
@@ -483,7 +505,8 @@ class StepPlan:
                 f.x_xf = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t))
             f.dy = g_dec_out[i].data_ptr()
             f.dy_xf = dy_xf
-            f.dw = self.g(dec_w[i] + ".weight")      # bias gradient: closed form in vae_bn_finalize
+            f.dw = self.g(dec_w[i] + ".weight")      # bias gradient: closed form (bn_finalize / bwd_extras)
+            self.bwd_extras(f, dec_pre[i])
             self._add(Bw, "vae_convT2d_bwd_filter", f)
         # decoder_input: dz -> d[mu|logvar] (reparameterization + KL), and its weight grads
         a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
@@ -537,7 +560,8 @@ class StepPlan:
                 f.x = self.enc[i - 1].data_ptr()
                 f.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]))
             if not (i == 0 and self.pad_rgb):
-                f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form in vae_bn_finalize
+                f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form (bn_finalize / bwd_extras)
+            self.bwd_extras(f, enc_pre[i])
             self._add(Bw, "vae_conv2d_bwd_filter", f)
             if i == 0 and self.pad_rgb:
                 Bw.append(("vae_unpad_accumulate", (h[0] * 9, 8, 3, self.dw8.data_ptr(), self.g("encoder.0.0.weight"))))
@@ -642,9 +666,10 @@ def make_swaps(layout: Layout, params: torch.Tensor, names, device, out: Dict[st
 
 def bn_reps(channels: int) -> int:
     """Replicas of a BatchNorm's statistics: enough that the ~1000 workgroups of a producing
-    kernel add into each address only a few dozen times, few enough that a consumer block
-    reads at most ~8K floats to reduce them."""
-    return max(1, min(32, 4096 // max(1, channels)))
+    kernel do not all add into the same 2*C addresses, few enough (reps*C <= 256: one element per
+    thread per statistic) that every consuming workgroup reduces them in one round of loads
+    (vae_common.hpp tab_build) — thousands of consumer workgroups re-read them."""
+    return max(1, min(32, 256 // max(1, channels)))
 
 
 def _pad4(n: int) -> int:

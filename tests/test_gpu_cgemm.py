@@ -257,3 +257,173 @@ DGRAD_T = [  # N, cin, cout, hw (input of the transposed conv), stride, R, pad
 def test_cgemm_convT2d_bwd_data(shape):
     L = _L()
     run_dgrad(True, *shape, L.X_BN_DY if shape[5] == 3 else L.X_NONE, L.X_BN_ACT if shape[5] == 3 else L.X_ACT)
+
+
+# ---------------------------------------------------------------------------------------------
+# Weight gradients (csrc/vae_wgemm.hpp) with the BatchNorm coefficients built in-kernel from
+# the statistics (no precomputed table: vae_common.hpp tab_build), plus the closed-form conv
+# bias gradient and dL/dgamma, dL/dbeta published by the first workgroup.
+
+class BN:
+    """A stored pre-BN tensor with consistent statistics (reps=1 sums over N*H*W, shift = the
+    producing conv's bias) as the producing kernels leave them."""
+
+    def __init__(self, y, g, shift=None):
+        C = y.shape[1]
+        self.y = y
+        self.gamma = 0.7 + 0.6 * torch.rand(C, generator=g)
+        self.beta = (torch.rand(C, generator=g) - 0.5) * 0.2
+        self.shift = shift if shift is not None else torch.zeros(C)
+        d = (y - self.shift.view(1, -1, 1, 1)).double()
+        self.sum = d.sum((0, 2, 3)).float()
+        self.sumsq = (d * d).sum((0, 2, 3)).float()
+        self.count = y.numel() // C
+        self.keep = []
+
+    def xf(self, L, kind, aux_dev=None, dgamma=None, dbeta=None, dgamma_out=None, dbeta_out=None):
+        C = self.gamma.numel()
+        x = L.Xform(kind=kind, channels=C, slope=SLOPE, count=float(self.count), eps=1e-5, momentum=0.1)
+        for name in ("sum", "sumsq", "shift", "gamma", "beta"):
+            t = getattr(self, name).float().cuda()
+            self.keep.append(t)
+            setattr(x, name, t.data_ptr())
+        x.reps, x.rstride = 1, C
+        if dgamma is not None:
+            for name, t in (("dgamma", dgamma), ("dbeta", dbeta)):
+                t = t.float().cuda()
+                self.keep.append(t)
+                setattr(x, name, t.data_ptr())
+        if dgamma_out is not None:
+            x.dgamma_out, x.dbeta_out = dgamma_out.data_ptr(), dbeta_out.data_ptr()
+        if aux_dev is not None:
+            x.aux = aux_dev.data_ptr()
+        return x
+
+    def act(self):
+        z = F.batch_norm(self.y.double(), None, None, self.gamma.double(), self.beta.double(), True, 0.1, 1e-5)
+        return bf(F.leaky_relu(z, SLOPE).float())
+
+
+def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed=3):
+    L = _L()
+    g = torch.Generator().manual_seed(seed)
+    if transposed:
+        P = (hw - 1) * stride - 2 * pad + R + (stride - 1 if R == 3 else 0)
+        wshape = (cin, cout, R, R)
+    else:
+        P = (hw + 2 * pad - R) // stride + 1
+        wshape = (cout, cin, R, R)
+    xst = bf(torch.randn(N, cin, hw, hw, generator=g) * 1.3 + 0.2)
+    yst = bf(torch.randn(N, cout, P, P, generator=g) * 1.1 - 0.1)      # pre-BN output (BN_DY aux)
+    gst = bf(torch.randn(N, cout, P, P, generator=g))                   # dL/dz of its BatchNorm
+    bnx = BN(xst, g)
+    bny = BN(yst, g, shift=torch.randn(cout, generator=g) * 0.1)
+    # operands as the kernel forms them
+    if x_kind == L.X_BN_ACT:
+        act = bnx.act()
+    elif x_kind == L.X_ACT:
+        act = bf(F.leaky_relu(xst, SLOPE))
+    else:
+        act = xst
+    if dy_kind == L.X_BN_DY:
+        yv = yst.double().requires_grad_(True)
+        z = F.batch_norm(yv, None, None, bny.gamma.double(), bny.beta.double(), True, 0.1, 1e-5)
+        z.backward(gst.double())
+        dyp = bf(yv.grad.float())
+        db_exact = yv.grad.sum((0, 2, 3))          # ~0: a train-mode BatchNorm's input gradient sums to 0
+        xh = ((yst.double() - yst.double().mean((0, 2, 3), keepdim=True)) /
+              torch.sqrt(yst.double().var((0, 2, 3), unbiased=False, keepdim=True) + 1e-5))
+        dgam, dbet = (gst.double() * xh).sum((0, 2, 3)), gst.double().sum((0, 2, 3))
+    else:
+        dyp, dgam, dbet = gst, None, None
+    w0 = torch.zeros(wshape, dtype=torch.float64, requires_grad=True)
+    if transposed:
+        out = F.conv_transpose2d(act.double(), w0, None, stride=stride, padding=pad,
+                                 output_padding=(stride - 1 if R == 3 else 0))
+    else:
+        out = F.conv2d(act.double(), w0, None, stride=stride, padding=pad)
+    out.backward(dyp.double())
+    want = w0.grad.permute(0, 2, 3, 1)                                 # native [a][r][s][b]
+    xd, yd, gd = nhwc(xst), nhwc(yst), nhwc(gst)
+    dw = torch.zeros(want.shape, device="cuda")
+    db = torch.zeros(cout, device="cuda")
+    dgo = torch.zeros(cout, device="cuda"); dbo = torch.zeros(cout, device="cuda")
+    a = L.ConvArgs(dtype=L.BF16, n=N, h=hw, w=hw, c=cin, k=cout, p=P, q=P, r=R, stride=stride, pad=pad)
+    a.x = xd.data_ptr(); a.x_xf = bnx.xf(L, x_kind) if x_kind == L.X_BN_ACT else L.Xform(kind=x_kind, channels=cin, slope=SLOPE)
+    a.dy = gd.data_ptr()
+    if dy_kind == L.X_BN_DY:
+        a.dy_xf = bny.xf(L, L.X_BN_DY, aux_dev=yd, dgamma=dgam, dbeta=dbet, dgamma_out=dgo, dbeta_out=dbo)
+        a.db = db.data_ptr()
+    a.dw = dw.data_ptr()
+    L.call("vae_convT2d_bwd_filter" if transposed else "vae_conv2d_bwd_filter", ctypes.byref(a),
+           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert relmax(dw.cpu(), want) < 2e-3
+    if dy_kind == L.X_BN_DY:
+        # closed form A*Σg + B*Σy + C*M (vaehip.h bn_args): exact up to fp32 cancellation
+        assert float((db.cpu().double() - db_exact).abs().max()) < 1e-6 * float(dyp.double().abs().sum((0, 2, 3)).max())
+        assert relmax(dgo.cpu(), dgam) < 1e-5 and relmax(dbo.cpu(), dbet) < 1e-5
+
+
+WGRAD = [  # N, cin, cout, hw (conv input), stride, R, pad
+    (8, 32, 64, 32, 2, 3, 1),
+    (8, 64, 128, 16, 2, 3, 1),
+    (8, 256, 512, 4, 2, 3, 1),
+    (8, 8, 32, 64, 2, 3, 1),             # padded-RGB first layer (x untransformed)
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD)
+def test_wgemm_conv2d_bn(shape):
+    L = _L()
+    run_wgrad(False, *shape, L.X_NONE if shape[1] == 8 else L.X_BN_ACT, L.X_BN_DY)
+
+
+def test_wgemm_conv2d_vq_shapes():
+    L = _L()
+    run_wgrad(False, 4, 256, 256, 16, 1, 3, 1, L.X_ACT, L.X_NONE)
+    run_wgrad(False, 4, 128, 256, 32, 2, 4, 1, L.X_ACT, L.X_NONE)
+
+
+WGRAD_T = [  # N, cin, cout, hw (convT input), stride, R, pad
+    (8, 512, 256, 2, 2, 3, 1),
+    (8, 128, 64, 8, 2, 3, 1),
+    (8, 32, 32, 32, 2, 3, 1),
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_T)
+def test_wgemm_convT2d_bn(shape):
+    L = _L()
+    run_wgrad(True, *shape, L.X_BN_ACT, L.X_BN_DY)
+
+
+def test_wgemm_convT2d_vq_shape():
+    L = _L()
+    run_wgrad(True, 4, 256, 128, 16, 2, 4, 1, L.X_ACT, L.X_NONE)
+
+
+def test_cgemm_fwd_table_built_in_kernel():
+    """Forward conv with BN_ACT from the raw statistics (no table): tab_build + running stats."""
+    L = _L()
+    g = torch.Generator().manual_seed(9)
+    N, cin, cout, hw = 8, 64, 128, 16
+    y = bf(torch.randn(N, cin, hw, hw, generator=g) * 0.9 + 0.4)
+    bn = BN(y, g, shift=torch.randn(cin, generator=g) * 0.05)
+    w = bf(torch.randn(cout, cin, 3, 3, generator=g) * 0.1)
+    ref = F.conv2d(bn.act().double(), w.double(), None, stride=2, padding=1)
+    out = torch.empty(N, hw // 2, hw // 2, cout, device="cuda", dtype=torch.bfloat16)
+    rm = torch.zeros(cin, device="cuda"); rv = torch.ones(cin, device="cuda")
+    xf = bn.xf(L, L.X_BN_ACT)
+    xf.running_mean, xf.running_var = rm.data_ptr(), rv.data_ptr()
+    yd = nhwc(y)
+    wd = w.permute(0, 2, 3, 1).contiguous().to("cuda", torch.bfloat16)
+    a = L.ConvArgs(dtype=L.BF16, n=N, h=hw, w=hw, c=cin, k=cout, p=hw // 2, q=hw // 2, r=3, stride=2, pad=1)
+    a.x = yd.data_ptr(); a.x_xf = xf; a.wt = wd.data_ptr(); a.y = out.data_ptr()
+    L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert relmax(nchw(out), ref) < OUT_TOL
+    mean = y.double().mean((0, 2, 3))
+    var_u = y.double().var((0, 2, 3), unbiased=True)
+    assert relmax(rm.cpu(), 0.1 * mean) < 1e-4
+    assert relmax(rv.cpu() - 0.9, 0.1 * var_u) < 1e-4
