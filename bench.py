@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64, help="per-GPU batch")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in path leg (model.forward + "
+                    "loss_function + backward + torch.optim.Adam through VAEXperiment.training_step)")
     ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae", "vq"],
                     help="vq: BASELINE.json configs[4], VQ-VAE B=128 (pass --batch 128)")
     ap.add_argument("--no-graph", action="store_true")
@@ -315,6 +317,48 @@ def selftest(args, distributed):
         dist.destroy_process_group()
 
 
+def dropin_leg(args, dtype, steps=None, warmup=3):
+    """The drop-in path a reference user runs (run.py -> VAEXperiment.training_step): the BaseVAE
+    model's forward, loss_function (vae_elbo_fwd on the GPU), loss.backward() (the fused HIP
+    backward behind autograd) and torch.optim.Adam on the flat parameter — eager, no graphs —
+    timed like the headline (same batch, synchronised region).  Returns its img/s."""
+    from vae_amd.experiment import VAEXperiment
+    from vae_amd.models import vae_models
+    arch = {"vanilla": ("VanillaVAE", {}), "betaH": ("BetaVAE", {"loss_type": "H", "beta": 4}),
+            "iwae": ("IWAE", {"num_samples": 5}), "vq": ("VQVAE", None)}[args.arch]
+    if arch[1] is None:
+        model = vae_models["VQVAE"](in_channels=3, embedding_dim=64, num_embeddings=512, dtype=dtype,
+                                    device="cuda", seed=1265)
+    else:
+        model = vae_models[arch[0]](in_channels=3, latent_dim=128, dtype=dtype, device="cuda", seed=1265, **arch[1])
+    model.train()
+    lr = 0.007 if args.arch == "iwae" else 0.005
+    exp = VAEXperiment(model, {"LR": lr, "weight_decay": 0.0, "kld_weight": 2.5e-4})
+    opt = exp.configure_optimizers()[0]
+    g = torch.Generator(device="cuda").manual_seed(1265)
+    x = torch.rand(args.batch, 3, 64, 64, generator=g, device="cuda")
+    batch = (x, torch.zeros(args.batch, device="cuda"), [f"{i}.png" for i in range(args.batch)])
+    steps = steps or max(10, min(args.steps, 50))
+
+    def one(i):
+        opt.zero_grad(set_to_none=True)
+        loss = exp.training_step(batch, i)
+        loss.backward()
+        opt.step()
+    for i in range(warmup):
+        one(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(i)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"value": round(args.batch * steps / el, 1), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "steps": steps, "path": "VAEXperiment.training_step -> loss.backward -> torch.optim.Adam (eager; "
+                                     "loss_function on the GPU ELBO kernel)",
+            "loss": float(exp.logged["loss"])}
+
+
 def main():
     args = parse()
     if "RANK" not in os.environ and args.gpus > 1:
@@ -403,6 +447,11 @@ def main():
     roof["us_per_launch"] = round(us, 2)
     roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}
     step_kernel_us = sum(r[0] for r in rows)
+    # the step-level attainable time — every kernel at its own roofline bound,
+    # max(flops / MFMA peak, bytes / HBM peak), summed — over the measured step time; and the
+    # literal MFMA fraction, all of the step's flops over the measured step at the bf16/fp32 peak
+    attain_us = sum(max(fl_ / (peak_tf * 1e6), by_ / (HBM_PEAK_GBS * 1e3)) for _, _, fl_, by_ in rows)
+    step_flops = sum(r[2] for r in rows)
 
     cpu = None
     if not args.no_cpu_baseline:
@@ -410,6 +459,13 @@ def main():
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
+    step_roof = {"attainable_us": round(attain_us, 2), "step_us": round(ms * 1e3, 2),
+                 "frac": round(attain_us / (ms * 1e3), 4),
+                 "mfma_frac": round(step_flops / (ms * 1e-3) / (peak_tf * 1e12), 4),
+                 "step_gflop": round(step_flops / 1e9, 3)}
+    dropin = None
+    if world == 1 and not args.no_dropin:
+        dropin = dropin_leg(args, dtype)
     line = {
         "metric": METRIC if args.arch == "vanilla" else f"train images/sec {args.arch} 64x64 bs={args.batch} (1 GPU config)",
         "value": round(value, 1),
@@ -434,6 +490,8 @@ def main():
                  ("VQ_Loss" if args.arch == "vq" else "KLD"): loss_terms[2], "finite": finite},
         "sum_kernel_us_isolated": round(step_kernel_us, 1),
         "roofline": roof,
+        "step_roofline": step_roof,
+        "dropin": dropin,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 8
+#define VAE_ABI_VERSION 9
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -362,6 +362,19 @@ typedef struct vae_swap_desc {
   int32_t a, rs, b;
 } vae_swap_desc;
 int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* stream);
+/* --- workspace queries ----------------------------------------------------
+ * Bytes of workspace the call `op` would use with these arguments — pass exactly the arguments
+ * the call will get (pointers included: alignment selects the kernel path; the workspace fields
+ * are ignored).  The query runs the call's own planning without launching anything (no device,
+ * no stream needed).  A call given a non-NULL workspace smaller than this fails with
+ * VAE_E_BADARG; a NULL workspace selects the plan that uses none (no split-K slabs, no staged
+ * weight copy, atomics for the head's filter partials).  Replaces the fixed host-side constant
+ * of round 1 and the silent split-K downgrade on a short workspace. */
+enum vae_op { VAE_OP_FWD = 0, VAE_OP_BWD_DATA = 1, VAE_OP_BWD_FILTER = 2, VAE_OP_BWD = 3 /* head: both halves */ };
+int vae_conv2d_workspace_size(const vae_conv_args* a, int32_t op, size_t* bytes);
+int vae_convT2d_workspace_size(const vae_conv_args* a, int32_t op, size_t* bytes);
+int vae_linear_workspace_size(const vae_linear_args* a, int32_t op, size_t* bytes);
+int vae_head_workspace_size(const vae_head_args* a, int32_t op, size_t* bytes);
 /* --- start of a training step: zero `bytes` at `zero` and ++*step ------------------ */
 int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream);
 

@@ -23,6 +23,51 @@ int bn_finalize_launch(const vae_bn_args* a, hipStream_t stream);
 // returned by a fast-path launcher whose preconditions do not hold (the caller falls back)
 constexpr int kHeadFallback = 0x7fff0001;
 
+// ---------------------------------------------------------------- workspace queries (host)
+// vae_*_workspace_size runs an entry point's whole planning with an unbounded workspace and the
+// query flag set: every site that would use workspace records its bytes (ws_fits) and VAE_LAUNCH
+// launches nothing.  Outside a query, a plan that needs more workspace than the caller passed
+// fails with VAE_E_BADARG; a NULL workspace selects the plan that uses none.  One flag per host
+// thread, shared by all translation units (inline function with external linkage).
+struct WsQuery {
+  int on;
+  long need;
+};
+inline WsQuery& ws_query() {
+  static thread_local WsQuery q = {0, 0};
+  return q;
+}
+inline bool querying() { return ws_query().on != 0; }
+inline bool ws_fits(long need, long have, const char* what) {
+  WsQuery& q = ws_query();
+  if (q.on) {
+    if (need > q.need) q.need = need;
+    return true;
+  }
+  if (need <= have) return true;
+  fail(VAE_E_BADARG, "%s: workspace of %ld bytes < %ld required (see vae_*_workspace_size)", what, have, need);
+  return false;
+}
+// Query accounting for a call that stages `tail` bytes at the END of the workspace and gives the
+// front to f's own sites: the requirement is f's, rounded to 256, plus the tail.
+template <class F>
+inline int with_ws_tail(long tail, F&& f) {
+  WsQuery& q = ws_query();
+  if (!q.on) return f();
+  const long outer = q.need;
+  q.need = 0;
+  const int rc = f();
+  const long inner = ((q.need + 255) / 256) * 256 + tail;
+  q.need = outer > inner ? outer : inner;
+  return rc;
+}
+}  // namespace vae
+#define VAE_LAUNCH(...)                                         \
+  do {                                                          \
+    if (!::vae::querying()) hipLaunchKernelGGL(__VA_ARGS__);    \
+  } while (0)
+namespace vae {
+
 // ---------------------------------------------------------------- scalar conversion
 __device__ __forceinline__ float ld_f(const float* p) { return *p; }
 __device__ __forceinline__ float ld_f(const __bf16* p) { return (float)(*p); }

@@ -30,17 +30,21 @@ extern "C" int vae_convT2d_fwd(const vae_conv_args* a, void* stream) {
     const long wbytes = (long)a->k * a->r * a->r * a->c * 2;
     long ws_slab = a->workspace_bytes;
     q.b_ptr = a->wt_t;
-    if (!q.b_ptr && a->workspace && a->workspace_bytes >= 2 * wbytes) {
+    const bool tail = !q.b_ptr && a->workspace;
+    if (tail) {
       ws_slab = ((a->workspace_bytes - wbytes) / 256) * 256;
-      q.b_ptr = static_cast<char*>(a->workspace) + ws_slab;
+      q.b_ptr = static_cast<char*>(a->workspace) + (ws_slab > 0 ? ws_slab : 0);
     }
     if (q.b_ptr && cg_ok(q, E_STORE)) {
-      if (!a->wt_t) {
-        if (int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), static_cast<__bf16*>(const_cast<void*>(q.b_ptr)),
-                                         a->c, a->r, a->k, (hipStream_t)stream, 0)) return rc;
-      }
-      return then_finalize(cg_launch<A_CONVT, E_STORE>(q, a->split_k, a->workspace, ws_slab, (hipStream_t)stream),
-                           a->bn_finalize, (hipStream_t)stream);
+      return with_ws_tail(tail ? wbytes : 0, [&]() -> int {
+        if (tail && !ws_fits(wbytes, a->workspace_bytes, "convT2d_fwd weight copy")) return VAE_E_BADARG;
+        if (!a->wt_t) {
+          if (int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), static_cast<__bf16*>(const_cast<void*>(q.b_ptr)),
+                                           a->c, a->r, a->k, (hipStream_t)stream, 0)) return rc;
+        }
+        return then_finalize(cg_launch<A_CONVT, E_STORE>(q, a->split_k, a->workspace, ws_slab, (hipStream_t)stream),
+                             a->bn_finalize, (hipStream_t)stream);
+      });
     }
   }
   return then_finalize(launch<A_CONVT, B_KN, E_STORE, false, false>(a->dtype, false, false, p, a->split_k, a->workspace, a->workspace_bytes,

@@ -31,29 +31,36 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
       q.residual = a->residual;
       long ws_slab = a->workspace_bytes;
       q.b_ptr = a->wt_t;
-      if (!q.b_ptr && a->workspace && a->workspace_bytes >= 2 * wbytes) {
+      const bool tail = !q.b_ptr && a->workspace;
+      if (tail) {
         ws_slab = ((a->workspace_bytes - wbytes) / 256) * 256;
-        q.b_ptr = static_cast<char*>(a->workspace) + ws_slab;
+        q.b_ptr = static_cast<char*>(a->workspace) + (ws_slab > 0 ? ws_slab : 0);
       }
       if (q.epi_xf.kind == VAE_X_BN_ACT && (!q.dgamma || !q.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
       if (q.b_ptr && cg_ok(q, E_BNBWD)) {
         if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "conv2d_bwd_data")) return rc;
-        if (!a->wt_t) {
-          if (int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), static_cast<__bf16*>(const_cast<void*>(q.b_ptr)),
-                                           a->k, a->r, a->c, (hipStream_t)stream, 0)) return rc;
-        }
-        return then_finalize(cg_launch<A_CONVT, E_BNBWD>(q, a->split_k, a->workspace, ws_slab, (hipStream_t)stream),
-                             a->bn_finalize, (hipStream_t)stream);
+        return with_ws_tail(tail ? wbytes : 0, [&]() -> int {
+          if (tail && !ws_fits(wbytes, a->workspace_bytes, "conv2d_bwd_data weight copy")) return VAE_E_BADARG;
+          if (!a->wt_t) {
+            if (int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), static_cast<__bf16*>(const_cast<void*>(q.b_ptr)),
+                                             a->k, a->r, a->c, (hipStream_t)stream, 0)) return rc;
+          }
+          return then_finalize(cg_launch<A_CONVT, E_BNBWD>(q, a->split_k, a->workspace, ws_slab, (hipStream_t)stream),
+                               a->bn_finalize, (hipStream_t)stream);
+        });
       }
     }
   }
   if (S == 1 && a->dtype == VAE_BF16 && a->c % 8 == 0 && a->k % 8 == 0 && a->workspace &&
-      a->workspace_bytes >= 2 * wbytes && !getenv("VAE_NO_DGRAD_FLIP")) {
+      !getenv("VAE_NO_DGRAD_FLIP")) {
     // stride 1: dx = conv(dy, W') with W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] and pad R-1-P — the
     // forward conv path (k-contiguous weight rows, packed im2col gather of dy) instead of the
     // phase-gather with k-strided weights.  W' lives at the end of the workspace.
+    return with_ws_tail(wbytes, [&]() -> int {
+    if (!ws_fits(wbytes, a->workspace_bytes, "conv2d_bwd_data weight copy")) return VAE_E_BADARG;
     char* ws = static_cast<char*>(a->workspace);
-    const long wsoff = ((a->workspace_bytes - wbytes) / 256) * 256;
+    long wsoff = ((a->workspace_bytes - wbytes) / 256) * 256;
+    if (wsoff < 0) wsoff = 0;
     __bf16* wf = reinterpret_cast<__bf16*>(ws + wsoff);
     int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), wf, a->k, a->r, a->c, (hipStream_t)stream);
     if (rc) return rc;
@@ -70,6 +77,7 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
     if (p.epi_xf.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta)) return fail(VAE_E_BADARG, "conv2d_bwd_data: dgamma/dbeta");
     if (int rc2 = check_finalize(a->bn_finalize, a->bn_counter, "conv2d_bwd_data")) return rc2;
     return then_finalize(launch<A_CONV, B_NK, E_BNBWD, true, false>(a->dtype, false, false, p, a->split_k, ws, wsoff, (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
+    });
   }
   GemmParams p = base_params();
   if (!make_taps(p, S, a->r, a->pad)) return fail(VAE_E_UNSUPPORTED, "conv2d_bwd_data: stride/kernel");

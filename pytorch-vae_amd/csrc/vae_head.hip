@@ -526,7 +526,7 @@ HeadQ head_q(const vae_head_args* a) {
 int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
   if (!head_mfma_ok(a)) return kHeadFallback;       // caller falls back to the VALU kernels
   HeadQ q = head_q(a);
-  hipLaunchKernelGGL(head_fwd_mfma, dim3(q.tiles), dim3(256), 0, st, q);
+  VAE_LAUNCH(head_fwd_mfma, dim3(q.tiles), dim3(256), 0, st, q);
   return check_launch("head_fwd_mfma");
 }
 
@@ -556,13 +556,14 @@ int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStre
   const int grid = q.tiles < head_grid() ? q.tiles : head_grid();
   const long need = (long)grid * SLAB_COLS * 4;
   float* ws = static_cast<float*>(a->workspace);
-  const bool slab = filter && ws && a->workspace_bytes >= need;
+  if (filter && ws && !ws_fits(need, a->workspace_bytes, "head_bwd filter partials")) return VAE_E_BADARG;
+  const bool slab = filter && ws;
   q.slab = slab ? ws : nullptr;
-  hipLaunchKernelGGL(head_bwd_mfma, dim3(grid), dim3(256), 0, st, q);
+  VAE_LAUNCH(head_bwd_mfma, dim3(grid), dim3(256), 0, st, q);
   int rc = check_launch("head_bwd_mfma");
   if (rc || !filter) return rc;
   if (slab) {
-    hipLaunchKernelGGL(reduce_rows_kernel, dim3((SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st, (const float*)ws,
+    VAE_LAUNCH(reduce_rows_kernel, dim3((SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st, (const float*)ws,
                        grid, a->dw, a->db);
     rc = check_launch("reduce_rows");
   }

@@ -170,18 +170,27 @@ inline Tile pick_tile(long M, long N, int nphase) {
   return c[nc - 1];
 }
 
-// K-slices: enough blocks to cover the CUs twice, >= 4 K-tiles per slice, and (for slab
-// epilogues) the partial slabs must fit the caller's workspace.
-inline int pick_split(long blocks, int ktiles, bool slab, long slab_elems_per_split, long ws_bytes) {
+// K-slices: enough blocks to cover the CUs twice, >= 4 K-tiles per slice.  The partial slabs of
+// a split need workspace (split * rows * N fp32); the caller checks it with split_fits.
+inline int pick_split(long blocks, int ktiles) {
   if (blocks >= kTargetBlocks || ktiles < 8) return 1;
   int s = (int)((kTargetBlocks + blocks - 1) / blocks);
   const int maxs = ktiles / 4;
   if (s > maxs) s = maxs;
-  if (slab) {
-    const long fit = slab_elems_per_split > 0 ? ws_bytes / (slab_elems_per_split * 4) : 0;
-    if (s > fit) s = (int)fit;
-  }
   return s < 2 ? 1 : s;
+}
+
+// Settle a split-K choice against the caller's workspace: no workspace (NULL) -> no split,
+// unless the caller asked for one (VAE_E_BADARG); a workspace too small for the slabs ->
+// VAE_E_BADARG.  Returns VAE_OK with *split updated, or the error code.
+inline int split_fits(int* split, int split_req, const GemmParams& p, const void* ws, long ws_bytes, const char* what) {
+  if (*split <= 1) return VAE_OK;
+  if (!ws && !querying()) {
+    if (split_req > 1) return fail(VAE_E_BADARG, "%s: split_k %d needs a workspace", what, split_req);
+    *split = 1;
+    return VAE_OK;
+  }
+  return ws_fits((long)*split * p.M * p.N * p.nphase * 4, ws_bytes, what) ? VAE_OK : VAE_E_BADARG;
 }
 
 template <class T, int EM>
@@ -189,14 +198,14 @@ inline int launch_finalize(const GemmParams& p, hipStream_t st) {
   const long rows = (long)p.M * p.nphase;
   const dim3 grid((unsigned)((rows + FIN_ROWS - 1) / FIN_ROWS), (unsigned)((p.N + 63) / 64));
   const size_t lds = EM == E_BNBWD ? (size_t)tab_floats(p.epi_xf, true) * 4 : 0;
-  if (p.N % 4 == 0) hipLaunchKernelGGL((igemm_finalize<T, EM, true>), grid, dim3(NTHREADS), lds, st, p);
-  else hipLaunchKernelGGL((igemm_finalize<T, EM, false>), grid, dim3(NTHREADS), lds, st, p);
+  if (p.N % 4 == 0) VAE_LAUNCH((igemm_finalize<T, EM, true>), grid, dim3(NTHREADS), lds, st, p);
+  else VAE_LAUNCH((igemm_finalize<T, EM, false>), grid, dim3(NTHREADS), lds, st, p);
   return check_launch("igemm_finalize");
 }
 
 #define VAE_TILE_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
-    hipLaunchKernelGGL((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VA, VB, DYA, DYB>), grid, block, lds, st, p); \
+    VAE_LAUNCH((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VA, VB, DYA, DYB>), grid, block, lds, st, p); \
     return; \
   }
 
@@ -299,13 +308,12 @@ inline int launch_fgemm(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
   // split-K over workgroups (slabs + igemm_finalize) until ~2 workgroups per CU, >= 4 k-steps
   // per workgroup (one per wave)
   int split = 1;
-  if (tiles < 2 * kCUs && ws) {
+  if (tiles < 2 * kCUs) {
     split = (int)((2 * kCUs + tiles - 1) / tiles);
     if (split > steps / 4) split = steps / 4;
-    const long per = (long)p.M * p.N * p.nphase * 4;
-    if (split > ws_bytes / per) split = (int)(ws_bytes / per);
     if (split < 2) split = 1;
   }
+  if (int rc = split_fits(&split, 0, p, ws, ws_bytes, "fgemm split-K")) return rc;
   p.ksplit = split;
   p.slab = split > 1 ? static_cast<float*>(ws) : nullptr;
 #ifdef VAE_PROBE
@@ -313,7 +321,7 @@ inline int launch_fgemm(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
 #endif
   const dim3 grid((p.M + BM - 1) / BM, (p.N + BN - 1) / BN, p.nphase * p.ksplit);
   const size_t lds = (size_t)(tab_floats(p.a_xf, false) + (EM == E_BNBWD ? tab_floats(p.epi_xf, true) : 0)) * 4;
-  hipLaunchKernelGGL((fgemm_kernel<T, TA, BM, BN, AM, EM, DYA>), grid, dim3(256), lds, st, p);
+  VAE_LAUNCH((fgemm_kernel<T, TA, BM, BN, AM, EM, DYA>), grid, dim3(256), lds, st, p);
   int rc = check_launch("fgemm");
   if (rc) return rc;
   if (p.slab) return launch_finalize<T, EM>(p, st);
@@ -346,10 +354,10 @@ inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req
   const int ktiles = (kmax + bk - 1) / bk;
   const long blocks = (long)((p.M + t.bm - 1) / t.bm) * ((p.N + t.bn - 1) / t.bn) * p.nphase;
   const bool slab = EM != E_ACC;
-  int split = split_req > 0 ? split_req : pick_split(blocks, ktiles, slab, (long)p.M * p.N * p.nphase, ws ? ws_bytes : 0);
+  int split = split_req > 0 ? split_req : pick_split(blocks, ktiles);
   if (slab && split > 1) {
-    if (!ws || (long)split * p.M * p.N * p.nphase * 4 > ws_bytes) split = 1;
-    else p.slab = static_cast<float*>(ws);
+    if (int rc = split_fits(&split, split_req, p, ws, ws_bytes, "igemm split-K")) return rc;
+    if (split > 1) p.slab = static_cast<float*>(ws);
   }
   p.ksplit = split < 1 ? 1 : split;
   if (dtype == VAE_F32) return launch_tiled<float, float, float, AM, BMD, EM, DYA, DYB>(p, t, st);
@@ -445,7 +453,7 @@ __global__ void __launch_bounds__(256) flip_weights_kernel(const __bf16* w, __bf
 
 inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C, hipStream_t st, int flip = 1) {
   const dim3 grid((C + 31) / 32, (K + 31) / 32, R * R);
-  hipLaunchKernelGGL(flip_weights_kernel, grid, dim3(256), 0, st, w, wf, K, R * R, C, flip);
+  VAE_LAUNCH(flip_weights_kernel, grid, dim3(256), 0, st, w, wf, K, R * R, C, flip);
   return check_launch("flip_weights");
 }
 
@@ -494,7 +502,7 @@ inline void cg_launch_tile(const GemmParams& p, CgTile t, hipStream_t st) {
 #define VAE_CG_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
     const unsigned nb = (unsigned)(((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.nphase * p.ksplit); \
-    hipLaunchKernelGGL((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM, OR>), dim3(nb), dim3(256), lds, st, p); \
+    VAE_LAUNCH((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM, OR>), dim3(nb), dim3(256), lds, st, p); \
     return; \
   }
   VAE_CG_CASE(128, 128)
@@ -539,7 +547,7 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
     split = (int)((2 * kCUs + blocks - 1) / blocks);
     if (split > ktiles / 2) split = ktiles / 2;
   }
-  if (split > 1 && (!ws || (long)split * p.M * p.N * p.nphase * 4 > ws_bytes)) split = 1;
+  if (int rc = split_fits(&split, split_req, p, ws, ws_bytes, "cgemm split-K")) return rc;
   p.ksplit = split < 1 ? 1 : split;
   p.slab = p.ksplit > 1 ? static_cast<float*>(ws) : nullptr;
   // one-round kernels when every slice's K-steps fit the ring of the chosen instantiation
@@ -578,17 +586,17 @@ inline int column_sum_launch(int dtype, const void* dy, long rows, int C, float*
     if (blocks < 1) blocks = 1;
     const size_t lds = (size_t)C * sizeof(float);
     if (dtype == VAE_F32) {
-      if (V == 8) hipLaunchKernelGGL((column_sum_flat<float, 8>), dim3((unsigned)blocks), dim3(bd), lds, st, (const float*)dy, nvec, C, db);
-      else hipLaunchKernelGGL((column_sum_flat<float, 1>), dim3((unsigned)blocks), dim3(bd), lds, st, (const float*)dy, nvec, C, db);
+      if (V == 8) VAE_LAUNCH((column_sum_flat<float, 8>), dim3((unsigned)blocks), dim3(bd), lds, st, (const float*)dy, nvec, C, db);
+      else VAE_LAUNCH((column_sum_flat<float, 1>), dim3((unsigned)blocks), dim3(bd), lds, st, (const float*)dy, nvec, C, db);
     } else {
-      if (V == 8) hipLaunchKernelGGL((column_sum_flat<__bf16, 8>), dim3((unsigned)blocks), dim3(bd), lds, st, (const __bf16*)dy, nvec, C, db);
-      else hipLaunchKernelGGL((column_sum_flat<__bf16, 1>), dim3((unsigned)blocks), dim3(bd), lds, st, (const __bf16*)dy, nvec, C, db);
+      if (V == 8) VAE_LAUNCH((column_sum_flat<__bf16, 8>), dim3((unsigned)blocks), dim3(bd), lds, st, (const __bf16*)dy, nvec, C, db);
+      else VAE_LAUNCH((column_sum_flat<__bf16, 1>), dim3((unsigned)blocks), dim3(bd), lds, st, (const __bf16*)dy, nvec, C, db);
     }
     return check_launch("column_sum");
   }
   const dim3 grid(64, (C + 63) / 64);
-  if (dtype == VAE_F32) hipLaunchKernelGGL(column_sum<float>, grid, dim3(256), 0, st, (const float*)dy, rows, C, db);
-  else hipLaunchKernelGGL(column_sum<__bf16>, grid, dim3(256), 0, st, (const __bf16*)dy, rows, C, db);
+  if (dtype == VAE_F32) VAE_LAUNCH(column_sum<float>, grid, dim3(256), 0, st, (const float*)dy, rows, C, db);
+  else VAE_LAUNCH(column_sum<__bf16>, grid, dim3(256), 0, st, (const __bf16*)dy, rows, C, db);
   return check_launch("column_sum");
 }
 

@@ -26,6 +26,7 @@ int fail(int code, const char* fmt, ...) {
 }
 
 int check_launch(const char* what) {
+  if (querying()) return VAE_OK;            // nothing was launched (workspace query)
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, "%s: %s", what, hipGetErrorString(e));
   return VAE_OK;
@@ -535,8 +536,8 @@ extern "C" int vae_head_fwd(const vae_head_args* a, void* stream) {
   if (rc != kHeadFallback) return rc;
   const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
   if (lds > 64 * 1024) return fail(VAE_E_UNSUPPORTED, "head_fwd: tile too large");
-  if (a->dtype == VAE_F32) hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(head_fwd_kernel<__bf16>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  if (a->dtype == VAE_F32) VAE_LAUNCH(head_fwd_kernel<float>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  else VAE_LAUNCH(head_fwd_kernel<__bf16>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   return check_launch("head_fwd");
 }
 
@@ -553,12 +554,12 @@ extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
   const bool f = a->dtype == VAE_F32;
   switch (a->c) {
     case 32:
-      if (f) hipLaunchKernelGGL((head_bwd_data_kernel<float, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
-      else hipLaunchKernelGGL((head_bwd_data_kernel<__bf16, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      if (f) VAE_LAUNCH((head_bwd_data_kernel<float, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      else VAE_LAUNCH((head_bwd_data_kernel<__bf16, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
       break;
     case 64:
-      if (f) hipLaunchKernelGGL((head_bwd_data_kernel<float, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
-      else hipLaunchKernelGGL((head_bwd_data_kernel<__bf16, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      if (f) VAE_LAUNCH((head_bwd_data_kernel<float, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      else VAE_LAUNCH((head_bwd_data_kernel<__bf16, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
       break;
     default:
       return fail(VAE_E_UNSUPPORTED, "head_bwd_data: channels %d (32 or 64)", a->c);
@@ -576,8 +577,8 @@ extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
   if (rc != kHeadFallback) return rc;
   const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
   const int grid = p.tiles < 256 ? p.tiles : 256;
-  if (a->dtype == VAE_F32) hipLaunchKernelGGL(head_bwd_filter_kernel<float>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(head_bwd_filter_kernel<__bf16>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  if (a->dtype == VAE_F32) VAE_LAUNCH(head_bwd_filter_kernel<float>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
+  else VAE_LAUNCH(head_bwd_filter_kernel<__bf16>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   return check_launch("head_bwd_filter");
 }
 
@@ -590,13 +591,13 @@ int vae::bn_finalize_launch(const vae_bn_args* a, hipStream_t stream) {
   if (a->mode < 0 || a->mode > 2) return fail(VAE_E_BADARG, "bn_finalize: mode %d", a->mode);
   if (a->mode == 2) {
     if (!a->xf.running_mean || !a->xf.running_var) return fail(VAE_E_BADARG, "bn_finalize: eval mode needs running statistics");
-    hipLaunchKernelGGL(bn_eval_table_kernel, dim3((a->xf.channels + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
+    VAE_LAUNCH(bn_eval_table_kernel, dim3((a->xf.channels + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
     return check_launch("bn_finalize(eval)");
   }
   if (a->mode == 1 && (!a->xf.dgamma || !a->xf.dbeta)) return fail(VAE_E_BADARG, "bn_finalize: backward sums");
   if (a->xf.reps > BNF_LANES * BNF_PER) return fail(VAE_E_UNSUPPORTED, "bn_finalize: %d replicas > %d", a->xf.reps, BNF_LANES * BNF_PER);
   const int grid = (a->xf.channels + 63) / 64;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
+  VAE_LAUNCH(bn_finalize_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
   return check_launch("bn_finalize");
 }
 
@@ -620,8 +621,8 @@ extern "C" int vae_reparam_fwd(int32_t dtype, int32_t rows, int32_t samples, int
   if (!mulv || !eps || !z || rows <= 0 || latent <= 0 || samples <= 0) return fail(VAE_E_BADARG, "reparam_fwd: args");
   const long n = (long)rows * latent;
   const int grid = (int)((n + 255) / 256);
-  if (dtype == VAE_F32) hipLaunchKernelGGL(reparam_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, samples, latent, mulv, eps, (float*)z);
-  else if (dtype == VAE_BF16) hipLaunchKernelGGL(reparam_kernel<__bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, samples, latent, mulv, eps, (__bf16*)z);
+  if (dtype == VAE_F32) VAE_LAUNCH(reparam_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, samples, latent, mulv, eps, (float*)z);
+  else if (dtype == VAE_BF16) VAE_LAUNCH(reparam_kernel<__bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, samples, latent, mulv, eps, (__bf16*)z);
   else return fail(VAE_E_BADDTYPE, "reparam_fwd: dtype");
   return check_launch("reparam_fwd");
 }
@@ -636,7 +637,7 @@ extern "C" int vae_elbo_fwd(const vae_elbo_args* a, void* stream) {
     if (!a->mulv || !a->head_coef || !a->kl_coef) return fail(VAE_E_BADARG, "elbo_fwd: args");
     if (a->batch <= 0 || a->batch > 1024 || a->latent <= 0 || a->img_elems <= 0) return fail(VAE_E_BADSHAPE, "elbo_fwd: sizes");
   }
-  hipLaunchKernelGGL(elbo_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *a);
+  VAE_LAUNCH(elbo_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *a);
   return check_launch("elbo_fwd");
 }
 
@@ -647,16 +648,16 @@ extern "C" int vae_adam_step(int64_t n, float* p, const float* g, float* m, floa
   if (!p || !g || !m || !v || !step || !lr) return fail(VAE_E_BADARG, "adam_step: null");
   const int grid = grid_for(n);
   if (p_lowp)
-    hipLaunchKernelGGL(adam_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)p_lowp);
+    VAE_LAUNCH(adam_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)p_lowp);
   else
-    hipLaunchKernelGGL(adam_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)nullptr);
+    VAE_LAUNCH(adam_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)nullptr);
   return check_launch("adam_step");
 }
 
 extern "C" int vae_cast_bf16(int64_t n, const float* src, void* dst, void* stream) {
   if (n <= 0) return VAE_OK;
   if (!src || !dst) return fail(VAE_E_BADARG, "cast_bf16: null");
-  hipLaunchKernelGGL(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (long)n, src, (__bf16*)dst);
+  VAE_LAUNCH(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (long)n, src, (__bf16*)dst);
   return check_launch("cast_bf16");
 }
 
@@ -665,7 +666,7 @@ extern "C" int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* st
   if (((uintptr_t)zero & 15) != 0) return fail(VAE_E_BADARG, "step_begin: zero region must be 16-B aligned");
   const long n16 = bytes / 16;
   const int ntail = (int)(bytes - n16 * 16);
-  hipLaunchKernelGGL(step_begin_kernel, dim3(grid_for(n16 > 0 ? n16 : 1)), dim3(256), 0, (hipStream_t)stream,
+  VAE_LAUNCH(step_begin_kernel, dim3(grid_for(n16 > 0 ? n16 : 1)), dim3(256), 0, (hipStream_t)stream,
                      (f32x4*)zero, n16, (unsigned char*)zero + n16 * 16, ntail, (int*)step);
   return check_launch("step_begin");
 }
@@ -723,6 +724,66 @@ extern "C" int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* st
   }
   sb.tiles0[count] = tiles;
   sb.count = count;
-  hipLaunchKernelGGL(swap_axes_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, sb);
+  VAE_LAUNCH(swap_axes_kernel, dim3(tiles), dim3(256), 0, (hipStream_t)stream, sb);
   return check_launch("swap_axes");
+}
+
+// ---------------------------------------------------------------- workspace queries
+// The entry point runs on a copy of the arguments with an unbounded (never dereferenced)
+// workspace while the thread's query flag is set: its planning is the real one, every workspace
+// site records its bytes (vae_common.hpp ws_fits) and nothing is launched, so the query needs no
+// device and no stream.
+namespace {
+template <class A, class F>
+int ws_size(const A* a, size_t* bytes, F&& call) {
+  if (!a || !bytes) return fail(VAE_E_BADARG, "workspace_size: null argument");
+  A c = *a;
+  c.workspace = reinterpret_cast<void*>(uintptr_t(1) << 40);
+  c.workspace_bytes = int64_t(1) << 50;
+  WsQuery& q = ws_query();
+  q.on = 1;
+  q.need = 0;
+  const int rc = call(&c);
+  *bytes = rc ? 0 : (size_t)q.need;
+  q.on = 0;
+  q.need = 0;
+  return rc;
+}
+}  // namespace
+
+extern "C" int vae_conv2d_workspace_size(const vae_conv_args* a, int32_t op, size_t* bytes) {
+  switch (op) {
+    case VAE_OP_FWD: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_conv2d_fwd(c, nullptr); });
+    case VAE_OP_BWD_DATA: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_conv2d_bwd_data(c, nullptr); });
+    case VAE_OP_BWD_FILTER: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_conv2d_bwd_filter(c, nullptr); });
+  }
+  return fail(VAE_E_BADARG, "conv2d_workspace_size: op %d", op);
+}
+
+extern "C" int vae_convT2d_workspace_size(const vae_conv_args* a, int32_t op, size_t* bytes) {
+  switch (op) {
+    case VAE_OP_FWD: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_fwd(c, nullptr); });
+    case VAE_OP_BWD_DATA: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_bwd_data(c, nullptr); });
+    case VAE_OP_BWD_FILTER: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_bwd_filter(c, nullptr); });
+  }
+  return fail(VAE_E_BADARG, "convT2d_workspace_size: op %d", op);
+}
+
+extern "C" int vae_linear_workspace_size(const vae_linear_args* a, int32_t op, size_t* bytes) {
+  switch (op) {
+    case VAE_OP_FWD: return ws_size(a, bytes, [](const vae_linear_args* c) { return vae_linear_fwd(c, nullptr); });
+    case VAE_OP_BWD_DATA: return ws_size(a, bytes, [](const vae_linear_args* c) { return vae_linear_bwd_data(c, nullptr); });
+    case VAE_OP_BWD_FILTER: return ws_size(a, bytes, [](const vae_linear_args* c) { return vae_linear_bwd_filter(c, nullptr); });
+  }
+  return fail(VAE_E_BADARG, "linear_workspace_size: op %d", op);
+}
+
+extern "C" int vae_head_workspace_size(const vae_head_args* a, int32_t op, size_t* bytes) {
+  switch (op) {
+    case VAE_OP_FWD: return ws_size(a, bytes, [](const vae_head_args* c) { return vae_head_fwd(c, nullptr); });
+    case VAE_OP_BWD_DATA: return ws_size(a, bytes, [](const vae_head_args* c) { return vae_head_bwd_data(c, nullptr); });
+    case VAE_OP_BWD_FILTER: return ws_size(a, bytes, [](const vae_head_args* c) { return vae_head_bwd_filter(c, nullptr); });
+    case VAE_OP_BWD: return ws_size(a, bytes, [](const vae_head_args* c) { return vae_head_bwd(c, nullptr); });
+  }
+  return fail(VAE_E_BADARG, "head_workspace_size: op %d", op);
 }

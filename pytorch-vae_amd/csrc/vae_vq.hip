@@ -192,8 +192,8 @@ int vq_check(const vae_vq_args* a, const char* what) {
 template <int D>
 int vq_fwd_launch(const vae_vq_args* a, hipStream_t st) {
   const dim3 grid((a->rows + VQ_ROWS - 1) / VQ_ROWS);
-  if (a->dtype == VAE_F32) hipLaunchKernelGGL((vq_fwd_kernel<float, D>), grid, dim3(256), 0, st, *a);
-  else hipLaunchKernelGGL((vq_fwd_kernel<__bf16, D>), grid, dim3(256), 0, st, *a);
+  if (a->dtype == VAE_F32) VAE_LAUNCH((vq_fwd_kernel<float, D>), grid, dim3(256), 0, st, *a);
+  else VAE_LAUNCH((vq_fwd_kernel<__bf16, D>), grid, dim3(256), 0, st, *a);
   return check_launch("vq_fwd");
 }
 
@@ -206,8 +206,8 @@ int recon_launch(const vae_recon_args* a, int bwd, hipStream_t st) {
   if (!bwd && !a->y) return fail(VAE_E_BADARG, "recon_fwd: y");
   if (bwd && (!a->grad_recon || !a->dy)) return fail(VAE_E_BADARG, "recon_bwd: grad_recon / dy");
   const dim3 grid((unsigned)((long)a->n * a->h * a->w / 256));
-  if (a->dtype == VAE_F32) hipLaunchKernelGGL((recon_kernel<float, 3>), grid, dim3(256), 0, st, *a, bwd);
-  else if (a->dtype == VAE_BF16) hipLaunchKernelGGL((recon_kernel<__bf16, 3>), grid, dim3(256), 0, st, *a, bwd);
+  if (a->dtype == VAE_F32) VAE_LAUNCH((recon_kernel<float, 3>), grid, dim3(256), 0, st, *a, bwd);
+  else if (a->dtype == VAE_BF16) VAE_LAUNCH((recon_kernel<__bf16, 3>), grid, dim3(256), 0, st, *a, bwd);
   else return fail(VAE_E_BADDTYPE, "recon: dtype");
   return check_launch("recon");
 }
@@ -248,8 +248,8 @@ extern "C" int vae_nchw_to_nhwc_pad(int32_t dtype, int32_t n, int32_t c, int32_t
   if (!x || !y || n <= 0 || c <= 0 || h <= 0 || w <= 0 || cp < c) return fail(VAE_E_BADARG, "nchw_to_nhwc_pad: args");
   const long pix = (long)n * h * w;
   const dim3 grid((unsigned)((pix + 255) / 256));
-  if (dtype == VAE_F32) hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, n, c, h, w, cp, x, (float*)y);
-  else if (dtype == VAE_BF16) hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, n, c, h, w, cp, x, (__bf16*)y);
+  if (dtype == VAE_F32) VAE_LAUNCH(nchw_to_nhwc_pad_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, n, c, h, w, cp, x, (float*)y);
+  else if (dtype == VAE_BF16) VAE_LAUNCH(nchw_to_nhwc_pad_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, n, c, h, w, cp, x, (__bf16*)y);
   else return fail(VAE_E_BADDTYPE, "nchw_to_nhwc_pad: dtype");
   return check_launch("nchw_to_nhwc_pad");
 }
@@ -257,8 +257,8 @@ extern "C" int vae_nchw_to_nhwc_pad(int32_t dtype, int32_t n, int32_t c, int32_t
 extern "C" int vae_pad_channels(int32_t dtype, int64_t rows, int32_t c, int32_t cp, const void* src, void* dst, void* stream) {
   if (!src || !dst || rows <= 0 || c <= 0 || cp < c) return fail(VAE_E_BADARG, "pad_channels: args");
   const dim3 grid((unsigned)((rows * cp + 255) / 256));
-  if (dtype == VAE_F32) hipLaunchKernelGGL(pad_channels_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, c, cp, (const float*)src, (float*)dst);
-  else if (dtype == VAE_BF16) hipLaunchKernelGGL(pad_channels_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, c, cp, (const __bf16*)src, (__bf16*)dst);
+  if (dtype == VAE_F32) VAE_LAUNCH(pad_channels_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, c, cp, (const float*)src, (float*)dst);
+  else if (dtype == VAE_BF16) VAE_LAUNCH(pad_channels_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, c, cp, (const __bf16*)src, (__bf16*)dst);
   else return fail(VAE_E_BADDTYPE, "pad_channels: dtype");
   return check_launch("pad_channels");
 }
@@ -266,7 +266,7 @@ extern "C" int vae_pad_channels(int32_t dtype, int64_t rows, int32_t c, int32_t 
 extern "C" int vae_unpad_accumulate(int64_t rows, int32_t cp, int32_t c, const float* src, float* dst, void* stream) {
   if (!src || !dst || rows <= 0 || c <= 0 || cp < c) return fail(VAE_E_BADARG, "unpad_accumulate: args");
   const dim3 grid((unsigned)((rows * c + 255) / 256));
-  hipLaunchKernelGGL(unpad_accumulate_kernel, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, cp, c, src, dst);
+  VAE_LAUNCH(unpad_accumulate_kernel, grid, dim3(256), 0, (hipStream_t)stream, (long)rows, cp, c, src, dst);
   return check_launch("unpad_accumulate");
 }
 
@@ -287,8 +287,8 @@ extern "C" int vae_vq_bwd(const vae_vq_args* a, void* stream) {
   const int groups = 256 / a->dim;
   const long runs = ((long)a->rows + VQB_RUN - 1) / VQB_RUN;
   const dim3 grid((unsigned)((runs + groups - 1) / groups));
-  if (a->dtype == VAE_F32) hipLaunchKernelGGL(vq_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
-  else hipLaunchKernelGGL(vq_bwd_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  if (a->dtype == VAE_F32) VAE_LAUNCH(vq_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  else VAE_LAUNCH(vq_bwd_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *a);
   return check_launch("vq_bwd");
 }
 

@@ -472,9 +472,9 @@ inline void wg2_launch_k(const WgParams& p, unsigned blocks, hipStream_t st) {
   if constexpr (BM == 32) {
     // 32 x 32 tiles of 3x3 kernels: every tap in one workgroup (the grid was sized without the
     // tap factor); larger tiles / kernels would exceed the LDS and register budget
-    if (p.R == 3) { hipLaunchKernelGGL((wgemm_taps_kernel<BM, BJ, XU, XV, 3>), dim3(blocks), dim3(256), lds, st, p); return; }
+    if (p.R == 3) { VAE_LAUNCH((wgemm_taps_kernel<BM, BJ, XU, XV, 3>), dim3(blocks), dim3(256), lds, st, p); return; }
   }
-  hipLaunchKernelGGL((wgemm_kernel<BM, BJ, XU, XV>), dim3(blocks), dim3(256), lds, st, p);
+  VAE_LAUNCH((wgemm_kernel<BM, BJ, XU, XV>), dim3(blocks), dim3(256), lds, st, p);
 }
 
 template <int BM, int BJ, int XU>

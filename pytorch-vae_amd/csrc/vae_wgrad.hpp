@@ -251,7 +251,7 @@ inline int wgrad_launch(WgradParams p, hipStream_t st) {
   p.kper = (int)(((ksteps + split - 1) / split) * WG_BK);
   split = (npix + p.kper - 1) / p.kper;
   const dim3 grid((p.M + WG_BM - 1) / WG_BM, (p.J + WG_BJ - 1) / WG_BJ, (unsigned)(p.R * p.R * split));
-  hipLaunchKernelGGL(wgrad_bf16_kernel, grid, dim3(256), 0, st, p);
+  VAE_LAUNCH(wgrad_bf16_kernel, grid, dim3(256), 0, st, p);
   return check_launch("wgrad_bf16");
 }
 

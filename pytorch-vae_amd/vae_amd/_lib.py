@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -138,6 +138,10 @@ _SIGS = {
     "vae_nchw_to_nhwc_pad": [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vae_pad_channels": [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vae_unpad_accumulate": [c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
+    "vae_conv2d_workspace_size": [POINTER(ConvArgs), c_int32, POINTER(ctypes.c_size_t)],
+    "vae_convT2d_workspace_size": [POINTER(ConvArgs), c_int32, POINTER(ctypes.c_size_t)],
+    "vae_linear_workspace_size": [POINTER(LinearArgs), c_int32, POINTER(ctypes.c_size_t)],
+    "vae_head_workspace_size": [POINTER(HeadArgs), c_int32, POINTER(ctypes.c_size_t)],
 }
 EXPORTED = tuple(_SIGS)
 
@@ -169,6 +173,35 @@ def call(name: str, *args):
     if rc != 0:
         msg = lib.vae_last_error().decode(errors="replace")
         raise VaeHipError(f"{name} failed (rc={rc}): {msg}")
+
+
+OP_FWD, OP_BWD_DATA, OP_BWD_FILTER, OP_BWD = 0, 1, 2, 3          # vaehip.h enum vae_op
+
+# entry point -> (its workspace query, op)
+WS_QUERY = {
+    "vae_conv2d_fwd": ("vae_conv2d_workspace_size", OP_FWD),
+    "vae_conv2d_bwd_data": ("vae_conv2d_workspace_size", OP_BWD_DATA),
+    "vae_conv2d_bwd_filter": ("vae_conv2d_workspace_size", OP_BWD_FILTER),
+    "vae_convT2d_fwd": ("vae_convT2d_workspace_size", OP_FWD),
+    "vae_convT2d_bwd_data": ("vae_convT2d_workspace_size", OP_BWD_DATA),
+    "vae_convT2d_bwd_filter": ("vae_convT2d_workspace_size", OP_BWD_FILTER),
+    "vae_linear_fwd": ("vae_linear_workspace_size", OP_FWD),
+    "vae_linear_bwd_data": ("vae_linear_workspace_size", OP_BWD_DATA),
+    "vae_linear_bwd_filter": ("vae_linear_workspace_size", OP_BWD_FILTER),
+    "vae_head_fwd": ("vae_head_workspace_size", OP_FWD),
+    "vae_head_bwd_data": ("vae_head_workspace_size", OP_BWD_DATA),
+    "vae_head_bwd_filter": ("vae_head_workspace_size", OP_BWD_FILTER),
+    "vae_head_bwd": ("vae_head_workspace_size", OP_BWD),
+}
+
+
+def workspace_size(fn: str, arg) -> int:
+    """Workspace bytes the entry point `fn` needs for `arg` (a ConvArgs / LinearArgs / HeadArgs
+    filled as for the call; its workspace fields are ignored).  Runs no kernel."""
+    q, op = WS_QUERY[fn]
+    out = ctypes.c_size_t(0)
+    call(q, ctypes.byref(arg), op, ctypes.byref(out))
+    return int(out.value)
 
 
 def ptr(t) -> int | None:

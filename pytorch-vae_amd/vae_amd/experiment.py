@@ -134,11 +134,53 @@ class VAEXperiment:
         return optims
 
 
-def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=None) -> List[Dict[str, float]]:
+class GraphedSteps:
+    """The graph path of VAEXperiment.training_step + loss.backward() + optimizer.step(): one
+    engine.TrainStep per batch size (HIP graphs of forward, vae_elbo_fwd, backward, Adam on the
+    model's own parameters, model.fused_train_step), with the experiment's logging — the loss
+    terms as device tensors in experiment.logged, per-image MSE to the data module and the
+    extreme-image tracking — and the torch optimizer's learning rate (so its schedulers keep
+    their semantics) copied into the fused Adam before every step."""
+
+    def __init__(self, experiment: VAEXperiment, optimizer):
+        self.exp, self.opt = experiment, optimizer
+        self.steps: Dict[int, Any] = {}
+        p = experiment.params
+        self.kw = dict(kld_weight=p['kld_weight'], lr=optimizer.param_groups[0]['lr'],
+                       weight_decay=p.get('weight_decay', 0.0), betas=optimizer.param_groups[0]['betas'])
+
+    def __call__(self, batch, batch_idx):
+        imgs, labels, names = batch
+        exp, model = self.exp, self.exp.model
+        B = imgs.shape[0]
+        step = self.steps.get(B)
+        if step is None:
+            step = self.steps[B] = model.fused_train_step(B, **self.kw)
+        step.opt.set_lr(self.opt.param_groups[0]['lr'])
+        exp.curr_device = imgs.device
+        plan = step.plan
+        eps = torch.randn(plan.eps.shape, device=imgs.device) if hasattr(plan, "eps") else None
+        step(imgs, eps)
+        if hasattr(model, "num_iter"):
+            model.num_iter += 1                       # BetaVAE: the loss_function's counter
+        out = plan.out
+        third = "VQ_Loss" if not hasattr(plan, "eps") else "KLD"
+        exp.log_dict({'loss': out[0], 'Reconstruction_Loss': out[1], third: out[2]})
+        per = plan.per_img.view(B, -1).mean(dim=1).cpu()
+        if exp.datamodule is not None and hasattr(exp.datamodule, "record_img_losses"):
+            exp.datamodule.record_img_losses(names, per)
+        recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:, 0]
+        exp._track_extremes(per, imgs, recon, names)
+        return exp.logged['loss']
+
+
+def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=None,
+        engine: str = "eager") -> List[Dict[str, float]]:
     """Minimal Trainer loop over an iterable of (imgs, labels, names) batches: the reference's
     Lightning fit() for one optimizer (zero_grad, training_step, backward, step, epoch-interval
     schedulers).  Returns the per-epoch mean of each logged term (host values, synced once per
-    epoch)."""
+    epoch).  engine="graph": each training step is one GraphedSteps replay (models with
+    fused_train_step; plain Adam on model.parameters())."""
     opt_cfg = experiment.configure_optimizers()
     sched, plateau = [], None
     if isinstance(opt_cfg, dict):
@@ -148,6 +190,13 @@ def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=No
         optims, sched = opt_cfg
     else:
         optims = opt_cfg
+    graphed = None
+    if engine == "graph":
+        if not hasattr(experiment.model, "fused_train_step") or len(optims) != 1:
+            raise ValueError("engine='graph' needs a vae_amd model and a single optimizer")
+        graphed = GraphedSteps(experiment, optims[0])
+    elif engine != "eager":
+        raise ValueError(f"engine {engine!r}")
     history = []
     for _ in range(epochs):
         sums: Dict[str, Tensor] = {}
@@ -158,6 +207,10 @@ def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=No
                 sums[k] = sums.get(k, 0) + v.float()
                 cnt[k] = cnt.get(k, 0) + 1
         for i, batch in enumerate(train_batches):
+            if graphed is not None:
+                graphed(batch, i)
+                acc()
+                continue
             for o in optims:
                 o.zero_grad(set_to_none=True)
             loss = experiment.training_step(batch, i)

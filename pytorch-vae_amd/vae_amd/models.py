@@ -10,11 +10,13 @@ Mirrors the reference interface (paths relative to the reference root):
   vae_models registry     models/__init__.py:35-56
 
 `forward(x)` runs the HIP encoder/decoder (libvaehip.so) and returns the reference's list
-([recons, input, mu, log_var], IWAE: [recons, input, mu, log_var, z, eps]); `loss_function`
-is the reference formula evaluated by torch on those tensors (so every loss variant and its
-returned dict are the reference's own); `loss.backward()` reaches `_VAEStep.backward`, which
-runs the fused HIP backward seeded with dL/drecon and dL/d[mu, log_var] and returns the
-gradient of the flat parameter buffer.  Optimizers see one flat nn.Parameter (`model.flat`);
+([recons, input, mu, log_var], IWAE: [recons, input, mu, log_var, z, eps]).  `loss_function`
+called on that list (what experiment.VAEXperiment.training_step does) runs the ELBO on the GPU
+(vae_elbo_fwd, `_HipELBO`) and returns the reference's dict; its backward is the fused HIP
+backward seeded by the kernel's coefficients — no dL/drecon tensor is materialised.  On any
+other tensors (eval mode, a caller's own loss, no grad) it is the reference formula in torch and
+`loss.backward()` reaches `_VAEStep.backward`, which seeds the same fused backward with autograd's
+dL/drecon and dL/d[mu, log_var].  Optimizers see one flat nn.Parameter (`model.flat`);
 `reference_state_dict()` / `load_reference_state_dict()` convert to the reference's keys and
 layouts (vae_amd/layout.py).
 
@@ -106,8 +108,10 @@ class _VAEStep(torch.autograd.Function):
         plan.eps.copy_(eps.detach().reshape(plan.eps.shape))
         L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, plan.step.data_ptr(), st)
         plan.forward(st)
+        plan.backward_done = False
         model.net.num_batches_tracked += 1
         ctx.plan = plan
+        ctx.set_materialize_grads(False)
         D = model.latent_dim
         recon = plan.recon.clone()
         mu = plan.mulv[:, :D].clone()
@@ -117,6 +121,11 @@ class _VAEStep(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_recon: Optional[Tensor], g_mu: Optional[Tensor], g_lv: Optional[Tensor]):
         plan = ctx.plan
+        if g_recon is None and g_mu is None and g_lv is None:
+            return None, None, None, None          # the loss came through _HipELBO (already done)
+        if plan.backward_done:                     # a second backward of the same forward
+            plan.reset_backward()
+        plan.backward_done = True
         D = plan.net.latent_dim
         if g_recon is None:
             plan.grad_recon.zero_()
@@ -127,6 +136,40 @@ class _VAEStep(torch.autograd.Function):
         dm[:, D:].copy_(g_lv if g_lv is not None else torch.zeros_like(dm[:, D:]))
         plan.backward(L.stream_ptr())
         return plan.grads.clone(), None, None, None
+
+
+class _HipELBO(torch.autograd.Function):
+    """loss_function of a VanillaVAE-family model on its own forward's outputs, on the GPU:
+    vae_elbo_fwd evaluates the reference's loss terms (vanilla_vae.py:124-146, beta_vae.py:129-152,
+    iwae.py:129-160) from the per-image SSE the head kernel accumulated and mu|log_var, and writes
+    the backward seeds; backward scales them by dL/dloss and runs the fused HIP backward from them,
+    returning the flat parameter gradient (recons / mu / log_var get none, so `_VAEStep.backward`
+    has nothing left to do)."""
+
+    @staticmethod
+    def forward(ctx, flat: Tensor, recons: Tensor, mu: Tensor, log_var: Tensor, plan, loss_kw: dict):
+        plan.run_elbo(L.stream_ptr(), **loss_kw)
+        ctx.plan = plan
+        loss, rl, kld = plan.out[0].clone(), plan.out[1].clone(), plan.out[2].clone()
+        ctx.mark_non_differentiable(rl, kld)
+        return loss, rl, kld
+
+    @staticmethod
+    def backward(ctx, g_loss: Optional[Tensor], g_rl, g_kld):
+        plan = ctx.plan
+        if g_loss is None:
+            return None, None, None, None, None, None
+        if plan.backward_done:
+            plan.reset_backward()
+        plan.backward_done = True
+        plan.head_coef.mul_(g_loss)
+        plan.kl_coef.mul_(g_loss)
+        plan.seed_fused(True)
+        try:
+            plan.backward(L.stream_ptr())
+        finally:
+            plan.seed_fused(False)
+        return plan.grads.clone(), None, None, None, None, None
 
 
 class _HipVAE(BaseVAE):
@@ -144,6 +187,33 @@ class _HipVAE(BaseVAE):
                           img_size=img_size, dtype=dtype, device=device, generator=gen)
         self.flat = nn.Parameter(self.net.params)      # shares storage with the kernels' buffer
         self._plans: Dict[int, StepPlan] = {}
+        self._last = None                              # (plan, input, recon, mu, log_var) of forward
+
+    def _loss_config(self) -> dict:
+        """StepPlan loss arguments of this model's loss_function."""
+        return dict(loss="iwae" if self.samples > 1 else "vanilla", samples=self.samples)
+
+    def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None):
+        """The whole training step of this model — forward, loss_function (vae_elbo_fwd), backward,
+        [gradient all-reduce], Adam — as one engine.TrainStep on the model's own parameters,
+        replayed from HIP graphs: the graph path of VAEXperiment.training_step + backward +
+        optimizer.step (experiment.fit(..., engine="graph"))."""
+        from .engine import FusedAdam, TrainStep
+        plan = StepPlan(self.net, batch, kld_weight=kld_weight, **self._loss_config())
+        opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
+        return TrainStep(self.net, plan, opt, graph=graph, process_group=process_group)
+
+    def _gpu_loss(self, args, loss: str, **kw):
+        """The loss dict terms from vae_elbo_fwd when `args` are exactly what this model's last
+        training forward returned (so its buffers hold them), else None (torch formula)."""
+        last = self._last
+        if last is None or not self.training or not torch.is_grad_enabled() or len(args) < 4:
+            return None
+        plan, inp, recon, mu, lv = last
+        if args[0] is not recon or args[1] is not inp or args[2] is not mu or args[3] is not lv:
+            return None
+        return _HipELBO.apply(self.flat, recon, mu, lv, plan, dict(loss=loss, **kw))
 
     def _plan(self, batch: int, training: Optional[bool] = None) -> StepPlan:
         """Launch plan for a batch size: train-mode BatchNorm (batch statistics, running-stat
@@ -207,6 +277,13 @@ class _HipVAE(BaseVAE):
         plan.decode(st)
         return plan.recon.clone()
 
+    def _remember(self, out):
+        """Keep the identity of a training forward's outputs for _gpu_loss (eval: forget)."""
+        if self.training and torch.is_grad_enabled() and out[0].grad_fn is not None:
+            self._last = (self._plan(out[1].shape[0]), out[1], out[0], out[2], out[3])
+        else:
+            self._last = None
+
     def _run(self, input: Tensor, eps: Optional[Tensor] = None):
         if not self.training:
             return self._eval_forward(input, eps)
@@ -230,12 +307,17 @@ class VanillaVAE(_HipVAE):
 
     def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
         recon, mu, log_var, _ = self._run(input, kwargs.get("eps"))
-        return [recon, input, mu, log_var]
+        out = [recon, input, mu, log_var]
+        self._remember(out)
+        return out
 
     def loss_function(self, *args, **kwargs) -> dict:
         """vanilla_vae.py:124-146."""
-        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
         kld_weight = kwargs['M_N']
+        g = self._gpu_loss(args, "vanilla", kld_weight=kld_weight)
+        if g is not None:
+            return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': g[2]}
+        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
         recons_loss = F.mse_loss(recons, input)
         kld_loss = torch.mean(-0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=1), dim=0)
         loss = recons_loss + kld_weight * kld_loss
@@ -259,13 +341,32 @@ class BetaVAE(_HipVAE):
 
     def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
         recon, mu, log_var, _ = self._run(input, kwargs.get("eps"))
-        return [recon, input, mu, log_var]
+        out = [recon, input, mu, log_var]
+        self._remember(out)
+        return out
+
+    def _loss_config(self) -> dict:
+        if self.loss_type not in ('H', 'B'):
+            raise ValueError('Undefined loss type.')
+        return dict(loss="betaH" if self.loss_type == 'H' else "betaB", beta=float(self.beta), gamma=float(self.gamma),
+                    max_capacity=float(self.C_max[0]), capacity_max_iter=float(self.C_stop_iter))
+
+    def fused_train_step(self, *args, **kwargs):
+        step = super().fused_train_step(*args, **kwargs)
+        step.plan.num_iter.fill_(float(self.num_iter))       # the capacity schedule continues
+        return step
 
     def loss_function(self, *args, **kwargs) -> dict:
         """beta_vae.py:129-152."""
         self.num_iter += 1
-        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
         kld_weight = kwargs['M_N']
+        if self.loss_type in ('H', 'B'):
+            g = self._gpu_loss(args, "betaH" if self.loss_type == 'H' else "betaB", kld_weight=kld_weight,
+                               beta=float(self.beta), gamma=float(self.gamma), c_max=float(self.C_max[0]),
+                               c_stop_iter=float(self.C_stop_iter), num_iter=self.num_iter)
+            if g is not None:
+                return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': g[2]}
+        recons, input, mu, log_var = args[0], args[1], args[2], args[3]
         recons_loss = F.mse_loss(recons, input)
         kld_loss = torch.mean(-0.5 * torch.sum(1 + log_var - mu ** 2 - log_var.exp(), dim=1), dim=0)
         if self.loss_type == 'H':
@@ -297,10 +398,15 @@ class IWAE(_HipVAE):
         eps_r = eps.reshape(B, S, D)
         z = eps_r * torch.exp(0.5 * lv_r) + mu_r
         eps_ret = (z - mu_r) / lv_r                         # iwae.py:126 (returned, unused by the loss)
-        return [recon.view(B, S, *recon.shape[1:]), input, mu_r, lv_r, z, eps_ret]
+        out = [recon.view(B, S, *recon.shape[1:]), input, mu_r, lv_r, z, eps_ret]
+        self._remember(out)
+        return out
 
     def loss_function(self, *args, **kwargs) -> dict:
         """iwae.py:129-160."""
+        g = self._gpu_loss(args, "iwae", kld_weight=kwargs['M_N'])
+        if g is not None:
+            return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': g[2]}
         recons, input, mu, log_var = args[0], args[1], args[2], args[3]
         input = input.repeat(self.num_samples, 1, 1, 1, 1).permute(1, 0, 2, 3, 4)
         kld_weight = kwargs['M_N']
@@ -397,6 +503,15 @@ class VQVAE(BaseVAE):
     def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
         recon, vq_loss = _VQStep.apply(self.flat, input, self)
         return [recon, input, vq_loss]
+
+    def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None):
+        """See _HipVAE.fused_train_step (the VQ-VAE loss ignores kld_weight, vq_vae.py:194-211)."""
+        from .engine import FusedAdam, TrainStep
+        from .vq import VQStepPlan
+        plan = VQStepPlan(self.net, batch, beta=self.beta)
+        opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
+        return TrainStep(self.net, plan, opt, graph=graph, process_group=process_group)
 
     def loss_function(self, *args, **kwargs) -> dict:
         """vq_vae.py:194-211."""

@@ -27,7 +27,6 @@ from .layout import Layout, default_init, reference_key_order, vanilla_layout
 SLOPE = 0.01         # nn.LeakyReLU default
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
-WORKSPACE_BYTES = 32 << 20
 
 
 class VAENet:
@@ -222,8 +221,6 @@ class StepPlan:
         self.bntab: Dict[str, torch.Tensor] = {
             b.prefix: torch.zeros(7 * b.channels, **f32) for b in net.layout.bns}
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
-        # split-K partial slabs (fp32), reused by every launch of the step on the stream
-        self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
         # side stream for the weight gradients (run_calls); None: one stream
@@ -236,6 +233,7 @@ class StepPlan:
             # agent-scope release in every workgroup, and lower GEMM occupancy).
             self._fuse_finalize(self.fwd_calls)
             self._fuse_finalize(self.bwd_calls)
+        size_workspaces(self, [self.fwd_calls, self.bwd_calls])
 
     # ------------------------------------------------------------------ helpers
     def g(self, name: str) -> int:
@@ -343,9 +341,6 @@ class StepPlan:
         calls[:] = out
 
     def _add(self, lst, fn, arg):
-        if isinstance(arg, (L.ConvArgs, L.LinearArgs, L.HeadArgs)):
-            arg.workspace = self.workspace.data_ptr()
-            arg.workspace_bytes = self.workspace.numel() * 4
         self._keep.append(arg)
         lst.append((fn, ctypes.byref(arg)))
 
@@ -455,6 +450,7 @@ class StepPlan:
         e.head_coef = self.head_coef.data_ptr()
         e.kl_coef = self.kl_coef.data_ptr()
         self.n_decode1 = len(F)
+        self.elbo_args = e
         if self.fused_loss:
             self._add(F, "vae_elbo_fwd", e)
 
@@ -480,6 +476,7 @@ class StepPlan:
         hb.dw = self.g("final_layer.3.weight")
         hb.db = self.g("final_layer.3.bias")
         self._add(Bw, "vae_head_bwd", hb)
+        self._head_bwd = hb
         # decoder, last block first
         sps = [2 * 2 ** i for i in range(len(r))]          # input spatial of each ConvT
         for i in reversed(range(len(r))):
@@ -518,6 +515,7 @@ class StepPlan:
         a.dmulv = self.dmulv.data_ptr()
         a.samples = self.S
         self._add(Bw, "vae_linear_bwd_data", a)
+        self._reparam_bwd = a
         f = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
         f.dy = self.g_h0.data_ptr()
         f.x = self.z.data_ptr()
@@ -605,9 +603,83 @@ class StepPlan:
         third = "KLD"
         return {"loss": o[0], "Reconstruction_Loss": o[1], third: o[2]}
 
+    # ------------------------------------------------------------------ drop-in ELBO
+    # A drop-in plan (fused_loss=False) can still take its loss on the GPU: the BaseVAE
+    # loss_function of vae_amd.models runs vae_elbo_fwd on the forward's own buffers (run_elbo)
+    # and seeds the backward from the kernel's coefficients (seed_fused) instead of autograd's
+    # dL/drecon and dL/d[mu|log_var].
+    LOSS_KINDS = {"vanilla": L.LOSS_VANILLA, "betaH": L.LOSS_BETA_H, "betaB": L.LOSS_BETA_B,
+                  "iwae": L.LOSS_IWAE}
+
+    def run_elbo(self, stream, loss: str, kld_weight: float, beta: float = 4.0, gamma: float = 1000.0,
+                 c_max: float = 25.0, c_stop_iter: float = 1e5, num_iter: Optional[int] = None):
+        """vae_elbo_fwd over this step's SSE and mu|log_var: out = [loss, Reconstruction_Loss, KLD
+        as the reference reports it, raw KLD]; per_img; head_coef / kl_coef = dloss/dsse_i and the
+        per-row KL gradient coefficient (the backward seeds)."""
+        e = self.elbo_args
+        e.kind = self.LOSS_KINDS[loss]
+        if (e.kind == L.LOSS_IWAE) != (self.S > 1):
+            raise ValueError(f"loss {loss!r} on a plan with {self.S} samples per image")
+        e.kld_weight, e.beta, e.gamma, e.c_max, e.c_stop_iter = kld_weight, beta, gamma, c_max, c_stop_iter
+        if num_iter is not None:
+            self.num_iter.fill_(float(num_iter))
+        L.call("vae_elbo_fwd", e, stream)
+
+    def seed_fused(self, on: bool):
+        """Backward seeding of a drop-in plan: on — from head_coef / kl_coef (run_elbo); off — from
+        grad_recon and dmulv as written by autograd (the caller's own loss)."""
+        if self.fused_loss or not self.training:
+            return
+        hb, rb = self._head_bwd, self._reparam_bwd
+        if on:
+            hb.coef, hb.grad_recon = self.head_coef.data_ptr(), None
+            rb.kl_coef = self.kl_coef.data_ptr()
+        else:
+            hb.coef, hb.grad_recon = None, self.grad_recon.data_ptr()
+            rb.kl_coef = None
+
+    def reset_backward(self):
+        """Zero what the backward accumulates (gradients, BatchNorm-backward sums, d[mu|logvar],
+        the padded first-layer dW) so the backward of the same forward can run again."""
+        self.grads.zero_()
+        for t in self.bnbwd.values():
+            t.zero_()
+        self.dmulv.zero_()
+        self.dw8.zero_()
+
 
 # Weight-gradient calls: nothing later in the backward reads their output (only the optimizer),
 # so they run on a side stream, concurrent with the data-gradient chain that is the critical path.
+def size_workspaces(plan, call_lists):
+    """Give a plan's calls their workspace: each call's need is queried from the library
+    (vaehip.h vae_*_workspace_size, which runs the call's own planning without launching), and
+    the calls of the main chain share one buffer sized to the largest need, the weight-gradient
+    calls of the side stream (run_calls) another — the two chains run concurrently.  A call
+    whose need is 0 gets no workspace (the same plan).  Sets plan.workspace / plan.workspace_side
+    and plan.workspace_need = {chain: bytes}."""
+    dev = plan.net.device
+    side_on = getattr(plan, "side", None) is not None
+    need = {"main": 0, "side": 0}
+    sized = []
+    for calls in call_lists:
+        for fn, ref in calls:
+            if fn not in L.WS_QUERY:
+                continue
+            arg = ref._obj
+            b = L.workspace_size(fn, arg)
+            chain = "side" if side_on and fn in SIDE_FNS else "main"
+            need[chain] = max(need[chain], b)
+            sized.append((arg, b, chain))
+    bufs = {c: torch.empty(max(1, (n + 3) // 4), dtype=torch.float32, device=dev) for c, n in need.items()}
+    for arg, b, chain in sized:
+        if b > 0:
+            arg.workspace = bufs[chain].data_ptr()
+            arg.workspace_bytes = bufs[chain].numel() * 4
+        else:
+            arg.workspace, arg.workspace_bytes = None, 0
+    plan.workspace, plan.workspace_side, plan.workspace_need = bufs["main"], bufs["side"], need
+
+
 SIDE_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_linear_bwd_filter",
                       "vae_unpad_accumulate"))     # (follows its padded weight gradient)
 

@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 from .layout import Layout, default_init, vq_layout, vq_param_spec
-from .net import SLOPE, WORKSPACE_BYTES, _pad4, run_calls
+from .net import SLOPE, _pad4, run_calls, size_workspaces
 
 NRES = 6             # ResidualLayers per stack (vq_vae.py:111, :138)
 
@@ -171,11 +171,11 @@ class VQStepPlan:
             self.dw8d = self.zero[o:o + r_[-1] * 16 * 8]; o += r_[-1] * 16 * 8
             self.db8d = self.zero[o:o + 8]; o += 8
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.workspace = torch.empty(WORKSPACE_BYTES // 4, **f32)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
         self.side = torch.cuda.Stream(device=dev) if concurrent else None     # weight gradients (run_calls)
         self._build()
+        size_workspaces(self, [self.fwd_calls, self.bwd_calls])
 
     # ------------------------------------------------------------------ helpers
     def g(self, name: str) -> int:
@@ -183,9 +183,6 @@ class VQStepPlan:
         return self.grads.data_ptr() + 4 * s.offset
 
     def _add(self, lst, fn, arg):
-        if isinstance(arg, L.ConvArgs):
-            arg.workspace = self.workspace.data_ptr()
-            arg.workspace_bytes = self.workspace.numel() * 4
         self._keep.append(arg)
         lst.append((fn, ctypes.byref(arg)))
 

@@ -59,3 +59,13 @@ def rel(a, b):
 
 def tol(dtype):
     return 2e-5 if dtype == torch.float32 else 2e-2
+
+
+def give_workspace(a, *fns):
+    """Query the workspace the calls `fns` need for args `a` (vae_*_workspace_size), allocate
+    it and point `a` at it; returns the buffer (keep it alive until the calls are done)."""
+    need = max(L.workspace_size(fn, a) for fn in fns)
+    ws = torch.empty(max(1, (need + 3) // 4), device="cuda")
+    a.workspace = ws.data_ptr()
+    a.workspace_bytes = ws.numel() * 4
+    return ws

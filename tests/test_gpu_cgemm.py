@@ -18,6 +18,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from gpu_util import give_workspace
+
 pytestmark = pytest.mark.gpu
 
 SLOPE = 0.01
@@ -107,11 +109,11 @@ def run_fwd(transposed, N, cin, cout, hw, stride, R, pad, kind, split=0, give_wt
     a = L.ConvArgs(dtype=L.BF16, n=N, h=hw, w=hw, c=cin, k=cout, p=P, q=P, r=R, stride=stride, pad=pad)
     a.x = yd.data_ptr(); a.x_xf = xf.x; a.wt = wd.data_ptr(); a.bias = bd.data_ptr(); a.y = out.data_ptr()
     a.y_sum = sums.data_ptr(); a.y_sumsq = sums.data_ptr() + 4 * cout
-    ws = torch.empty(8 << 20, device="cuda")
-    a.split_k = split; a.workspace = ws.data_ptr(); a.workspace_bytes = ws.numel() * 4
+    a.split_k = split
     if give_wt_t:
         wt = w.permute(1, 2, 3, 0).contiguous().to("cuda", torch.bfloat16)     # [cout][r][s][cin]
         a.wt_t = wt.data_ptr()
+    ws = give_workspace(a, "vae_convT2d_fwd" if transposed else "vae_conv2d_fwd")
     L.call("vae_convT2d_fwd" if transposed else "vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert relmax(nchw(out), ref) < OUT_TOL
@@ -209,11 +211,10 @@ def run_dgrad(transposed, N, cin, cout, hw, stride, R, pad, dy_kind, epi_kind, g
     a = L.ConvArgs(dtype=L.BF16, n=N, h=hw, w=hw, c=cin, k=cout, p=P, q=P, r=R, stride=stride, pad=pad)
     a.dy = gyd.data_ptr(); a.dy_xf = dyx.x; a.wt = wd.data_ptr(); a.dx = dx.data_ptr(); a.dx_epi = epx.x
     a.dx_dgamma = dgam.data_ptr(); a.dx_dbeta = dbet.data_ptr()
-    ws = torch.empty(8 << 20, device="cuda")
-    a.workspace = ws.data_ptr(); a.workspace_bytes = ws.numel() * 4
     if give_wt_t:
         wt = w.permute(1, 2, 3, 0).contiguous().to("cuda", torch.bfloat16)
         a.wt_t = wt.data_ptr()
+    ws = give_workspace(a, "vae_convT2d_bwd_data" if transposed else "vae_conv2d_bwd_data")
     L.call("vae_convT2d_bwd_data" if transposed else "vae_conv2d_bwd_data", ctypes.byref(a),
            torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()

@@ -1,20 +1,27 @@
-"""The data-parallel training step (engine.TrainStep with more than one rank) on a real GPU:
-two ranks on cuda:0 over gloo (one box has one GPU; RCCL needs distinct devices), HIP-graph
-segments per gradient bucket with the bucket all-reduces launched between them.
+"""The data-parallel training step (engine.TrainStep with more than one rank) on a real GPU, at
+BASELINE.json configs[2]'s per-GPU shape: BetaVAE-H (beta 4, models/beta_vae.py:129-152), 32
+images per rank.  Two ranks share cuda:0 over gloo (one box has one GPU; RCCL needs distinct
+devices); the backward runs as HIP-graph segments per gradient bucket with each bucket's
+all-reduce launched between them, and the loss terms ride in the last bucket.
 
-Checked against a single-process reference on the same device: each rank's shard run through
-its own plan, gradients averaged by hand, one Adam step — the two ranks' parameters after the
-data-parallel step must equal it (DDP semantics, run.py:86) and equal each other."""
+Checked against the CPU oracle, not against another HIP run: each rank's shard through
+oracle.train_step, the shard gradients averaged (DDP semantics, run.py:86), one Adam step.  Bars
+are the single-GPU parity bars (test_gpu_parity_shapes.py): averaged gradients within 1e-3
+relative norm per parameter (3e-3 BatchNorm affine), loss terms (the rank mean the reference logs
+with sync_dist, experiment.py:55) within 1e-4, BatchNorm buffers = rank 0's shard statistics
+(DDP broadcast_buffers), and the Adam update equal to the oracle's on every element whose
+averaged gradient is not within noise of zero."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-B, WORLD = 8, 2
+B, WORLD, SEED, M_N, LR = 32, 2, 1265, 2.5e-4, 0.005
 
 
 def _port():
@@ -25,9 +32,9 @@ def _port():
     return p
 
 
-def _inputs(rank):
-    g = torch.Generator().manual_seed(100 + rank)
-    return torch.rand(B, 3, 64, 64, generator=g), torch.randn(B, 128, generator=g)
+def _shard(rank):
+    from oracle import vae_oracle as O
+    return O.make_inputs(B, 128, 100 + rank)
 
 
 def _worker(rank, port, q):
@@ -36,16 +43,20 @@ def _worker(rank, port, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        from oracle import vae_oracle as O
         from vae_amd.engine import FusedAdam, TrainStep
         from vae_amd.net import StepPlan, VAENet
-        net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda:0", generator=torch.Generator().manual_seed(1265))
-        plan = StepPlan(net, B, loss="vanilla", kld_weight=2.5e-4)
-        step = TrainStep(net, plan, FusedAdam(net, lr=0.005), graph=True, nbuckets=4)
+        net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda:0")
+        net.load_reference_state_dict(O.make_params(O.vanilla_param_spec(), SEED))
+        plan = StepPlan(net, B, loss="betaH", kld_weight=M_N, beta=4.0)
+        step = TrainStep(net, plan, FusedAdam(net, lr=LR), graph=True, nbuckets=4)
         assert len(step.buckets) >= 2, step.buckets
-        x, eps = _inputs(rank)
+        x, eps = _shard(rank)
         step(x.cuda(), eps.cuda())
         torch.cuda.synchronize()
-        q.put((rank, net.params.cpu().clone(), net.running.cpu().clone(), plan.grads.cpu().clone(), step.buckets))
+        grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
+        q.put((rank, {k: v.cpu() for k, v in net.reference_state_dict().items()}, grads, step.loss_terms(),
+               plan.out[:3].tolist()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
@@ -53,7 +64,8 @@ def _worker(rank, port, q):
         q.put((rank, traceback.format_exc(), None, None, None))
 
 
-def test_data_parallel_step_matches_averaged_reference():
+def test_data_parallel_betaH_matches_oracle_shard_mean():
+    from oracle import vae_oracle as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
@@ -62,55 +74,45 @@ def test_data_parallel_step_matches_averaged_reference():
         p.start()
     res = {}
     for _ in range(WORLD):
-        r, params, run, grads, buckets = q.get(timeout=240)
-        assert not isinstance(params, str), params
-        res[r] = (params, run, grads)
+        r, state, grads, terms, local = q.get(timeout=240)
+        assert not isinstance(state, str), state
+        res[r] = (state, grads, terms, local)
     for p in procs:
         p.join(timeout=60)
-    # single-process reference: both shards' gradients, averaged, one Adam step
-    from vae_amd import _lib as L
-    from vae_amd.engine import FusedAdam
-    from vae_amd.net import StepPlan, VAENet
-    net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda:0", generator=torch.Generator().manual_seed(1265))
-    opt = FusedAdam(net, lr=0.005)
-    gsum = torch.zeros_like(net.params)
-    runs = []
+    sd = O.make_params(O.vanilla_param_spec(), SEED)
+    shards = [O.train_step("BetaVAE", sd, *_shard(r), M_N=M_N, lr=LR, loss_type="H", beta=4.0, do_adam=False)
+              for r in range(WORLD)]
+    # both ranks hold the same averaged gradient, parameters and (broadcast) buffers
+    for k in res[0][0]:
+        assert torch.equal(res[0][0][k], res[1][0][k]), k
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+    state, grads, terms, _ = res[0]
+    # loss terms: rank mean (sync_dist) on both ranks; each rank's own terms match its shard
     for r in range(WORLD):
-        plan = StepPlan(net, B, loss="vanilla", kld_weight=2.5e-4)
-        x, eps = _inputs(r)
-        plan.x.copy_(x)
-        plan.eps.copy_(eps)
-        run0 = net.running.clone()
-        st = L.stream_ptr()
-        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
-        plan.forward(st)
-        plan.backward(st)
-        torch.cuda.synchronize()
-        gsum += plan.grads
-        runs.append(net.running.clone())
-        net.running.copy_(run0)
-        opt.step.fill_(0)
-    gmean = gsum / WORLD
-    opt.step.fill_(0)
-    L.call("vae_step_begin", gmean.new_zeros(4).data_ptr(), 0, opt.step.data_ptr(), L.stream_ptr())
-    opt.apply(gmean)
-    torch.cuda.synchronize()
-    want = net.params.cpu()
-    p0 = VAENet(latent_dim=128, dtype=torch.float32, device="cpu" if False else "cuda:0",
-                generator=torch.Generator().manual_seed(1265)).params.cpu()
-    # after the exchange both ranks hold the same averaged gradient and take the same Adam step
-    assert torch.equal(res[0][2], res[1][2])
-    assert torch.equal(res[0][0], res[1][0])
-    params, run, grads = res[0]
-    gm = gmean.cpu()
-    # each bucket holds the mean of the two shards' gradients.  The bar allows the run-to-run
-    # spread of a train-mode BatchNorm backward at 8 images per shard (atomics order; SURVEY
-    # §8(c) measured 1.1e-4 CPU-vs-CPU at 16 images) and is far below the O(1) error of a bucket
-    # that was reduced early, late or not at all (the shards' gradients differ by ~100 %).
-    for e, s0, t in buckets:
-        err = float((grads[s0:t] - gm[s0:t]).norm() / gm[s0:t].norm().clamp_min(1e-30))
-        assert err < 2e-2, (e, s0, t, err)
-    du, dw = params - p0, want - p0
-    assert float((du - dw).norm() / dw.norm()) < 5e-2
-    assert torch.equal(res[0][1], res[1][1])              # rank-0 BatchNorm buffers (broadcast_buffers)
-    assert torch.allclose(run, runs[0].cpu(), rtol=1e-4, atol=1e-6)
+        for i, t in enumerate(("loss", "Reconstruction_Loss", "KLD")):
+            want = sum(s["loss"][t] for s in shards) / WORLD
+            assert abs(res[r][2][i] - want) <= 1e-4 * abs(want), (r, t, res[r][2][i], want)
+            assert abs(res[r][3][i] - shards[r]["loss"][t]) <= 1e-4 * abs(shards[r]["loss"][t]), (r, t)
+    gmean = {k: sum(s["grads"][k] for s in shards) / WORLD for k in shards[0]["grads"]}
+    worst = 0.0
+    for name, gr in gmean.items():
+        if name.endswith(".0.bias") and not name.startswith("final_layer.3"):
+            continue                                    # analytically zero under train-mode BN
+        err = float((grads[name].double() - gr.double()).norm() / gr.double().norm())
+        worst = max(worst, err)
+        bound = 3e-3 if name.endswith(".1.weight") or name.endswith(".1.bias") else 1e-3
+        assert err < bound, (name, err)
+    print(f"DP betaH 2x{B}: worst averaged-gradient rel-norm {worst:.2e}")
+    # one Adam step from zero state on the averaged gradient: lr * g / (|g| + eps) elementwise —
+    # compared where the oracle's averaged gradient is clear of the noise floor (sign-stable)
+    for name, gr in gmean.items():
+        if name.endswith(".0.bias") and not name.startswith("final_layer.3"):
+            continue
+        p0 = sd[name].double()
+        want = p0 - LR * gr.double() / (gr.double().abs() + 1e-8)
+        ok = gr.abs() > 1e-2 * gr.abs().max()
+        np.testing.assert_allclose(state[name].double()[ok].numpy(), want[ok].numpy(), rtol=0,
+                                   atol=1e-6 + 1e-3 * LR, err_msg=name)
+    for k, v in shards[0]["running"].items():           # rank 0's statistics (broadcast_buffers)
+        np.testing.assert_allclose(state[k].numpy(), v.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)

@@ -21,8 +21,12 @@ def _build(meta, dtype=torch.float32):
     return model
 
 
+@pytest.mark.parametrize("via", ["gpu_elbo", "torch_loss"])
 @pytest.mark.parametrize("case", CASES)
-def test_models_forward_loss_backward_adam(case):
+def test_models_forward_loss_backward_adam(case, via):
+    """via gpu_elbo: loss_function on forward's own list — vae_elbo_fwd and the fused seeds
+    (what VAEXperiment.training_step runs); via torch_loss: on views of those tensors — the
+    reference formula in torch, autograd's dL/drecon and dL/d[mu|log_var] seeding the backward."""
     meta, ref = load_case(case)
     sd, x, eps = case_inputs(meta)
     model = _build(meta)
@@ -31,7 +35,10 @@ def test_models_forward_loss_backward_adam(case):
     S = meta["samples"] or 1
     xd, ed = x.cuda(), eps.cuda().reshape(meta["batch"] * S, -1)
     results = model(xd, eps=ed)
+    if via == "torch_loss":
+        results = [t.view_as(t) for t in results]
     losses = model.loss_function(*results, M_N=meta["M_N"], optimizer_idx=0, batch_idx=0)
+    assert ("_HipELBO" in type(losses["loss"].grad_fn).__name__) == (via == "gpu_elbo"), type(losses["loss"].grad_fn)
     assert set(losses) == set(meta["loss"])
     for k, v in meta["loss"].items():
         got = float(losses[k])
@@ -219,3 +226,45 @@ def test_run_cli_synthetic_end_to_end(tmp_path):
     assert (ck / "last.ckpt").exists() and (ck / "best.ckpt").exists()
     sd = torch.load(ck / "last.ckpt", weights_only=True)["state_dict"]
     assert "model.encoder.0.0.weight" in sd and "model.final_layer.3.bias" in sd
+
+
+@pytest.mark.parametrize("arch", ["VanillaVAE", "BetaVAE", "IWAE"])
+def test_experiment_graph_engine_matches_eager(arch):
+    """fit(engine="graph") — one HIP-graph TrainStep per batch with FusedAdam — against the eager
+    drop-in (training_step -> GPU ELBO -> loss.backward -> torch.optim.Adam) from the same
+    parameters: the logged loss terms of the first step agree to fp32 rounding, and the first Adam
+    update to 1e-2 of its norm (elements whose gradient is within noise of zero may flip the sign
+    of their first step, lr*g/|g|)."""
+    from vae_amd.experiment import GraphedSteps, VAEXperiment
+    from vae_amd.models import vae_models
+    kw = dict(in_channels=3, latent_dim=128, dtype=torch.float32, device="cuda", seed=1265)
+    if arch == "BetaVAE":
+        kw.update(loss_type="H", beta=4)
+    params = {'LR': 0.005, 'weight_decay': 0.0, 'kld_weight': 2.5e-4}
+    B = 16
+    x = torch.rand(B, 3, 64, 64, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+    batch = (x, torch.zeros(B), [f"{i}.png" for i in range(B)])
+    runs = {}
+    for engine in ("eager", "graph"):
+        model = vae_models[arch](**kw)
+        model.train()
+        p0 = model.flat.detach().clone()
+        exp = VAEXperiment(model, params)
+        opt = exp.configure_optimizers()[0]
+        torch.manual_seed(11)                          # the same eps draws on both paths
+        torch.cuda.manual_seed(11)
+        if engine == "eager":
+            opt.zero_grad(set_to_none=True)
+            loss = exp.training_step(batch, 0)
+            assert "_HipELBO" in type(loss.grad_fn).__name__
+            loss.backward()
+            opt.step()
+        else:
+            GraphedSteps(exp, opt)(batch, 0)
+        torch.cuda.synchronize()
+        runs[engine] = ({k: float(v) for k, v in exp.logged.items()}, model.flat.detach() - p0)
+    (le, de), (lg, dg) = runs["eager"], runs["graph"]
+    assert set(le) == set(lg)
+    for k in le:
+        assert abs(le[k] - lg[k]) <= 1e-5 * abs(le[k]) + 1e-7, (k, le[k], lg[k])
+    assert float((dg - de).norm() / de.norm()) < 1e-2

@@ -9,7 +9,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from gpu_util import BNState, nhwc, rel, to_nchw, tol
+from gpu_util import BNState, give_workspace, nhwc, rel, to_nchw, tol
 
 pytestmark = pytest.mark.gpu
 
@@ -44,8 +44,8 @@ def test_conv2d_fwd_bnact_and_stats(dtype, cin, cout, hw, split):
     a = L.ConvArgs(dtype=L.dtype_code(dtype), n=N, h=hw, w=hw, c=cin, k=cout, p=hw // 2, q=hw // 2, r=3, stride=2, pad=1)
     a.x = bn.y_dev.data_ptr(); a.x_xf = bn.xf(); a.wt = wd.data_ptr(); a.bias = bd.data_ptr(); a.y = out.data_ptr()
     a.y_sum = s.data_ptr(); a.y_sumsq = s.data_ptr() + 4 * cout
-    ws = torch.empty(1 << 20, device="cuda")
-    a.split_k = split; a.workspace = ws.data_ptr(); a.workspace_bytes = ws.numel() * 4
+    a.split_k = split
+    ws = give_workspace(a, "vae_conv2d_fwd")
     L.call("vae_conv2d_fwd", ctypes.byref(a), _stream())
     torch.cuda.synchronize()
     assert rel(to_nchw(out), ref) < tol(dtype)
@@ -177,8 +177,8 @@ def test_conv2d_backward_bn(dtype, split):
     a.dx_dgamma = dgp.data_ptr(); a.dx_dbeta = dbp.data_ptr()
     a.x = bnp.y_dev.data_ptr(); a.x_xf = bnp.xf(L.X_BN_ACT)
     a.dw = dw.data_ptr(); a.db = db.data_ptr()
-    ws = torch.empty(1 << 20, device="cuda")
-    a.split_k = split; a.workspace = ws.data_ptr(); a.workspace_bytes = ws.numel() * 4
+    a.split_k = split
+    ws = give_workspace(a, "vae_conv2d_bwd_data", "vae_conv2d_bwd_filter")
     L.call("vae_conv2d_bwd_data", ctypes.byref(a), _stream())
     L.call("vae_conv2d_bwd_filter", ctypes.byref(a), _stream())
     torch.cuda.synchronize()
@@ -252,10 +252,8 @@ def test_head_fwd_bwd(dtype, fused):
     a.recon = recon.data_ptr(); a.sse = sse.data_ptr(); a.coef = coef.data_ptr()
     a.dx = dx.data_ptr(); a.dx_epi = bn.xf(aux=bn.y_dev); a.dx_dgamma = dgp.data_ptr(); a.dx_dbeta = dbp.data_ptr()
     a.dw = dw.data_ptr(); a.db = db.data_ptr()
-    ws = torch.empty(1 << 20, device="cuda")
     if fused:
-        a.workspace = ws.data_ptr()
-        a.workspace_bytes = ws.numel() * 4
+        ws = give_workspace(a, "vae_head_bwd")
     L.call("vae_head_fwd", ctypes.byref(a), _stream())
     if fused:
         L.call("vae_head_bwd", ctypes.byref(a), _stream())

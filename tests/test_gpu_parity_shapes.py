@@ -1,0 +1,199 @@
+"""Parity at the benchmarked shapes (BASELINE.json configs[1..4]) — the fp32 HIP step against the
+CPU oracle on the same seeded parameters and inputs:
+
+  VanillaVAE B=64            configs[1]   models/vanilla_vae.py:11-146
+  BetaVAE-H  B=32 (per GPU)  configs[2]   models/beta_vae.py:12-152 (loss_type H, beta 4)
+  IWAE       B=64, K=5       configs[3]   models/iwae.py:10-160 (decoder at 320 rows)
+  VQ-VAE     B=128           configs[4]   models/vq_vae.py:7-211 (32,768 codebook lookups)
+
+The golden-vector tests (test_gpu_step.py, test_gpu_vq.py) pin the same kernels at B<=16 against
+the reference's own modules; the oracle itself is pinned to those vectors (test_oracle_golden.py).
+
+Bars (north_star; SURVEY.md §8(c), measured CPU 8-thread vs 1-thread spread of 1.1e-4 on the
+gradient norms): ELBO terms within 1e-4 relative; mu / log_var / reconstructions within 1e-4 of
+their scale; per-image MSE within 1e-4 relative; every parameter gradient within 1e-3 relative
+norm (3e-3 for the BatchNorm affine gradients, reductions with ~100x cancellation); BatchNorm
+running statistics within 1e-4.
+
+VQ index exactness: the codebook index of every one of the 32,768 rows equals the oracle's
+(torch.argmin of the same fp32 expansion Σz²+ΣE²−2z·E, first minimum) wherever the oracle's gap
+between the best and second-best distance exceeds 1e-6 of the row's distance scale |z|²+|e|²
+(an fp32 rounding of that expansion is ~6e-8 of it); rows under that are reported, and the rest of
+the step is teacher-forced with the GPU's indices."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1265
+
+
+def _is_bn_affine(name):
+    return name.endswith(".1.weight") or name.endswith(".1.bias")
+
+
+def _pre_bn_bias(name):
+    return name.endswith(".0.bias") and not name.startswith("final_layer.3")
+
+
+def _hip_vanilla_step(loss, batch, samples, M_N, sd, x, eps, lr=0.005):
+    from vae_amd import _lib as L
+    from vae_amd.engine import FusedAdam
+    from vae_amd.net import StepPlan, VAENet
+    net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda")
+    net.load_reference_state_dict(sd)
+    plan = StepPlan(net, batch, loss=loss, kld_weight=M_N, samples=samples or 1, beta=4.0)
+    opt = FusedAdam(net, lr=lr)
+    plan.x.copy_(x)
+    plan.eps.copy_(eps.reshape(plan.eps.shape))
+    st = L.stream_ptr()
+    L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
+    plan.forward(st)
+    plan.backward(st)
+    torch.cuda.synchronize()
+    return net, plan, opt
+
+
+def _check_grads(grads, want, skip=lambda n: False):
+    report = []
+    for name, gr in want.items():
+        g = grads[name]
+        if skip(name):
+            continue
+        err = float((g.double() - gr.double()).norm() / gr.double().norm().clamp_min(1e-30))
+        report.append((err, name))
+        bound = 3e-3 if _is_bn_affine(name) else 1e-3
+        assert err < bound, (name, err)
+    return max(report)
+
+
+@pytest.mark.parametrize("arch,loss,batch,samples,M_N", [
+    ("VanillaVAE", "vanilla", 64, None, 2.5e-4),       # configs/vae/vae.yaml kld_weight
+    ("BetaVAE", "betaH", 32, None, 2.5e-4),            # configs/vae/bhvae.yaml (H, beta 4)
+    ("IWAE", "iwae", 64, 5, 2.5e-4),                   # configs/vae/iwae.yaml (K=5)
+])
+def test_step_matches_oracle_at_bench_shape(arch, loss, batch, samples, M_N):
+    from oracle import vae_oracle as O
+    sd = O.make_params(O.vanilla_param_spec(), SEED)
+    x, eps = O.make_inputs(batch, 128, SEED + batch, samples=samples)
+    net, plan, opt = _hip_vanilla_step(loss, batch, samples, M_N, sd, x, eps)
+    o = O.train_step(arch, sd, x, eps, M_N=M_N, lr=0.005, loss_type="H", beta=4.0, do_adam=False)
+    out = plan.out.cpu().tolist()
+    got = {"loss": out[0], "Reconstruction_Loss": out[1], "KLD": out[2]}
+    for k in ("loss", "Reconstruction_Loss", "KLD"):
+        v = o["loss"][k]
+        assert abs(got[k] - v) <= 1e-4 * abs(v), (k, got[k], v)
+    S = samples or 1
+    recon = plan.recon.cpu()
+    if S > 1:
+        recon = recon.view(batch, S, 3, 64, 64)
+    np.testing.assert_allclose(recon.numpy(), o["recon"].numpy(), rtol=0, atol=1e-4)
+    per_img = plan.per_img.cpu().view(batch, S) if S > 1 else plan.per_img.cpu()
+    np.testing.assert_allclose(per_img.numpy(), o["per_img_mse"].numpy(), rtol=1e-4)
+    mu, lv = plan.mulv[:batch, :128].cpu(), plan.mulv[:batch, 128:].cpu()
+    np.testing.assert_allclose(mu.numpy(), o["mu"].numpy(), rtol=0, atol=1e-4 * float(o["mu"].abs().max()))
+    np.testing.assert_allclose(lv.numpy(), o["log_var"].numpy(), rtol=0, atol=1e-4 * float(o["log_var"].abs().max()))
+    grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
+    for name, gr in o["grads"].items():
+        if _pre_bn_bias(name):     # analytically zero under train-mode BN: bound by the weight grad
+            assert float(grads[name].abs().max()) <= 1e-4 * float(o["grads"][name[:-4] + "weight"].abs().max()) + 1e-7
+    worst = _check_grads(grads, o["grads"], skip=_pre_bn_bias)
+    print(f"{arch} B={batch}: worst grad rel-norm {worst[0]:.2e} ({worst[1]})")
+    run = {k: v.cpu() for k, v in net.reference_state_dict().items()}
+    for k, v in o["running"].items():
+        np.testing.assert_allclose(run[k].numpy(), v.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
+
+
+def test_vq_step_matches_oracle_at_bench_shape():
+    """VQ-VAE B=128: indices on all 32,768 rows, then the teacher-forced step."""
+    from oracle import vae_oracle as O
+    from vae_amd import _lib as L
+    from vae_amd.engine import FusedAdam
+    from vae_amd.vq import VQNet, VQStepPlan
+    B = 128
+    sd = O.make_params(O.vq_param_spec(), SEED)
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(SEED + B))
+    net = VQNet(dtype=torch.float32, device="cuda")
+    net.load_reference_state_dict(sd)
+    plan = VQStepPlan(net, B, beta=0.25)
+    opt = FusedAdam(net, lr=0.005)
+    plan.x.copy_(x)
+    st = L.stream_ptr()
+    L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
+    plan.forward(st)
+    plan.backward(st)
+    torch.cuda.synchronize()
+    idx = plan.indices.cpu()
+    assert idx.numel() == B * 16 * 16
+    # untouched oracle (its own argmin) for the index check
+    with torch.no_grad():
+        P = {k: v for k, v in sd.items()}
+        enc = O.vq_encode(P, x, O.VQ_HIDDEN)
+        E = P["vq_layer.embedding.weight"]
+        _, _, want, gap = O.vq_quantize(enc, E, 0.25)
+        flat = enc.permute(0, 2, 3, 1).reshape(-1, E.shape[1])
+        scale = (flat ** 2).sum(1) + (E[want] ** 2).sum(1)
+    clear = gap > 1e-6 * scale
+    n_clear = int(clear.sum())
+    mism = int((idx[clear] != want[clear]).sum())
+    print(f"VQ B=128: {n_clear} of {idx.numel()} rows above the gap bar, {idx.numel() - n_clear} near-ties, "
+          f"{int((idx != want).sum())} rows differ in total")
+    assert n_clear > 0.99 * idx.numel()
+    assert mism == 0, mism
+    o = O.train_step("VQVAE", sd, x, M_N=0.0, lr=0.005, vq_beta=0.25, vq_indices=idx, do_adam=False)
+    got = plan.loss_dict()
+    for k in ("loss", "Reconstruction_Loss", "VQ_Loss"):
+        assert abs(got[k] - o["loss"][k]) <= 1e-4 * abs(o["loss"][k]), (k, got[k], o["loss"][k])
+    np.testing.assert_allclose(plan.recon.cpu().numpy(), o["recon"].numpy(), rtol=0, atol=1e-4)
+    np.testing.assert_allclose(plan.per_img.cpu().numpy(), o["per_img_mse"].numpy(), rtol=1e-4)
+    grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
+    worst = _check_grads(grads, o["grads"])
+    print(f"VQ B=128: worst grad rel-norm {worst[0]:.2e} ({worst[1]})")
+
+
+def test_vq_three_steps_follow_oracle():
+    """Three VQ-VAE steps with Adam state (FusedAdam vs torch.optim.Adam) on one fixed batch, as
+    bench.py runs them.  After the first Adam step the trajectory is chaotic (every weight moves by
+    ~lr; SURVEY §8(c) measured 6e-4 -> 1e-2 CPU-vs-CPU over steps 2-3 for VanillaVAE), so steps 2-3
+    are checked teacher-forced: the oracle restarts from the HIP parameters, Adam moments and codes
+    of that step and must reproduce the HIP step's loss terms (1e-4) and gradients (1e-3)."""
+    from oracle import vae_oracle as O
+    from vae_amd import _lib as L
+    from vae_amd.engine import FusedAdam
+    from vae_amd.vq import VQNet, VQStepPlan
+    B, lr = 32, 0.005
+    sd = O.make_params(O.vq_param_spec(), SEED)
+    x = torch.rand(B, 3, 64, 64, generator=torch.Generator().manual_seed(SEED + 1))
+    net = VQNet(dtype=torch.float32, device="cuda")
+    net.load_reference_state_dict(sd)
+    plan = VQStepPlan(net, B, beta=0.25)
+    opt = FusedAdam(net, lr=lr)
+    plan.x.copy_(x)
+    st = L.stream_ptr()
+    for k in range(3):
+        before = {n: v.cpu().clone() for n, v in net.reference_state_dict().items()}
+        m0 = {n: v.cpu().clone() for n, v in net.layout.export_reference(opt.m).items()}
+        v0 = {n: v.cpu().clone() for n, v in net.layout.export_reference(opt.v).items()}
+        L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
+        plan.forward(st)
+        plan.backward(st)
+        opt.apply(plan.grads)
+        torch.cuda.synchronize()
+        idx = plan.indices.cpu()
+        o = O.train_step("VQVAE", before, x, M_N=0.0, lr=lr, vq_beta=0.25, vq_indices=idx, do_adam=False)
+        got = plan.loss_dict()
+        for t in ("loss", "Reconstruction_Loss", "VQ_Loss"):
+            assert abs(got[t] - o["loss"][t]) <= 1e-4 * abs(o["loss"][t]), (k, t, got[t], o["loss"][t])
+        grads = {n: g.cpu() for n, g in net.layout.export_reference(plan.grads).items()}
+        _check_grads(grads, o["grads"])
+        # Adam with the carried moments: torch.optim.Adam loaded with the HIP state of this step
+        after = {n: v.cpu() for n, v in net.reference_state_dict().items()}
+        for n, g in grads.items():
+            p = before[n].clone().requires_grad_(True)
+            ta = torch.optim.Adam([p], lr=lr)
+            p.grad = g.clone()
+            ta.state[p] = {"step": torch.tensor(float(k)), "exp_avg": m0[n].clone(), "exp_avg_sq": v0[n].clone()}
+            ta.step()
+            np.testing.assert_allclose(after[n].numpy(), p.detach().numpy(), rtol=0, atol=2e-6 + 1e-5 * lr,
+                                       err_msg=f"step {k + 1} {n}")

@@ -184,7 +184,7 @@ def test_recon_kernel(dtype):
 def test_conv_stride1_bwd_data_residual_act(dtype, r, pad):
     """conv2d_bwd_data at stride 1 (the ResidualLayer convs, vq_vae.py:62-66): dx = W^T * dy + skip,
     times lrelu'(x_pre) — against torch autograd in fp32 (bf16 runs the flipped-weight conv path)."""
-    from gpu_util import nhwc, to_nchw
+    from gpu_util import give_workspace, nhwc, to_nchw
     from vae_amd import _lib as L
     g = torch.Generator().manual_seed(11 + r)
     n, hw, c, k = 2, 8, 32, 64
@@ -200,12 +200,11 @@ def test_conv_stride1_bwd_data_residual_act(dtype, r, pad):
     wn = w.permute(0, 2, 3, 1).contiguous().to(device="cuda", **dev)
     dy_d, skip_d, xp_d = nhwc(dy, dtype), nhwc(skip, dtype), nhwc(x_pre, dtype)
     dx = torch.empty_like(xp_d)
-    ws = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
     a = L.ConvArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=c, k=k, p=hw, q=hw, r=r, stride=1, pad=pad)
     a.dy, a.wt, a.dx, a.residual = dy_d.data_ptr(), wn.data_ptr(), dx.data_ptr(), skip_d.data_ptr()
     a.dx_epi = L.Xform(kind=L.X_ACT, channels=c, slope=0.01)
     a.dx_epi.aux = xp_d.data_ptr()
-    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    ws = give_workspace(a, "vae_conv2d_bwd_data")
     L.call("vae_conv2d_bwd_data", a, L.stream_ptr())
     torch.cuda.synchronize()
     got = to_nchw(dx)

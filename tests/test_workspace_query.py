@@ -1,0 +1,97 @@
+"""Workspace queries of the C ABI (vaehip.h vae_*_workspace_size) — CPU only: a
+query runs the entry point's own planning with the launches switched off, so it needs no device,
+and a call whose workspace is short fails in planning, before anything is launched.
+
+Shapes are the VanillaVAE B=64 layers (models/vanilla_vae.py:25-75): the deep-K / small-M encoder
+tail and the linears split K over workgroups (fp32 partial slabs in the workspace), the big-M
+early layers do not."""
+import ctypes
+
+import pytest
+
+from vae_amd import _lib as L
+
+FAKE = 1 << 24          # aligned, never dereferenced (nothing launches)
+
+
+def _conv(n, h, c, k, stride=2, r=3, pad=1, dtype=None):
+    p = h // stride
+    a = L.ConvArgs(dtype=L.BF16 if dtype is None else dtype, n=n, h=h, w=h, c=c, k=k, p=p, q=p, r=r,
+                   stride=stride, pad=pad)
+    a.x = a.wt = a.y = FAKE
+    a.x_xf = L.Xform(kind=L.X_NONE, channels=c)
+    return a
+
+
+def _need(fn, a):
+    return L.workspace_size(fn, a)
+
+
+def test_split_k_layers_need_workspace_and_big_layers_none():
+    deep = _conv(64, 4, 256, 512)            # encoder.4: M = 64*2*2 = 256 rows, K = 2304
+    wide = _conv(64, 64, 8, 32)              # encoder.0 (padded RGB): M = 64*32*32 rows
+    nd, nw = _need("vae_conv2d_fwd", deep), _need("vae_conv2d_fwd", wide)
+    assert nd > 0 and nd % 4 == 0
+    assert nd >= 2 * 256 * 512 * 4          # at least two fp32 partial slabs of the output
+    assert nw == 0
+
+
+def test_query_is_deterministic_and_ignores_workspace_fields():
+    a = _conv(64, 4, 256, 512)
+    n0 = _need("vae_conv2d_fwd", a)
+    a.workspace, a.workspace_bytes = FAKE, 7
+    assert _need("vae_conv2d_fwd", a) == n0
+    assert a.workspace_bytes == 7            # the caller's struct is not modified
+
+
+def test_short_workspace_is_an_error_not_a_silent_downgrade():
+    lib = L.load()
+    a = _conv(64, 4, 256, 512)
+    need = _need("vae_conv2d_fwd", a)
+    a.workspace, a.workspace_bytes = FAKE, need - 4
+    rc = lib.vae_conv2d_fwd(ctypes.byref(a), None)
+    assert rc == -1
+    msg = lib.vae_last_error()
+    assert b"workspace" in msg and str(need).encode() in msg
+
+
+def test_explicit_split_without_workspace_is_rejected():
+    lib = L.load()
+    a = _conv(64, 4, 256, 512)
+    a.split_k = 4
+    rc = lib.vae_conv2d_fwd(ctypes.byref(a), None)
+    assert rc == -1 and b"split_k" in lib.vae_last_error()
+
+
+def test_staged_weight_copy_counts_in_the_need():
+    """convT2d_fwd without a caller-supplied swapped weight copy (wt_t) stages it at the end of the
+    workspace: the need includes its bf16 bytes; with wt_t it does not."""
+    a = _conv(64, 4, 256, 128)               # decoder.1 convT 256 -> 128 at 4x4 -> 8x8
+    a.p = a.q = 8
+    n_stage = _need("vae_convT2d_fwd", a)
+    a.wt_t = FAKE
+    n_given = _need("vae_convT2d_fwd", a)
+    wbytes = 128 * 9 * 256 * 2
+    assert n_stage >= n_given + wbytes
+
+
+@pytest.mark.parametrize("op", ["vae_head_bwd", "vae_head_bwd_filter"])
+def test_head_filter_partials_need_workspace(op):
+    a = L.HeadArgs(dtype=L.BF16, n=64, h=64, w=64, c=32, samples=1)
+    a.x = a.wt = a.bias = a.target = a.recon = a.sse = a.coef = a.dx = a.dw = a.db = FAKE
+    a.dx_dgamma = a.dx_dbeta = FAKE
+    a.x_xf = L.Xform(kind=L.X_BN_ACT, channels=32, count=1.0, slope=0.01)     # lrelu(BN(x)), as in the net
+    a.dx_epi = L.Xform(kind=L.X_BN_ACT, channels=32, count=1.0, slope=0.01)
+    for f in ("sum", "sumsq", "gamma", "beta", "aux"):
+        setattr(a.x_xf, f, FAKE)
+        setattr(a.dx_epi, f, FAKE)
+    n = _need(op, a)
+    assert n > 0 and n % (64 * 4) == 0          # one fp32 row of partials per workgroup
+    assert _need("vae_head_fwd", a) == 0
+
+
+def test_bad_op_is_rejected():
+    lib = L.load()
+    a = _conv(4, 8, 8, 8)
+    out = ctypes.c_size_t(0)
+    assert lib.vae_conv2d_workspace_size(ctypes.byref(a), 9, ctypes.byref(out)) == -1
