@@ -108,6 +108,66 @@ class VAEXperiment:
         self.log_dict({f"val_{k}": v for k, v in val_loss.items()})
         return val_loss
 
+    # ------------------------------------------------------------------ test
+    def test_step(self, batch, batch_idx):
+        """experiment.py:155-217: the batch's loss terms (logged as test_*), then for every image
+        the loss of that image alone (x1000, with running min/max in loss_stats) and the original
+        and reconstruction resized to 256x256 (bilinear, align_corners=False) into test_data.
+
+        The reference runs one extra forward per image at batch 1.  Under model.eval() BatchNorm
+        uses the running statistics, so an image's outputs do not depend on the rest of its batch:
+        here one batched forward serves all images and each image's loss is loss_function on its
+        slice of the outputs (the same formula on the same values).  VQ-VAE's vq_loss is a batch
+        scalar in the forward's outputs, so it keeps the per-image forwards."""
+        imgs, labels, img_names = batch
+        self.curr_device = imgs.device
+        if not hasattr(self, 'test_data'):
+            self.test_data = []
+            self.loss_stats = {k: {'min': float('inf'), 'max': float('-inf')}
+                               for k in ('total_loss', 'recon_loss', 'feature_loss')}
+        kw = dict(M_N=self.params['kld_weight'], optimizer_idx=0, batch_idx=batch_idx)
+        B = imgs.shape[0]
+        with torch.no_grad():
+            results = self.forward(imgs, labels=labels)
+            test_loss = self.model.loss_function(*results, **kw)
+            self.log_dict({f"test_{k}": v for k, v in test_loss.items()})
+            sliceable = all(torch.is_tensor(r) and r.dim() > 0 and r.shape[0] == B for r in results)
+            for i in range(B):
+                if sliceable:
+                    single_results = [r[i:i + 1] for r in results]
+                else:
+                    single_results = self.forward(imgs[i:i + 1], labels=labels[i:i + 1] if labels is not None else None)
+                single_loss = self.model.loss_function(*single_results, **kw)
+                recons = self.ensure_4_dims(single_results[0])
+                total = float(single_loss['loss']) * 1000
+                recon = float(single_loss['Reconstruction_Loss']) * 1000
+                feat = float(single_loss['feature_loss']) * 1000 if 'feature_loss' in single_loss else None
+                for key, v in (('total_loss', total), ('recon_loss', recon), ('feature_loss', feat)):
+                    if v is not None:
+                        st = self.loss_stats[key]
+                        st['min'], st['max'] = min(st['min'], v), max(st['max'], v)
+                orig = F.interpolate(imgs[i:i + 1], size=self.test_output_size, mode='bilinear', align_corners=False)
+                rec = F.interpolate(recons, size=self.test_output_size, mode='bilinear', align_corners=False)
+                self.test_data.append({'name': img_names[i], 'original': orig.cpu(), 'reconstruction': rec.cpu(),
+                                       'total_loss': total, 'recon_loss': recon, 'feature_loss': feat})
+        return test_loss
+
+    def normalize_loss(self, loss_value, loss_type):
+        """experiment.py:359-374: the fraction of test images whose loss is <= loss_value."""
+        key = {'total_loss': 'total_loss', 'recon_loss': 'recon_loss', 'feature_loss': 'feature_loss'}[loss_type]
+        vals = [d[key] for d in self.test_data if d[key] is not None]
+        return sum(1 for x in vals if x <= loss_value) / len(vals)
+
+    def ensure_4_dims(self, t: Tensor) -> Tensor:
+        """experiment.py:376-392: [B,S,C,H,W] -> the first sample; [B,_,S,C,H,W] -> [:, 0, 0]."""
+        if t.dim() == 6:
+            return t[:, 0, 0]
+        if t.dim() == 5:
+            return t[:, 0]
+        if t.dim() == 3:
+            return t.unsqueeze(0)
+        return t
+
     def configure_optimizers(self):
         """experiment.py:304-357: Adam(lr, weight_decay); ReduceLROnPlateau on val_loss when
         adaptive_lr, else ExponentialLR(scheduler_gamma) stepped per epoch; a second optimizer

@@ -136,6 +136,7 @@ def main(argv=None) -> Dict[str, float]:
     config = load_config(args)
     import torch.distributed as dist
     from .dp import allreduce_mean, broadcast_buffers
+    from .data import ImageSet, VAEDataset
     from .experiment import VAEXperiment
     from .models import vae_models
 
@@ -153,30 +154,28 @@ def main(argv=None) -> Dict[str, float]:
     dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
     model = vae_models[name](**mp, dtype=dtype, device=f"cuda:{local}", seed=seed)
     experiment = VAEXperiment(model, config['exp_params'])
-    dpar = config['data_params']
+    dpar = dict(config['data_params'])
     size = dpar.get('patch_size', 64)
+    size = size if isinstance(size, int) else size[0]
+    dev = torch.device("cuda", local)
     if args.synthetic:
         g = torch.Generator().manual_seed(seed)
         imgs = torch.rand(args.synthetic, 3, size, size, generator=g)
         names = [f"{i}.png" for i in range(args.synthetic)]
         cut = int(0.9 * args.synthetic)
-        train, val = (imgs[:cut], names[:cut]), (imgs[cut:], names[cut:])
-        test = val
+        dm = VAEDataset("", **{k: v for k, v in dpar.items() if k not in ("data_path", "train_dataset", "test_dataset")},
+                        train_dataset=None, test_dataset=None, device=dev, rank=rank, world=world)
+        dm.train_set = ImageSet(imgs[:cut].to(dev), names[:cut])
+        dm.val_set = dm.test_set = ImageSet(imgs[cut:].to(dev), names[cut:])
     else:
-        root = dpar['data_path']
-        if args.train_dataset:
-            tr, va = folder_split(os.path.join(root, args.train_dataset), 0.9, seed)
-            train = (torch.stack([_load_png(f, size) for f in tr]), [os.path.basename(f) for f in tr])
-            val = (torch.stack([_load_png(f, size) for f in va]), [os.path.basename(f) for f in va])
-        else:
-            train = val = None
-        if args.test_dataset:
-            _, te = folder_split(os.path.join(root, args.test_dataset), 0.0, seed)
-            test = (torch.stack([_load_png(f, size) for f in te]), [os.path.basename(f) for f in te])
-        else:
-            test = val
-    dev = torch.device("cuda", local)
-    to_dev = lambda bl: [(x.to(dev), y, n) for x, y, n in bl]
+        # dataset.py VAEDataset(**data_params) with the -r / -t folders (run.py:71-76), resident on
+        # the device; split_images uses Python's `random`, seeded above like seed_everything
+        dm = VAEDataset(**{k: v for k, v in dpar.items() if k not in ("train_dataset", "test_dataset")},
+                        train_dataset=args.train_dataset, test_dataset=args.test_dataset, device=dev,
+                        rank=rank, world=world)
+        dm.setup()
+    experiment.datamodule = dm
+    train = dm.train_set
     log_dir = os.path.join(config['logging_params']['save_dir'], config['exp_name'], "version_0")
     ck_dir = os.path.join(log_dir, "checkpoints")
     result: Dict[str, float] = {}
@@ -194,8 +193,7 @@ def main(argv=None) -> Dict[str, float]:
         for epoch in range(epochs):
             model.train()
             sums: Dict[str, float] = {}
-            tb = to_dev(batches(*train, dpar['train_batch_size'], True, seed + epoch, rank, world))
-            for i, batch in enumerate(tb):
+            for i, batch in enumerate(dm.train_dataloader()):
                 optims[0].zero_grad(set_to_none=True)
                 loss = experiment.training_step(batch, i)
                 loss.backward()
@@ -204,11 +202,11 @@ def main(argv=None) -> Dict[str, float]:
                     broadcast_buffers(model.net.running)
                 optims[0].step()
                 step += 1
+            dm.on_epoch_end()                                   # difficulty sampler update
             for k, v in experiment.logged.items():
                 sums[k] = float(v)
             model.eval()
-            vb = to_dev(batches(*val, dpar.get('val_batch_size', 64), False, seed, rank, world))
-            vals = [experiment.validation_step(b, i) for i, b in enumerate(vb)]
+            vals = [experiment.validation_step(b, i) for i, b in enumerate(dm.val_dataloader())]
             if vals:
                 for k in vals[0]:
                     sums[f"val_{k}"] = sum(float(v[k]) for v in vals) / len(vals)
@@ -230,11 +228,13 @@ def main(argv=None) -> Dict[str, float]:
     if (args.test_dataset is not None or args.synthetic) and checkpoint_path and os.path.exists(checkpoint_path):
         load_checkpoint(checkpoint_path, model)
         model.eval()
-        tb = to_dev(batches(*test, 16, False, seed, rank, world))
-        outs = [experiment.validation_step(b, i) for i, b in enumerate(tb)]
+        outs = [experiment.test_step(b, i) for i, b in enumerate(dm.test_dataloader())]
         if outs and rank == 0:
             result.update({f"test_{k}": sum(float(o[k]) for o in outs) / len(outs) for k in outs[0]})
-            print("test: " + ", ".join(f"{k}={v:.5f}" for k, v in sorted(result.items()) if k.startswith("test_")))
+            st = experiment.loss_stats['total_loss']
+            print("test: " + ", ".join(f"{k}={v:.5f}" for k, v in sorted(result.items()) if k.startswith("test_"))
+                  + f"; per-image total loss x1000 in [{st['min']:.3f}, {st['max']:.3f}] over "
+                  f"{len(experiment.test_data)} images")
     if world > 1 and dist.is_initialized():
         dist.destroy_process_group()
     if rank == 0:

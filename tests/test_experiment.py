@@ -125,3 +125,31 @@ def test_fit_validates_in_eval_mode():
     assert m.modes == [False, False]
     assert torch.equal(rm, m.bn.running_mean) and torch.equal(rv, m.bn.running_var)
     assert m.training                           # back in train mode afterwards
+
+
+def test_test_step_per_image_losses_match_per_image_forwards():
+    """test_step (experiment.py:155-217): the per-image losses from one batched forward equal the
+    reference's per-image forwards (the stand-in has no cross-sample coupling, as eval-mode BN),
+    x1000, min/max tracked, 256x256 bilinear resizes, batch terms logged as test_*."""
+    m = TinyAE()
+    exp = VAEXperiment(m, dict(PARAMS))
+    batch = _batch(3, B=5)
+    out = exp.test_step(batch, 0)
+    assert set(exp.logged) == {'test_loss', 'test_Reconstruction_Loss', 'test_KLD'}
+    assert len(exp.test_data) == 5
+    imgs = batch[0]
+    for i, d in enumerate(exp.test_data):
+        single = m(imgs[i:i + 1])
+        want = m.loss_function(*single, M_N=0.5)
+        assert abs(d['total_loss'] - float(want['loss']) * 1000) < 1e-3
+        assert abs(d['recon_loss'] - float(want['Reconstruction_Loss']) * 1000) < 1e-3
+        assert d['feature_loss'] is None and d['name'] == batch[2][i]
+        assert tuple(d['original'].shape) == (1, 3, 256, 256)
+        ref = F.interpolate(single[0].detach(), size=(256, 256), mode='bilinear', align_corners=False)
+        assert torch.allclose(d['reconstruction'], ref, atol=1e-6)
+    tl = [d['total_loss'] for d in exp.test_data]
+    assert exp.loss_stats['total_loss'] == {'min': min(tl), 'max': max(tl)}
+    assert abs(exp.normalize_loss(max(tl), 'total_loss') - 1.0) < 1e-12
+    assert float(out['loss']) > 0
+    # IWAE-shaped reconstructions: the first sample
+    assert exp.ensure_4_dims(torch.zeros(2, 5, 3, 4, 4)).shape == (2, 3, 4, 4)
