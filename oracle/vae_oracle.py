@@ -72,6 +72,21 @@ def vanilla_param_spec(in_channels: int = 3, latent_dim: int = 128,
     return spec
 
 
+def ae_param_spec(in_channels: int = 3, latent_dim: int = 128,
+                  hidden_dims: Optional[List[int]] = None) -> List[Tuple[str, tuple, str]]:
+    """models/autoencoder.py:16-93 in state_dict order: the VanillaVAE stack with one `fc`
+    (Linear 4C -> D, :50) in place of fc_mu / fc_var (five stride-2 layers, the configs' case)."""
+    spec = []
+    for name, shape, kind in vanilla_param_spec(in_channels, latent_dim, hidden_dims):
+        if name == "fc_mu.weight":
+            spec.append(("fc.weight", shape, kind))
+        elif name == "fc_mu.bias":
+            spec.append(("fc.bias", shape, kind))
+        elif not name.startswith("fc_var."):
+            spec.append((name, shape, kind))
+    return spec
+
+
 def _bn_spec(pre: str, c: int):
     return [(f"{pre}.weight", (c,), "bn_w"), (f"{pre}.bias", (c,), "bn_b"),
             (f"{pre}.running_mean", (c,), "bn_rm"), (f"{pre}.running_var", (c,), "bn_rv"),
@@ -209,6 +224,34 @@ def vanilla_decode(P, z, hidden_dims, training, stats):
     h = _bn_act(h, P, "final_layer.1", training, stats)
     h = F.conv2d(h, P["final_layer.3.weight"], P["final_layer.3.bias"], padding=1)
     return torch.tanh(h)
+
+
+def ae_encode(P, x, hidden_dims, training, stats):
+    """models/autoencoder.py:147-163: encoder, flatten, fc -> z."""
+    h = x
+    for i in range(len(hidden_dims)):
+        h = F.conv2d(h, P[f"encoder.{i}.0.weight"], P[f"encoder.{i}.0.bias"], stride=2, padding=1)
+        h = _bn_act(h, P, f"encoder.{i}.1", training, stats)
+    return F.linear(torch.flatten(h, start_dim=1), P["fc.weight"], P["fc.bias"])
+
+
+def center_weight_mask(h, w, sigma):
+    """models/autoencoder.py:95-125: Gaussian weights around the image centre, mean 1."""
+    yy, xx = torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing="ij")
+    d2 = (yy - (h - 1) / 2) ** 2 + (xx - (w - 1) / 2) ** 2
+    wgt = torch.exp(-d2 / (2 * sigma ** 2))
+    return (wgt * (h * w / wgt.sum())).unsqueeze(0).unsqueeze(0)
+
+
+def ae_loss(recons, x, center_focus_sigma=None):
+    """models/autoencoder.py:230-262 (no VGG / MSSIM): MSE or the centre-weighted MSE."""
+    if center_focus_sigma is not None:
+        m = center_weight_mask(x.shape[2], x.shape[3], center_focus_sigma)
+        rl = ((recons - x) ** 2 * m.expand(x.shape[0], x.shape[1], -1, -1)).mean()
+    else:
+        rl = F.mse_loss(recons, x)
+    zero = torch.tensor(0.0)
+    return {"loss": rl, "Reconstruction_Loss": rl, "KLD": zero, "feature_loss": zero}
 
 
 def reparameterize(mu, log_var, eps):
@@ -358,7 +401,8 @@ TRAINABLE_KINDS = ("conv_w", "convT_w", "lin_w", "bias", "bn_w", "bn_b", "codebo
 
 def train_step(arch: str, sd, x, eps=None, *, M_N: float, lr: float = 0.005, hidden_dims=None,
                beta=4.0, gamma=1000.0, loss_type="H", max_capacity=25.0, Capacity_max_iter=1e5,
-               num_iter=1, vq_beta=0.25, do_adam=True, training=True, vq_indices=None):
+               num_iter=1, vq_beta=0.25, do_adam=True, training=True, vq_indices=None,
+               center_focus_sigma=None):
     """forward -> loss_function -> backward -> Adam on a copy of ``sd``.
 
     Returns a dict: outputs (recon, mu, log_var / vq_loss, indices), loss terms, per-image
@@ -391,6 +435,13 @@ def train_step(arch: str, sd, x, eps=None, *, M_N: float, lr: float = 0.005, hid
         per_img = ((recon.detach() - x.unsqueeze(1)) ** 2).flatten(2).mean(-1)  # [B,S]
         out.update(recon=recon.detach(), mu=mu_s[:, 0].detach(), log_var=lv_s[:, 0].detach(),
                    log_weight=lw.detach(), weight=w.detach())
+    elif arch == "Autoencoder":
+        hd = list(hidden_dims or DEFAULT_HIDDEN)
+        z = ae_encode(P, x, hd, training, stats)
+        recon = vanilla_decode(P, z, hd, training, stats)
+        ld = ae_loss(recon, x, center_focus_sigma)
+        per_img = F.mse_loss(recon.detach(), x, reduction="none").mean(dim=[1, 2, 3])
+        out.update(recon=recon.detach(), z=z.detach())
     elif arch == "VQVAE":
         hd = list(hidden_dims or VQ_HIDDEN)
         enc = vq_encode(P, x, hd)
@@ -420,6 +471,8 @@ def _kinds_of(arch, sd, hidden_dims):
     if arch == "VQVAE":
         spec = vq_param_spec(hidden_dims=hidden_dims, embedding_dim=sd["vq_layer.embedding.weight"].shape[1],
                              num_embeddings=sd["vq_layer.embedding.weight"].shape[0])
+    elif arch == "Autoencoder":
+        spec = ae_param_spec(latent_dim=sd["fc.weight"].shape[0], hidden_dims=hidden_dims)
     else:
         spec = vanilla_param_spec(latent_dim=sd["fc_mu.weight"].shape[0], hidden_dims=hidden_dims)
     kinds = {n: k for n, _, k in spec}

@@ -219,13 +219,19 @@ class GraphedSteps:
         step.opt.set_lr(self.opt.param_groups[0]['lr'])
         exp.curr_device = imgs.device
         plan = step.plan
-        eps = torch.randn(plan.eps.shape, device=imgs.device) if hasattr(plan, "eps") else None
+        eps = None
+        if hasattr(plan, "eps"):
+            eps = (torch.zeros(plan.eps.shape, device=imgs.device) if getattr(step, "zero_eps", False)
+                   else torch.randn(plan.eps.shape, device=imgs.device))
         step(imgs, eps)
         if hasattr(model, "num_iter"):
             model.num_iter += 1                       # BetaVAE: the loss_function's counter
         out = plan.out
         third = "VQ_Loss" if not hasattr(plan, "eps") else "KLD"
-        exp.log_dict({'loss': out[0], 'Reconstruction_Loss': out[1], third: out[2]})
+        terms = {'loss': out[0], 'Reconstruction_Loss': out[1], third: out[2]}
+        if getattr(step, "zero_eps", False):                  # Autoencoder: no KL, no feature loss
+            terms.update(KLD=torch.zeros_like(out[2]), feature_loss=torch.zeros_like(out[2]))
+        exp.log_dict(terms)
         per = plan.per_img.view(B, -1).mean(dim=1).cpu()
         if exp.datamodule is not None and hasattr(exp.datamodule, "record_img_losses"):
             exp.datamodule.record_img_losses(names, per)

@@ -60,7 +60,7 @@ class BaseVAE(nn.Module):
         if net is None:
             return super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
                                                  unexpected_keys, error_msgs)
-        expected = list(net.ref_order)
+        expected = list(self._ref_keys()) if hasattr(self, "_ref_keys") else list(net.ref_order)
         mine = {k[len(prefix):]: v for k, v in state_dict.items() if k.startswith(prefix)}
         for k in expected:
             if k not in mine:
@@ -418,6 +418,147 @@ class IWAE(_HipVAE):
         return {'loss': loss, 'Reconstruction_Loss': log_p_x_z.mean(), 'KLD': -kld_loss.mean()}
 
 
+class Autoencoder(_HipVAE):
+    """models/autoencoder.py:9-305 (the fork's main model) on libvaehip.
+
+    The reference's network is the VanillaVAE stack with one `fc` (Linear 4C -> D, :50) and no
+    reparameterization: z = fc(h), recons = decode(z).  Here it runs the VanillaVAE plan with the
+    log-variance half of the fused fc_mu|fc_var GEMM pinned at zero and eps = 0, so
+    z = mu + exp(0) * 0 = fc(h) exactly, the log-variance weights receive exactly zero gradient
+    (dlogvar = dz * eps * std / 2 = 0) and stay zero under Adam, and `fc` is fc_mu.  The loss is
+    the reference's: MSE on the GPU ELBO kernel (kind vanilla, M_N = 0 — no KL term), or the
+    centre-weighted MSE (center_focus_sigma, :95-146) in torch on the HIP forward's output, whose
+    autograd gradient seeds the fused HIP backward.  forward returns [recons, input, zeros, zeros]
+    (the VGG-feature placeholders, :224-227); the dict adds KLD = 0 and feature_loss = 0.
+
+    Not on this path (raise): the VGG feature loss (needs pretrained vgg19_bn weights, a network
+    download), the MSSIM loss, hidden_dims other than five stride-2 layers (the stride-1 extra
+    layers, :39) and BatchNorm widths above the kernels' 512-channel transform tables."""
+
+    def __init__(self, in_channels: int, latent_dim: int, hidden_dims: List = None, use_vgg: bool = False,
+                 center_focus_sigma: float = None, use_skip_connections: bool = False,
+                 use_mssim_loss: bool = False, **kwargs) -> None:
+        if use_vgg:
+            raise NotImplementedError("Autoencoder(use_vgg=True) needs pretrained vgg19_bn weights (network "
+                                      "download) — not on the MI355X path")
+        if use_mssim_loss:
+            raise NotImplementedError("Autoencoder(use_mssim_loss=True) is not on the MI355X path")
+        hd = list(hidden_dims) if hidden_dims is not None else [32, 64, 128, 256, 512]
+        if len(hd) != 5:
+            raise NotImplementedError(f"Autoencoder with {len(hd)} layers (stride-1 extra layers, "
+                                      "autoencoder.py:39) is not on the MI355X path; five stride-2 layers are")
+        if max(hd) > 512:
+            raise NotImplementedError(f"Autoencoder hidden width {max(hd)} > 512 channels (BatchNorm transform "
+                                      "tables of the GEMM kernels)")
+        super().__init__(in_channels, latent_dim, hd, **kwargs)
+        self.center_focus_sigma = center_focus_sigma
+        self.center_weight_mask = None
+        # with five stride-2 layers no decoder output matches an encoder output's spatial size
+        # (autoencoder.py:205-210 compares shapes), so the skip connections never fire
+        self.use_skip_connections = use_skip_connections
+        self.use_vgg = False
+        self._zero_logvar()
+
+    # ---- the fc_var half held at zero
+    def _zero_logvar(self):
+        lay = self.net.layout
+        with torch.no_grad():
+            for n in ("fc_var.weight", "fc_var.bias"):
+                sp = lay.by_name[n]
+                self.net.params[sp.offset:sp.offset + sp.numel].zero_()
+        self.net.sync_lowp()
+
+    def _ref_keys(self) -> List[str]:
+        out = []
+        for k in self.net.ref_order:
+            if k in ("fc_mu.weight", "fc_mu.bias"):
+                out.append("fc." + k.split(".")[1])
+            elif not k.startswith("fc_var."):
+                out.append(k)
+        return out
+
+    def reference_state_dict(self) -> Dict[str, Tensor]:
+        sd = self.net.reference_state_dict()
+        out = {}
+        for k in self._ref_keys():
+            src = "fc_mu." + k[3:] if k.startswith("fc.") else k
+            out[k] = sd[src]
+        return out
+
+    def load_reference_state_dict(self, sd: Dict[str, Tensor]):
+        full = dict(sd)
+        for part in ("weight", "bias"):
+            t = full.pop("fc." + part)
+            full["fc_mu." + part] = t
+            full["fc_var." + part] = torch.zeros_like(t)
+        with torch.no_grad():
+            self.net.load_reference_state_dict(full)
+
+    def _loss_config(self) -> dict:
+        return dict(loss="vanilla", samples=1)
+
+    def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None):
+        if self.center_focus_sigma is not None:
+            raise NotImplementedError("the fused step computes the plain MSE; the centre-weighted loss runs "
+                                      "through loss_function (torch loss, HIP backward)")
+        step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group)
+        step.plan.eps.zero_()
+        step.zero_eps = True
+        return step
+
+    # ---- BaseVAE
+    def encode(self, input: Tensor) -> List[Tensor]:
+        """autoencoder.py:147-163: [z]."""
+        return [super().encode(input)[0]]
+
+    def forward(self, input: Tensor, **kwargs) -> List[Tensor]:
+        B = input.shape[0]
+        recon, z, lv, _ = self._run(input, torch.zeros(B, self.latent_dim, device=input.device))
+        zeros = torch.zeros(B, self.latent_dim, device=input.device)
+        out = [recon, input, zeros, zeros.clone()]
+        if self.training and torch.is_grad_enabled() and recon.grad_fn is not None:
+            self._last = (self._plan(B), input, recon, z, lv)
+        else:
+            self._last = None
+        return out
+
+    def loss_function(self, *args, **kwargs) -> dict:
+        """autoencoder.py:230-262."""
+        recons, input = args[0], args[1]
+        zero = torch.tensor(0.0, device=recons.device)
+        last = self._last
+        if (self.center_focus_sigma is None and last is not None and self.training and torch.is_grad_enabled()
+                and recons is last[2] and input is last[1]):
+            g = _HipELBO.apply(self.flat, last[2], last[3], last[4], last[0], dict(loss="vanilla", kld_weight=0.0))
+            return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': zero, 'feature_loss': zero}
+        if self.center_focus_sigma is not None:
+            if self.center_weight_mask is None:
+                self.center_weight_mask = self.create_center_weight_mask(input.shape[2], input.shape[3], input.device)
+            recons_loss = self.weighted_mse_loss(recons, input, self.center_weight_mask)
+        else:
+            recons_loss = F.mse_loss(recons, input)
+        return {'loss': recons_loss, 'Reconstruction_Loss': recons_loss, 'KLD': zero, 'feature_loss': zero}
+
+    def create_center_weight_mask(self, height, width, device):
+        """autoencoder.py:95-125."""
+        y, x = torch.meshgrid(torch.arange(height, device=device).float(), torch.arange(width, device=device).float(),
+                              indexing='ij')
+        d2 = (y - (height - 1) / 2) ** 2 + (x - (width - 1) / 2) ** 2
+        w = torch.exp(-d2 / (2 * self.center_focus_sigma ** 2))
+        return (w * (height * width / w.sum())).unsqueeze(0).unsqueeze(0)
+
+    @staticmethod
+    def weighted_mse_loss(input, target, weight_mask):
+        """autoencoder.py:127-145."""
+        return ((input - target) ** 2 * weight_mask.expand(input.size(0), input.size(1), -1, -1)).mean()
+
+    def sample(self, num_samples: int, current_device: int, **kwargs) -> Tensor:
+        """autoencoder.py:264-279: z ~ U(-1, 1)."""
+        z = torch.rand(num_samples, self.latent_dim, device=current_device) * 2 - 1
+        return self.decode(z)
+
+
 class _VQStep(torch.autograd.Function):
     """VQ-VAE forward on the HIP network; backward = the fused HIP backward seeded with
     dL/drecon and dL/dvq_loss (straight-through estimator inside, vq_vae.py:53)."""
@@ -528,7 +669,7 @@ class VQVAE(BaseVAE):
 
 
 # models/__init__.py:35-56: the families on the MI355X path; the others raise on use.
-_ON_PATH = {'VanillaVAE': VanillaVAE, 'BetaVAE': BetaVAE, 'IWAE': IWAE, 'VQVAE': VQVAE}
+_ON_PATH = {'VanillaVAE': VanillaVAE, 'BetaVAE': BetaVAE, 'IWAE': IWAE, 'VQVAE': VQVAE, 'Autoencoder': Autoencoder}
 _REFERENCE_NAMES = ['HVAE', 'LVAE', 'IWAE', 'SWAE', 'MIWAE', 'VQVAE', 'DFCVAE', 'DIPVAE', 'BetaVAE', 'InfoVAE',
                     'WAE_MMD', 'VampVAE', 'GammaVAE', 'MSSIMVAE', 'JointVAE', 'BetaTCVAE', 'FactorVAE',
                     'LogCoshVAE', 'VanillaVAE', 'ConditionalVAE', 'CategoricalVAE', 'Autoencoder']
@@ -537,7 +678,7 @@ _REFERENCE_NAMES = ['HVAE', 'LVAE', 'IWAE', 'SWAE', 'MIWAE', 'VQVAE', 'DFCVAE', 
 def _not_on_path(name):
     def ctor(*args, **kwargs):
         raise NotImplementedError(f"{name} is not on the MI355X training path of this build "
-                                  f"(VanillaVAE, BetaVAE, IWAE, VQVAE are; DESIGN.md §7)")
+                                  f"(VanillaVAE, BetaVAE, IWAE, VQVAE, Autoencoder are; DESIGN.md §7)")
     return ctor
 
 

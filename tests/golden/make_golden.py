@@ -41,6 +41,8 @@ CASES = {
     "betaB_b8": ("BetaVAE", 8, dict(in_channels=3, latent_dim=128, loss_type="B", gamma=1000.0,
                                      max_capacity=25, Capacity_max_iter=1e5), 2.5e-4, 0.005, {}),
     "iwae_b4": ("IWAE", 4, dict(in_channels=3, latent_dim=128, num_samples=5), 2.5e-4, 0.007, {"S": 5}),
+    "ae_b16": ("Autoencoder", 16, dict(in_channels=3, latent_dim=128), 0.0, 0.005, {}),
+    "ae_center_b8": ("Autoencoder", 8, dict(in_channels=3, latent_dim=128, center_focus_sigma=11), 0.0, 0.0005, {}),
     "vq_b4": ("VQVAE", 4, dict(in_channels=3, embedding_dim=64, num_embeddings=512, img_size=64, beta=0.25),
               0.0, 0.005, {}),
 }
@@ -74,7 +76,8 @@ def run_case(models, name):
     torch.manual_seed(0)
     model = models.vae_models[arch](**kw)
     spec = (O.vq_param_spec(embedding_dim=kw["embedding_dim"], num_embeddings=kw["num_embeddings"])
-            if arch == "VQVAE" else O.vanilla_param_spec(latent_dim=kw["latent_dim"]))
+            if arch == "VQVAE" else O.ae_param_spec(latent_dim=kw["latent_dim"]) if arch == "Autoencoder"
+            else O.vanilla_param_spec(latent_dim=kw["latent_dim"]))
     sd = O.make_params(spec, SEED)
     model.load_state_dict(sd, strict=True)
     model.train()
@@ -89,11 +92,16 @@ def run_case(models, name):
         assert tuple(t.shape) == tuple(eps.shape), (t.shape, eps.shape)
         return eps.clone()
 
+    captured = {}
+    hook = (model.fc.register_forward_hook(lambda m, i, o: captured.__setitem__("z", o.detach().clone()))
+            if arch == "Autoencoder" else None)
     torch.randn_like = fake_randn_like
     try:
         results = model(x, labels=torch.zeros(B))
     finally:
         torch.randn_like = real_randn_like
+        if hook is not None:
+            hook.remove()
     ld = model.loss_function(*results, M_N=M_N, optimizer_idx=0, batch_idx=0)
     ld["loss"].reshape(()).backward()
 
@@ -122,6 +130,8 @@ def run_case(models, name):
         arrays["per_img_mse"] = torch.nn.functional.mse_loss(recon, x, reduction="none").mean(dim=[1, 2, 3]).numpy()
     if arch in ("VanillaVAE", "BetaVAE"):
         arrays["mu"], arrays["log_var"] = results[2].detach().numpy(), results[3].detach().numpy()
+    if arch == "Autoencoder":
+        arrays["z"] = captured["z"].numpy()
     if arch == "VQVAE":
         with torch.no_grad():
             enc = model.encode(x)[0]
@@ -158,7 +168,8 @@ def main():
     ref_root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     torch.set_num_threads(8)
     models = import_reference(ref_root)
-    for name in CASES:
+    only = sys.argv[2:] or list(CASES)
+    for name in only:
         run_case(models, name)
 
 

@@ -5,7 +5,7 @@ import os
 import numpy as np
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["vanilla_b16", "vanilla_b8_kl", "betaH_b16", "betaB_b8", "iwae_b4", "vq_b4"]
+CASES = ["vanilla_b16", "vanilla_b8_kl", "betaH_b16", "betaB_b8", "iwae_b4", "vq_b4", "ae_b16", "ae_center_b8"]
 
 
 def load_case(name):
@@ -32,6 +32,8 @@ def case_inputs(meta):
     kw = meta["ctor"]
     if meta["arch"] == "VQVAE":
         spec = O.vq_param_spec(embedding_dim=kw["embedding_dim"], num_embeddings=kw["num_embeddings"])
+    elif meta["arch"] == "Autoencoder":
+        spec = O.ae_param_spec(latent_dim=kw["latent_dim"])
     else:
         spec = O.vanilla_param_spec(latent_dim=kw["latent_dim"])
     sd = O.make_params(spec, meta["seed"])
@@ -51,4 +53,6 @@ def oracle_kwargs(meta):
                  num_iter=1)
     if meta["arch"] == "VQVAE":
         d.update(vq_beta=kw.get("beta", 0.25))
+    if meta["arch"] == "Autoencoder":
+        d.update(center_focus_sigma=kw.get("center_focus_sigma"))
     return d

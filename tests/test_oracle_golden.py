@@ -29,6 +29,8 @@ def test_oracle_matches_reference(case):
     if meta["arch"] == "IWAE":
         np.testing.assert_allclose(out["log_weight"].numpy(), ref["log_weight"], rtol=1e-5)
         np.testing.assert_allclose(out["weight"].numpy(), ref["weight"], rtol=1e-4, atol=1e-7)
+    if meta["arch"] == "Autoencoder":
+        assert rel_err(out["z"].numpy(), ref["z"]) < 1e-5
     if meta["arch"] == "VQVAE":
         sure = ref["gap"] > 1e-6
         assert np.array_equal(out["indices"].numpy()[sure], ref["indices"][sure])
