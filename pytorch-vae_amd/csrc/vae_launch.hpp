@@ -479,6 +479,17 @@ inline bool cg_ok(const GemmParams& p, int em) {
 
 struct CgTile { int bm, bn; };
 
+// Launch-shape tunables (read once): VAE_CG_MINWG — workgroups per CU a tile must give before a
+// smaller one is tried (default 2); VAE_CG_SPLITWG — split K while a launch has fewer than this
+// many workgroups per CU (default 1); VAE_WG_WGPERCU — the weight-gradient GEMM's K-slice target.
+inline int tune_env(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+inline int cg_minwg() { static const int v = tune_env("VAE_CG_MINWG", 2); return v; }
+inline int cg_splitwg() { static const int v = tune_env("VAE_CG_SPLITWG", 1); return v; }
+
 // Largest tile that still gives every CU ~2 workgroups; split-K (slabs + igemm_finalize) when
 // even the smallest leaves the chip half empty and K is deep.
 inline CgTile cg_pick(long M, long N, int nphase) {
@@ -488,7 +499,7 @@ inline CgTile cg_pick(long M, long N, int nphase) {
     if (t.bn > 32 && N < t.bn) continue;
     // 128 x 32 only for the long thin maps (>= 8 workgroups per CU at 64 x 32)
     if (t.bm == 128 && t.bn == 32 && tile_blocks(M, N, nphase, Tile{64, 32}) < 8 * kCUs) continue;
-    if (tile_blocks(M, N, nphase, Tile{t.bm, t.bn}) >= 2 * kCUs) return t;
+    if (tile_blocks(M, N, nphase, Tile{t.bm, t.bn}) >= (long)cg_minwg() * kCUs) return t;
   }
   return CgTile{32, 32};
 }
@@ -543,8 +554,8 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   const int ktiles = (kmax + bk - 1) / bk;
   const long blocks = tile_blocks(p.M, p.N, p.nphase, Tile{t.bm, t.bn});
   int split = split_req > 0 ? split_req : 1;
-  if (split_req <= 0 && blocks < kCUs && ktiles >= 4) {
-    split = (int)((2 * kCUs + blocks - 1) / blocks);
+  if (split_req <= 0 && blocks < (long)cg_splitwg() * kCUs && ktiles >= 4) {
+    split = (int)((2 * (long)cg_splitwg() * kCUs + blocks - 1) / blocks);
     if (split > ktiles / 2) split = ktiles / 2;
   }
   if (int rc = split_fits(&split, split_req, p, ws, ws_bytes, "cgemm split-K")) return rc;

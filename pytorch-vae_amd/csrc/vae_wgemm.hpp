@@ -511,7 +511,8 @@ inline int wg2_launch(WgParams p, hipStream_t st) {
   const long tiles = (long)((p.M + T - 1) / T) * ((p.J + T - 1) / T) * (taps_in_block ? 1 : p.R * p.R);
   const long ksteps = (npix + 31) / 32;
   // K slices: ~2 workgroups per CU, >= 4 K-steps per slice
-  long split = (2 * kCUs + tiles - 1) / tiles;
+  static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
+  long split = ((long)wgpercu * kCUs + tiles - 1) / tiles;
   if (split > ksteps / 4) split = ksteps / 4;
   if (split < 1) split = 1;
   p.kper = (int)(((ksteps + split - 1) / split) * 32);

@@ -6,8 +6,8 @@ all-reduce launched between them, and the loss terms ride in the last bucket.
 
 Checked against the CPU oracle, not against another HIP run: each rank's shard through
 oracle.train_step, the shard gradients averaged (DDP semantics, run.py:86), one Adam step.  Bars
-are the single-GPU parity bars (test_gpu_parity_shapes.py): averaged gradients within 1e-3
-relative norm per parameter (3e-3 BatchNorm affine), loss terms (the rank mean the reference logs
+are the single-GPU parity bars (test_gpu_parity_shapes.py): averaged gradients within max(1e-3,
+3 x the oracle's own thread-count spread) relative norm per parameter (3e-3 floor BatchNorm affine), loss terms (the rank mean the reference logs
 with sync_dist, experiment.py:55) within 1e-4, BatchNorm buffers = rank 0's shard statistics
 (DDP broadcast_buffers), and the Adam update equal to the oracle's on every element whose
 averaged gradient is not within noise of zero."""
@@ -54,9 +54,11 @@ def _worker(rank, port, q):
         x, eps = _shard(rank)
         step(x.cuda(), eps.cuda())
         torch.cuda.synchronize()
-        grads = {k: v.cpu() for k, v in net.layout.export_reference(plan.grads).items()}
-        q.put((rank, {k: v.cpu() for k, v in net.reference_state_dict().items()}, grads, step.loss_terms(),
-               plan.out[:3].tolist()))
+        # numpy, not torch tensors: a torch CPU tensor crosses the queue as a shared-memory file
+        # descriptor that dies with this process
+        grads = {k: v.cpu().numpy() for k, v in net.layout.export_reference(plan.grads).items()}
+        state = {k: v.cpu().numpy() for k, v in net.reference_state_dict().items()}
+        q.put((rank, state, grads, step.loss_terms(), plan.out[:3].tolist()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception:
@@ -76,12 +78,16 @@ def test_data_parallel_betaH_matches_oracle_shard_mean():
     for _ in range(WORLD):
         r, state, grads, terms, local = q.get(timeout=240)
         assert not isinstance(state, str), state
+        state = {k: torch.from_numpy(v) for k, v in state.items()}
+        grads = {k: torch.from_numpy(v) for k, v in grads.items()}
         res[r] = (state, grads, terms, local)
     for p in procs:
         p.join(timeout=60)
+    from parity_util import grad_bar, oracle_with_spread
     sd = O.make_params(O.vanilla_param_spec(), SEED)
-    shards = [O.train_step("BetaVAE", sd, *_shard(r), M_N=M_N, lr=LR, loss_type="H", beta=4.0, do_adam=False)
-              for r in range(WORLD)]
+    shards, spreads = zip(*[oracle_with_spread("BetaVAE", sd, *_shard(r), M_N=M_N, lr=LR, loss_type="H", beta=4.0)
+                            for r in range(WORLD)])
+    spread = {k: max(sp[k] for sp in spreads) for k in spreads[0]}
     # both ranks hold the same averaged gradient, parameters and (broadcast) buffers
     for k in res[0][0]:
         assert torch.equal(res[0][0][k], res[1][0][k]), k
@@ -101,8 +107,8 @@ def test_data_parallel_betaH_matches_oracle_shard_mean():
             continue                                    # analytically zero under train-mode BN
         err = float((grads[name].double() - gr.double()).norm() / gr.double().norm())
         worst = max(worst, err)
-        bound = 3e-3 if name.endswith(".1.weight") or name.endswith(".1.bias") else 1e-3
-        assert err < bound, (name, err)
+        bound = grad_bar(name, spread)
+        assert err < bound, (name, err, bound)
     print(f"DP betaH 2x{B}: worst averaged-gradient rel-norm {worst:.2e}")
     # one Adam step from zero state on the averaged gradient: lr * g / (|g| + eps) elementwise —
     # compared where the oracle's averaged gradient is clear of the noise floor (sign-stable)

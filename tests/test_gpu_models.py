@@ -233,8 +233,8 @@ def test_experiment_graph_engine_matches_eager(arch):
     """fit(engine="graph") — one HIP-graph TrainStep per batch with FusedAdam — against the eager
     drop-in (training_step -> GPU ELBO -> loss.backward -> torch.optim.Adam) from the same
     parameters: the logged loss terms of the first step agree to fp32 rounding, and the first Adam
-    update to 1e-2 of its norm (elements whose gradient is within noise of zero may flip the sign
-    of their first step, lr*g/|g|)."""
+    update except on a few elements whose gradient is within rounding of zero (their first step
+    lr*g/|g| may flip sign)."""
     from vae_amd.experiment import GraphedSteps, VAEXperiment
     from vae_amd.models import vae_models
     kw = dict(in_channels=3, latent_dim=128, dtype=torch.float32, device="cuda", seed=1265)
@@ -267,7 +267,13 @@ def test_experiment_graph_engine_matches_eager(arch):
     assert set(le) == set(lg)
     for k in le:
         assert abs(le[k] - lg[k]) <= 1e-5 * abs(le[k]) + 1e-7, (k, le[k], lg[k])
-    assert float((dg - de).norm() / de.norm()) < 1e-2
+    # the first Adam step is lr * g / (|g| + eps) ~ lr * sign(g): the two paths' gradients differ
+    # only in atomic summation order, so only elements whose gradient is within rounding of zero
+    # may move differently — a small fraction, each by at most 2 lr
+    lr = params['LR']
+    moved = (dg - de).abs() > 0.1 * lr
+    assert float(moved.float().mean()) < 2e-3, float(moved.float().mean())
+    assert float((dg - de).abs().max()) <= 2 * lr * 1.001
 
 
 @pytest.mark.parametrize("case", ["ae_b16", "ae_center_b8"])

@@ -9,11 +9,12 @@ CPU oracle on the same seeded parameters and inputs:
 The golden-vector tests (test_gpu_step.py, test_gpu_vq.py) pin the same kernels at B<=16 against
 the reference's own modules; the oracle itself is pinned to those vectors (test_oracle_golden.py).
 
-Bars (north_star; SURVEY.md §8(c), measured CPU 8-thread vs 1-thread spread of 1.1e-4 on the
-gradient norms): ELBO terms within 1e-4 relative; mu / log_var / reconstructions within 1e-4 of
-their scale; per-image MSE within 1e-4 relative; every parameter gradient within 1e-3 relative
-norm (3e-3 for the BatchNorm affine gradients, reductions with ~100x cancellation); BatchNorm
-running statistics within 1e-4.
+Bars (north_star): ELBO terms within 1e-4 relative; mu / log_var /
+reconstructions within 1e-4 of their scale; per-image MSE within 1e-4 relative; BatchNorm running
+statistics within 1e-4; every parameter gradient within max(1e-3, 3 x the oracle's own spread on
+that tensor) relative norm (3e-3 floor for the BatchNorm affine gradients).  The spread is measured
+in the test — the oracle at the default thread count against the oracle on 1 thread — because at
+these batch sizes it exceeds 1e-3 (measured 1.4e-3 at B=64, 2.4e-3 at B=32: tests/parity_util.py).
 
 VQ index exactness: the codebook index of every one of the 32,768 rows equals the oracle's
 (torch.argmin of the same fp32 expansion Σz²+ΣE²−2z·E, first minimum) wherever the oracle's gap
@@ -55,7 +56,8 @@ def _hip_vanilla_step(loss, batch, samples, M_N, sd, x, eps, lr=0.005):
     return net, plan, opt
 
 
-def _check_grads(grads, want, skip=lambda n: False):
+def _check_grads(grads, want, skip=lambda n: False, spread=None):
+    from parity_util import grad_bar
     report = []
     for name, gr in want.items():
         g = grads[name]
@@ -63,8 +65,8 @@ def _check_grads(grads, want, skip=lambda n: False):
             continue
         err = float((g.double() - gr.double()).norm() / gr.double().norm().clamp_min(1e-30))
         report.append((err, name))
-        bound = 3e-3 if _is_bn_affine(name) else 1e-3
-        assert err < bound, (name, err)
+        bound = grad_bar(name, spread or {})
+        assert err < bound, (name, err, bound)
     return max(report)
 
 
@@ -77,8 +79,9 @@ def test_step_matches_oracle_at_bench_shape(arch, loss, batch, samples, M_N):
     from oracle import vae_oracle as O
     sd = O.make_params(O.vanilla_param_spec(), SEED)
     x, eps = O.make_inputs(batch, 128, SEED + batch, samples=samples)
+    from parity_util import oracle_with_spread
     net, plan, opt = _hip_vanilla_step(loss, batch, samples, M_N, sd, x, eps)
-    o = O.train_step(arch, sd, x, eps, M_N=M_N, lr=0.005, loss_type="H", beta=4.0, do_adam=False)
+    o, spread = oracle_with_spread(arch, sd, x, eps, M_N=M_N, lr=0.005, loss_type="H", beta=4.0)
     out = plan.out.cpu().tolist()
     got = {"loss": out[0], "Reconstruction_Loss": out[1], "KLD": out[2]}
     for k in ("loss", "Reconstruction_Loss", "KLD"):
@@ -98,8 +101,9 @@ def test_step_matches_oracle_at_bench_shape(arch, loss, batch, samples, M_N):
     for name, gr in o["grads"].items():
         if _pre_bn_bias(name):     # analytically zero under train-mode BN: bound by the weight grad
             assert float(grads[name].abs().max()) <= 1e-4 * float(o["grads"][name[:-4] + "weight"].abs().max()) + 1e-7
-    worst = _check_grads(grads, o["grads"], skip=_pre_bn_bias)
-    print(f"{arch} B={batch}: worst grad rel-norm {worst[0]:.2e} ({worst[1]})")
+    worst = _check_grads(grads, o["grads"], skip=_pre_bn_bias, spread=spread)
+    print(f"{arch} B={batch}: worst grad rel-norm {worst[0]:.2e} ({worst[1]}); oracle thread spread of it "
+          f"{spread[worst[1]]:.2e}, largest spread {max(spread.values()):.2e}")
     run = {k: v.cpu() for k, v in net.reference_state_dict().items()}
     for k, v in o["running"].items():
         np.testing.assert_allclose(run[k].numpy(), v.numpy(), rtol=1e-4, atol=1e-6, err_msg=k)
