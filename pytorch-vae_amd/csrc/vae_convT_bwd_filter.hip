@@ -19,7 +19,7 @@ extern "C" int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream) {
     w.n = a->n; w.hu = a->h; w.wu = a->w; w.M = a->c; w.hv = a->p; w.wv = a->q; w.J = a->k;
     w.R = a->r; w.S = a->stride; w.P = a->pad; w.dw = a->dw;
     w.db = closed ? a->db : nullptr; w.dy_is_v = 1;
-    int rc = wg2_launch(w, (hipStream_t)stream);
+    int rc = wg2_launch(w, a->workspace, a->workspace_bytes, (hipStream_t)stream);
     if (rc || !a->db || closed) return rc;
     return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
   }

@@ -38,6 +38,8 @@ struct WgParams {
   float* db;                         // closed-form bias gradient (first workgroup; with u/v BN_DY extras)
   int dy_is_v;                       // which operand carries the BN_DY transform (bias gradient of its conv)
   FastDiv fd_wu, fd_hu, fd_r;
+  float* slab;                       // non-NULL: K slice s stores its partial dW at slab + s*slab_ld
+  long slab_ld;                      //   (plain stores; wg_slab_reduce adds the slices into dw)
 };
 
 template <int BM> constexpr int wg_rs() { return BM == 32 ? 64 : (BM == 64 ? 160 : 288); }
@@ -229,6 +231,7 @@ __global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
   }
   // D[m][j]: lane holds rows 4g + e of fragment i, column li of fragment j
   const long rowstride = (long)p.R * p.R * p.J;
+  float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -238,7 +241,10 @@ __global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int mm = m0 + wm * WTM + i * 16 + 4 * g + e;
-        if (mm < p.M) atomicAdd(p.dw + mm * rowstride + (long)tap * p.J + jj, acc[i][j][e]);
+        if (mm >= p.M) continue;
+        const long o = mm * rowstride + (long)tap * p.J + jj;
+        if (part) part[o] = acc[i][j][e];
+        else atomicAdd(p.dw + o, acc[i][j][e]);
       }
     }
 }
@@ -434,6 +440,7 @@ __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
     }
   }
   const long rowstride = (long)TAPS * p.J;
+  float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
 #pragma unroll
   for (int t = 0; t < TAPS; ++t)
 #pragma unroll
@@ -445,9 +452,34 @@ __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int mm = m0 + wm * WTM + i * 16 + 4 * g + e;
-          if (mm < p.M) atomicAdd(p.dw + mm * rowstride + (long)t * p.J + jj, acc[t][i][j][e]);
+          if (mm >= p.M) continue;
+          const long o = mm * rowstride + (long)t * p.J + jj;
+          if (part) part[o] = acc[t][i][j][e];
+          else atomicAdd(p.dw + o, acc[t][i][j][e]);
         }
       }
+}
+
+// dw[c] += sum over the K slices of slab[s][c]: blockIdx.y takes a contiguous run of slices, one
+// float4 of columns per thread, one atomic per column per run (cols % 4 == 0, 16-byte aligned).
+static __global__ void __launch_bounds__(256) wg_slab_reduce(const float* slab, long cols, int slices, int per_part,
+                                                       float* dw) {
+  const long c = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (c >= cols) return;
+  const int s0 = blockIdx.y * per_part;
+  const int s1 = min(slices, s0 + per_part);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(slab + (long)s * cols + c);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(slab + (long)(s + 1) * cols + c);
+    const f32x4 d = *reinterpret_cast<const f32x4*>(slab + (long)(s + 2) * cols + c);
+    const f32x4 e = *reinterpret_cast<const f32x4*>(slab + (long)(s + 3) * cols + c);
+    acc += (a + b) + (d + e);
+  }
+  for (; s < s1; ++s) acc += *reinterpret_cast<const f32x4*>(slab + (long)s * cols + c);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) atomicAdd(dw + c + i, acc[i]);
 }
 
 // ------------------------------------------------------------------ host
@@ -497,7 +529,16 @@ inline void wg2_launch_u(const WgParams& p, unsigned blocks, hipStream_t st) {
   }
 }
 
-inline int wg2_launch(WgParams p, hipStream_t st) {
+// K slices at or above which the partials go through a workspace slab and wg_slab_reduce
+// instead of fp32 atomics straight into dw: hundreds of workgroups adding into the same few
+// thousand words serialise at the L2.  Measured (B=64): the decoder's final ConvT wgrad (512
+// slices x 9216 words) 45.3 -> 33.5 us and the first conv's (512 x 2304) 36.3 -> 20.7 us with the
+// slab; at 256 slices x 18432 words or 28 slices x 295k words the slab traffic costs more than the
+// atomics save (26 -> 32 us, 19 -> 55 us), hence the slice floor and the byte cap.
+constexpr int kWgSlabMin = 384;
+constexpr long kWgSlabMaxBytes = 32l << 20;
+
+inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   p.fd_wu = make_fastdiv(p.wu);
   p.fd_hu = make_fastdiv(p.hu);
   p.fd_r = make_fastdiv(p.R);
@@ -512,16 +553,32 @@ inline int wg2_launch(WgParams p, hipStream_t st) {
   const long ksteps = (npix + 31) / 32;
   // K slices: ~2 workgroups per CU, >= 4 K-steps per slice
   static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
+  static const int mink = tune_env("VAE_WG_MINK", 4);
   long split = ((long)wgpercu * kCUs + tiles - 1) / tiles;
-  if (split > ksteps / 4) split = ksteps / 4;
+  if (split > ksteps / mink) split = ksteps / mink;
   if (split < 1) split = 1;
   p.kper = (int)(((ksteps + split - 1) / split) * 32);
   split = (npix + p.kper - 1) / p.kper;
   const unsigned blocks = (unsigned)(tiles * split);
+  const long cols = (long)p.M * p.R * p.R * p.J;
+  const int slab_min = tune_env("VAE_WG_SLAB_MIN", kWgSlabMin);      // read per call (tests lower it)
+  p.slab = nullptr;
+  p.slab_ld = cols;
+  if (split >= slab_min && split * cols * 4 <= kWgSlabMaxBytes && (ws || querying()) && cols % 4 == 0 &&
+      !getenv("VAE_NO_WG_SLAB")) {
+    if (!ws_fits(split * cols * 4, ws_bytes, "wgemm K-slice partials")) return VAE_E_BADARG;
+    p.slab = static_cast<float*>(ws);
+  }
   if (T == 128) wg2_launch_u<128, 128>(p, blocks, st);
   else if (T == 64) wg2_launch_u<64, 64>(p, blocks, st);
   else wg2_launch_u<32, 32>(p, blocks, st);
-  return check_launch("wgemm");
+  int rc = check_launch("wgemm");
+  if (rc || !p.slab) return rc;
+  const int parts = split < 32 ? (int)split : 32;
+  const int per = (int)((split + parts - 1) / parts);
+  const dim3 grid((unsigned)((cols / 4 + 255) / 256), (unsigned)((split + per - 1) / per));
+  VAE_LAUNCH(wg_slab_reduce, grid, dim3(256), 0, st, (const float*)p.slab, cols, (int)split, per, p.dw);
+  return check_launch("wg_slab_reduce");
 }
 
 }  // namespace vae

@@ -1,0 +1,7 @@
+# Quick iteration: GEMM-level tests, then the bench with its breakdown.  Usage: bash scripts/gpu_r2_quick.sh TAG [env...]
+set -o pipefail
+TAG=${1:-q}; shift
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_cgemm.py -q -x --timeout 120 --timeout-method thread > gpurun_out/${TAG}_cg.log 2>&1 || exit $?
+env "$@" timeout -k 10 120 python3 -u bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-dropin --kernel-breakdown > gpurun_out/${TAG}_bench.log 2>&1

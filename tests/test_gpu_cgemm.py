@@ -305,7 +305,9 @@ class BN:
         return bf(F.leaky_relu(z, SLOPE).float())
 
 
-def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed=3):
+def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed=3, slab=False):
+    """slab: give the call its queried workspace — K slices write partials to it and a fixed-order
+    slab reduction adds them into dw (vae_wgemm.hpp wg_slab_reduce); else fp32 atomics into dw."""
     L = _L()
     g = torch.Generator().manual_seed(seed)
     if transposed:
@@ -356,8 +358,20 @@ def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, see
         a.dy_xf = bny.xf(L, L.X_BN_DY, aux_dev=yd, dgamma=dgam, dbeta=dbet, dgamma_out=dgo, dbeta_out=dbo)
         a.db = db.data_ptr()
     a.dw = dw.data_ptr()
-    L.call("vae_convT2d_bwd_filter" if transposed else "vae_conv2d_bwd_filter", ctypes.byref(a),
-           torch.cuda.current_stream().cuda_stream)
+    fn = "vae_convT2d_bwd_filter" if transposed else "vae_conv2d_bwd_filter"
+    import os
+    old_env = os.environ.get("VAE_WG_SLAB_MIN")
+    if slab:                      # the slab path from 2 K slices on (in the net: >= 384, vae_wgemm.hpp)
+        os.environ["VAE_WG_SLAB_MIN"] = "2"
+        ws = give_workspace(a, fn)           # 4 bytes when the shape has a single K slice
+    try:
+        L.call(fn, ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    finally:
+        if slab:
+            if old_env is None:
+                os.environ.pop("VAE_WG_SLAB_MIN", None)
+            else:
+                os.environ["VAE_WG_SLAB_MIN"] = old_env
     torch.cuda.synchronize()
     assert relmax(dw.cpu(), want) < 2e-3
     if dy_kind == L.X_BN_DY:
@@ -374,10 +388,11 @@ WGRAD = [  # N, cin, cout, hw (conv input), stride, R, pad
 ]
 
 
+@pytest.mark.parametrize("slab", [False, True])
 @pytest.mark.parametrize("shape", WGRAD)
-def test_wgemm_conv2d_bn(shape):
+def test_wgemm_conv2d_bn(shape, slab):
     L = _L()
-    run_wgrad(False, *shape, L.X_NONE if shape[1] == 8 else L.X_BN_ACT, L.X_BN_DY)
+    run_wgrad(False, *shape, L.X_NONE if shape[1] == 8 else L.X_BN_ACT, L.X_BN_DY, slab=slab)
 
 
 def test_wgemm_conv2d_vq_shapes():
@@ -393,10 +408,11 @@ WGRAD_T = [  # N, cin, cout, hw (convT input), stride, R, pad
 ]
 
 
+@pytest.mark.parametrize("slab", [False, True])
 @pytest.mark.parametrize("shape", WGRAD_T)
-def test_wgemm_convT2d_bn(shape):
+def test_wgemm_convT2d_bn(shape, slab):
     L = _L()
-    run_wgrad(True, *shape, L.X_BN_ACT, L.X_BN_DY)
+    run_wgrad(True, *shape, L.X_BN_ACT, L.X_BN_DY, slab=slab)
 
 
 def test_wgemm_convT2d_vq_shape():
