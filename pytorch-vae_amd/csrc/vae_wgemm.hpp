@@ -255,13 +255,18 @@ __global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
 // (BM/2 x BJ/2) wave tile.
 template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : cg_stages<LOADS>(); }
 
+// K-step: every thread loads one 16-byte chunk of U and of each tap's V row — 64 pixels for the
+// 32-channel tiles (128 of the 256 threads idled at 32) — and the LDS holds one step (single
+// buffer, two barriers per step) so two workgroups still fit a CU: each memory round trip (the
+// loop is latency-bound, one step in flight per ring slot) now carries twice the MFMA work.
 template <int BM, int BJ, int XU, int XV, int RR>
 __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
   constexpr int TAPS = RR * RR;
-  constexpr int KP = 32;
-  constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int CU = BM / 8, CV = BJ / 8;
   constexpr int RPU = 256 / CU, RPV = 256 / CV;
+  constexpr int KP = RPU < RPV ? (RPU < 32 ? 32 : (RPU > 64 ? 64 : RPU)) : (RPV < 32 ? 32 : (RPV > 64 ? 64 : RPV));
+  constexpr int NB = KP > 32 ? 1 : 2;                  // LDS buffers
+  constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int UPT = RPU >= KP ? 1 : KP / RPU, VPT = RPV >= KP ? 1 : KP / RPV;
   constexpr bool DU = XU == VAE_X_BN_DY, DV = XV == VAE_X_BN_DY;
   constexpr bool BU = XU == VAE_X_BN_ACT || DU, BV = XV == VAE_X_BN_ACT || DV;
@@ -270,8 +275,8 @@ __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
   constexpr int WTM = BM / 2, WTJ = BJ / 2;
   constexpr int TM = WTM / 16, TJ = WTJ / 16;
 
-  __shared__ __attribute__((aligned(16))) char Us[2][KP * RSU];
-  __shared__ __attribute__((aligned(16))) char Vs[2][TAPS][KP * RSV];
+  __shared__ __attribute__((aligned(16))) char Us[NB][KP * RSU];
+  __shared__ __attribute__((aligned(16))) char Vs[NB][TAPS][KP * RSV];
   extern __shared__ float tabs[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -404,26 +409,32 @@ __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
     for (int j = 0; j < TJ; ++j) boff[j][h] = row * RSV + (wn * WTJ + j * 16 + 4 * p4) * 2;
   }
   auto compute = [&](int buf) {
-    bf16x8 af[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const wgm_bf16x4 a0 = wgm_tr_read(Us[buf] + aoff[i][0]), a1 = wgm_tr_read(Us[buf] + aoff[i][1]);
+    for (int kk = 0; kk < KP / 32; ++kk) {             // MFMA K = 32 pixels
+      bf16x8 af[TM];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
-    }
+      for (int i = 0; i < TM; ++i) {
+        const wgm_bf16x4 a0 = wgm_tr_read(Us[buf] + kk * 32 * RSU + aoff[i][0]);
+        const wgm_bf16x4 a1 = wgm_tr_read(Us[buf] + kk * 32 * RSU + aoff[i][1]);
 #pragma unroll
-    for (int t = 0; t < TAPS; ++t) {
-      bf16x8 bfr[TJ];
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const wgm_bf16x4 b0 = wgm_tr_read(Vs[buf][t] + boff[j][0]), b1 = wgm_tr_read(Vs[buf][t] + boff[j][1]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { bfr[j][e] = b0[e]; bfr[j][4 + e] = b1[e]; }
+        for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
       }
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int t = 0; t < TAPS; ++t) {
+        bf16x8 bfr[TJ];
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+        for (int j = 0; j < TJ; ++j) {
+          const wgm_bf16x4 b0 = wgm_tr_read(Vs[buf][t] + kk * 32 * RSV + boff[j][0]);
+          const wgm_bf16x4 b1 = wgm_tr_read(Vs[buf][t] + kk * 32 * RSV + boff[j][1]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { bfr[j][e] = b0[e]; bfr[j][4 + e] = b1[e]; }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+      }
     }
   };
 
@@ -432,11 +443,12 @@ __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
       const bool live = kb + u < nsteps;
+      if constexpr (NB == 1) __syncthreads();         // the previous step's reads of the buffer
       if (live) store(buf, ring[u]);
       __syncthreads();
       issue(kb + u + NS, ring[u]);
       if (live) compute(buf);
-      buf ^= 1;
+      if constexpr (NB == 2) buf ^= 1;
     }
   }
   const long rowstride = (long)TAPS * p.J;
