@@ -91,20 +91,31 @@ __device__ __forceinline__ uint4 cg_xform(const uint32_t (&w)[4], const uint32_t
 // (80 VGPRs).  The VanillaVAE layers have 1-9 K-steps, so for most of them the whole K range is
 // requested in the prologue and a block pays one memory round trip, not one per step (the
 // round trip under load is 1.5-2 us, tools/kprobe.py).
-template <int LOADS> constexpr int cg_stages() {
+// ~20 16-byte loads in flight per thread (80 VGPRs).  Measured at 40 (kRingMax 12): the 5-9
+// K-step layers gain 1-3 us from one fewer round trip, the big-M maps lose as much or more to the
+// halved occupancy (VanillaVAE step 0.760 -> 0.767 ms), so the ring stays at 20.
+constexpr int kRingLoads = 20, kRingMax = 8;
+constexpr int cg_ring(int loads) {
+  return kRingLoads / loads < 2 ? 2 : (kRingLoads / loads > kRingMax ? kRingMax : kRingLoads / loads);
+}
+template <int LOADS> constexpr int cg_stages() { return cg_ring(LOADS); }
+// the weight-gradient kernels keep ~20 loads in flight (their K slices are sized for it)
+template <int LOADS> constexpr int wg_stages() {
   return 20 / LOADS < 2 ? 2 : (20 / LOADS > 8 ? 8 : 20 / LOADS);
 }
 
-template <int BM, int BN, int BK> struct CgSmem {
+template <int BM, int BN, int BK, int NBUF = 2> struct CgSmem {
   static constexpr int LDK = BK + 8;
-  static constexpr int LOOP = 2 * (BM + BN) * LDK * 2;          // bytes: double-buffered A and B tiles
+  static constexpr int LOOP = NBUF * (BM + BN) * LDK * 2;       // bytes: (double-)buffered A and B tiles
   static constexpr int EPI = BM * (BN + 4) * 4;                 // fp32 accumulator tile
   static constexpr int BYTES = LOOP > EPI ? LOOP : EPI;
 };
 
 // OR ("one round"): every workgroup's K slice fits the register ring (host-checked), so the
-// prologue requests all of it and the loop never refills.
-template <int BM, int BN, int BK, int AM, int XA, int EM, bool OR>
+// prologue requests all of it and the loop never refills.  OR == 2: at most two K-steps per slice
+// (the big-M maps: K = 72-288), so the ring is cut to two stages — the registers of the unused
+// stages would otherwise halve the workgroups a CU holds while these launches are latency-bound.
+template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
 __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
   using WG = CgWaves<BM, BN>;
   constexpr int TM = WG::TM, TN = WG::TN, WTM = TM * 16, WTN = TN * 16;
@@ -113,15 +124,19 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
   constexpr int RPP = 256 / KC;                      // rows covered per pass of the block
   constexpr int APT = (BM + RPP - 1) / RPP, BPT = (BN + RPP - 1) / RPP;
   constexpr bool DY = XA == VAE_X_BN_DY;
-  constexpr int NS = cg_stages<APT * (DY ? 2 : 1) + BPT>();
+  constexpr int NSF = cg_stages<APT * (DY ? 2 : 1) + BPT>();
+  constexpr int NS = OR == 2 ? (NSF < 2 ? NSF : 2) : NSF;
+  // OR == 2 keeps one LDS buffer (a barrier between its two steps): with half the LDS, 4-6
+  // workgroups fit a CU instead of 2-3 — these big-M launches have thousands of short workgroups
+  constexpr int NBUF = OR == 2 ? 1 : 2;
   constexpr bool ABN = XA == VAE_X_BN_ACT || XA == VAE_X_BN_DY;
   static_assert(BM % RPP == 0 || BM < RPP, "A tile rows");
   static_assert(BN % RPP == 0 || BN < RPP, "B tile rows");
 
-  __shared__ __attribute__((aligned(16))) char smem[CgSmem<BM, BN, BK>::BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[CgSmem<BM, BN, BK, NBUF>::BYTES];
   extern __shared__ float tabs[];
   __bf16* As = reinterpret_cast<__bf16*>(smem);                 // [2][BM][LDK]
-  __bf16* Bs = As + 2 * BM * LDK;                                // [2][BN][LDK]
+  __bf16* Bs = As + NBUF * BM * LDK;                             // [NBUF][BN][LDK]
 
 #ifdef VAE_PROBE
   unsigned long long clk[4] = {0, 0, 0, 0};
@@ -323,13 +338,14 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
   // step kt+NS (loads past the K range read zeros through the buffer resource)
   // (loads are issued on every path, so the compiler's vmcnt bookkeeping stays exact across
   // the loop back-edge; only the LDS work of steps past the slice's end is skipped)
-  if constexpr (OR) {
+  if constexpr (OR != 0) {
 #pragma unroll
     for (int u = 0; u < NS; ++u) {
       if (kt0 + u < kt1) {
-        store(u & 1, ring[u]);
+        if (NBUF == 1 && u > 0) __syncthreads();        // the previous step's reads of the buffer
+        store(u & (NBUF - 1), ring[u]);
         __syncthreads();
-        compute(u & 1);
+        compute(u & (NBUF - 1));
       }
     }
   } else {

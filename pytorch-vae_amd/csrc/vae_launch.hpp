@@ -506,7 +506,7 @@ inline CgTile cg_pick(long M, long N, int nphase) {
 
 template <int BM, int BN> constexpr int cg_bk() { return BM >= 128 ? 64 : 128; }
 
-template <int AM, int XA, int EM, bool OR>
+template <int AM, int XA, int EM, int OR>
 inline void cg_launch_tile(const GemmParams& p, CgTile t, hipStream_t st) {
   const size_t lds = (size_t)((XA == VAE_X_BN_ACT || XA == VAE_X_BN_DY ? 3 * tab_stride(p.a_xf.channels) : 0) +
                               (EM == E_BNBWD ? 4 * tab_stride(p.epi_xf.channels) : 0)) * 4;
@@ -566,9 +566,10 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   const bool dy = p.a_xf.kind == VAE_X_BN_DY;
   const int KCt = bk / 8, RPPt = 256 / KCt;
   const int loads = ((t.bm + RPPt - 1) / RPPt) * (dy ? 2 : 1) + (t.bn + RPPt - 1) / RPPt;
-  const int ns = 20 / loads < 2 ? 2 : (20 / loads > 8 ? 8 : 20 / loads);   // == cg_stages<loads>()
+  const int ns = cg_ring(loads);                                           // == cg_stages<loads>()
   const bool one = kps <= ns;
-#define VAE_CG_XA(XA_) (one ? cg_launch_tile<AM, XA_, EM, true>(p, t, st) : cg_launch_tile<AM, XA_, EM, false>(p, t, st))
+#define VAE_CG_XA(XA_) (!one ? cg_launch_tile<AM, XA_, EM, 0>(p, t, st) \
+                              : kps <= 2 ? cg_launch_tile<AM, XA_, EM, 2>(p, t, st) : cg_launch_tile<AM, XA_, EM, 1>(p, t, st))
   switch (p.a_xf.kind) {
     case VAE_X_NONE: VAE_CG_XA(VAE_X_NONE); break;
     case VAE_X_ACT: VAE_CG_XA(VAE_X_ACT); break;

@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
   constexpr bool DU = XU == VAE_X_BN_DY, DV = XV == VAE_X_BN_DY;
   constexpr bool BU = XU == VAE_X_BN_ACT || DU, BV = XV == VAE_X_BN_ACT || DV;
   constexpr int LOADS = UPT * (DU ? 2 : 1) + VPT * (DV ? 2 : 1);
-  constexpr int NS = cg_stages<LOADS>();
+  constexpr int NS = wg_stages<LOADS>();
   constexpr int WTM = BM / 2, WTJ = BJ / 2;            // 2 x 2 waves
   constexpr int TM = WTM / 16, TJ = WTJ / 16;
 
@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
 // transformed once and reused by every tap (per-tap workgroups did it R*R times), V is gathered
 // per tap from the pixel decomposition computed once per row.  Accumulators: R*R x the
 // (BM/2 x BJ/2) wave tile.
-template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : cg_stages<LOADS>(); }
+template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : wg_stages<LOADS>(); }
 
 // K-step: every thread loads one 16-byte chunk of U and of each tap's V row — 64 pixels for the
 // 32-channel tiles (128 of the 256 threads idled at 32) — and the LDS holds one step (single
