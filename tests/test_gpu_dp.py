@@ -111,13 +111,15 @@ def test_data_parallel_betaH_matches_oracle_shard_mean():
         assert err < bound, (name, err, bound)
     print(f"DP betaH 2x{B}: worst averaged-gradient rel-norm {worst:.2e}")
     # one Adam step from zero state on the averaged gradient: lr * g / (|g| + eps) elementwise —
-    # compared where the oracle's averaged gradient is clear of the noise floor (sign-stable)
+    # compared where the oracle's averaged gradient is clear of the noise floor (sign-stable) and
+    # of Adam's eps: d/dg [g / (|g| + eps)] = eps / (|g| + eps)^2, so at |g| >= 1e-5 a relative
+    # gradient error e moves the update by at most lr * 1e-3 * e
     for name, gr in gmean.items():
         if name.endswith(".0.bias") and not name.startswith("final_layer.3"):
             continue
         p0 = sd[name].double()
         want = p0 - LR * gr.double() / (gr.double().abs() + 1e-8)
-        ok = gr.abs() > 1e-2 * gr.abs().max()
+        ok = (gr.abs() > 1e-2 * gr.abs().max()) & (gr.abs() > 1e-5)
         np.testing.assert_allclose(state[name].double()[ok].numpy(), want[ok].numpy(), rtol=0,
                                    atol=1e-6 + 1e-3 * LR, err_msg=name)
     for k, v in shards[0]["running"].items():           # rank 0's statistics (broadcast_buffers)
