@@ -43,44 +43,41 @@ __device__ __forceinline__ uint4 cg_xform(const uint32_t (&w)[4], const uint32_t
   if constexpr (XA == VAE_X_NONE) {
     return uint4{w[0], w[1], w[2], w[3]};
   } else {
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[2 * e] = __uint_as_float(w[e] << 16);
-      v[2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
-    }
-    if constexpr (XA == VAE_X_ACT) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = lrelu(v[e], slope);
-    } else if constexpr (XA == VAE_X_BN_ACT) {
-      const f32x4 a0 = tab4(t.a, ch), a1 = tab4(t.a, ch + 4), b0 = tab4(t.b, ch), b1 = tab4(t.b, ch + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = lrelu(fmaf(v[e], a0[e], b0[e]), slope);
-        v[e + 4] = lrelu(fmaf(v[e + 4], a1[e], b1[e]), slope);
-      }
-    } else {  // BN_DY: a*g + b*y + c
-      const f32x4 a0 = tab4(t.a, ch), a1 = tab4(t.a, ch + 4), b0 = tab4(t.b, ch), b1 = tab4(t.b, ch + 4);
-      const f32x4 c0 = tab4(t.c, ch), c1 = tab4(t.c, ch + 4);
-      float u[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        u[2 * e] = __uint_as_float(y[e] << 16);
-        u[2 * e + 1] = __uint_as_float(y[e] & 0xffff0000u);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = fmaf(a0[e], v[e], fmaf(b0[e], u[e], c0[e]));
-        v[e + 4] = fmaf(a1[e], v[e + 4], fmaf(b1[e], u[e + 4], c1[e]));
-      }
-    }
+    // channel pairs (2e, 2e+1) in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: half the VALU issue of
+    // the scalar form — this transform runs once per gathered element, measured +1.5-2 us per
+    // launch in the K loop, tools/kprobe.py) and one v_cvt_pk_bf16_f32 per pair
     uint4 o;
     uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+    f32x2 ab[4], bb[4], cb[4];
+    if constexpr (XA != VAE_X_ACT) {                  // (LeakyReLU alone has no table)
+      const f32x4 a0 = tab4(t.a, ch), a1 = tab4(t.a, ch + 4);
+      ab[0] = f32x2{a0[0], a0[1]}; ab[1] = f32x2{a0[2], a0[3]}; ab[2] = f32x2{a1[0], a1[1]}; ab[3] = f32x2{a1[2], a1[3]};
+      {
+        const f32x4 b0 = tab4(t.b, ch), b1 = tab4(t.b, ch + 4);
+        bb[0] = f32x2{b0[0], b0[1]}; bb[1] = f32x2{b0[2], b0[3]}; bb[2] = f32x2{b1[0], b1[1]}; bb[3] = f32x2{b1[2], b1[3]};
+      }
+      if constexpr (XA == VAE_X_BN_DY) {
+        const f32x4 c0 = tab4(t.c, ch), c1 = tab4(t.c, ch + 4);
+        cb[0] = f32x2{c0[0], c0[1]}; cb[1] = f32x2{c0[2], c0[3]}; cb[2] = f32x2{c1[0], c1[1]}; cb[3] = f32x2{c1[2], c1[3]};
+      }
+    }
+    const f32x2 sl = f32x2{slope, slope};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+      const f32x2 v = f32x2{__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xffff0000u)};
+      f32x2 r;
+      if constexpr (XA == VAE_X_ACT) {
+        r = __builtin_elementwise_max(v, v * sl);
+      } else if constexpr (XA == VAE_X_BN_ACT) {
+        const f32x2 z = __builtin_elementwise_fma(v, ab[e], bb[e]);
+        r = __builtin_elementwise_max(z, z * sl);
+      } else {  // BN_DY: a*g + b*y + c
+        const f32x2 u = f32x2{__uint_as_float(y[e] << 16), __uint_as_float(y[e] & 0xffff0000u)};
+        r = __builtin_elementwise_fma(ab[e], v, __builtin_elementwise_fma(bb[e], u, cb[e]));
+      }
       bf16x2 pk;
-      pk[0] = (__bf16)v[2 * e];
-      pk[1] = (__bf16)v[2 * e + 1];
+      pk[0] = (__bf16)r[0];
+      pk[1] = (__bf16)r[1];
       op[e] = *reinterpret_cast<uint32_t*>(&pk);
     }
     return o;
@@ -254,6 +251,14 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
       for (int q = 0; q < 4; ++q) tve[q][j] = p.epi_xf.table[q * C + ch];
     }
   }
+  // in-kernel BatchNorm tables: their loads go out before the ring's (vae_common.hpp TabPre)
+  // (the reductions' LDS scratch is the operand-tile area, unused until the main loop)
+  TabPre<DY ? 4 : 2> pa;
+  TabPre<2> pe;
+  const bool a_pre = ABN && !a_tab && tab_pre_ok<XA>(p.a_xf);
+  const bool e_pre = EM == E_BNBWD && !e_tab && tab_pre_ok<VAE_X_BN_ACT>(p.epi_xf);
+  if (a_pre) tab_pre_load(p.a_xf, pa);
+  if (e_pre) tab_pre_load(p.epi_xf, pe);
   Stage ring[NS];
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
@@ -272,7 +277,7 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
       }
     }
   } else if constexpr (ABN) {
-    tab_fill(p.a_xf, ta, false, first_block);
+    tab_fill_pre(p.a_xf, pa, a_pre, ta, false, first_block, reinterpret_cast<float*>(smem));
   }
   if constexpr (ABN) {
     if (tid < 8) { const int z = tab_pad(p.a_xf.channels) + tid; ta.a[z] = 0.f; ta.b[z] = 0.f; ta.c[z] = 0.f; }
@@ -285,9 +290,10 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
       if (ch < C) { te.a[ch] = tve[0][j]; te.b[ch] = tve[1][j]; te.p[ch] = tve[2][j]; te.q[ch] = tve[3][j]; }
     }
   } else if constexpr (EM == E_BNBWD) {
-    tab_fill(p.epi_xf, te, true, false);
+    tab_fill_pre(p.epi_xf, pe, e_pre, te, true, false, reinterpret_cast<float*>(smem));
   }
   __syncthreads();
+  PROBE_MARK(1);                                     // probe: operands of the first steps + tables in
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -362,8 +368,8 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
       }
     }
   }
-  // probe marks: 1 = K loop done, 2 = epilogue loads landed, 3 = end
-  PROBE_MARK(1);
+  // probe marks: 1 = prologue done (tables built, first loads landed), 2 = K loop done, 3 = end
+  PROBE_MARK(2);
 #ifdef VAE_PROBE
   struct ProbeEnd {
     unsigned long long* pr; unsigned long long* clk; unsigned long long w0;
@@ -446,10 +452,6 @@ __global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) bias[e] = p.bias[col + e];     // (parameter slices are 4-B aligned only)
   }
-#ifdef VAE_PROBE
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  PROBE_MARK(2);
   // pass 2: apply (outputs stay in registers), per-column sums -> this block's flush, then the
   // stores: nothing waits on the stores (a barrier behind them would drain them: vmcnt(0))
   float s1[8], s2[8];

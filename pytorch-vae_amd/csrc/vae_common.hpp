@@ -291,37 +291,62 @@ __host__ __device__ inline bool bn_fast_ok(const vae_xform& x) {
   return C <= 256 ? (256 % C == 0) : (C % 256 == 0);
 }
 
-__device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, bool update_running) {
-  __shared__ float scr[4][256];
+// The build split in two so a kernel can issue the table's loads BEFORE its operand loads and
+// reduce them after: vmcnt counts in issue order, so table loads issued behind the operand ring
+// wait for every operand load in flight.  TabPre<NS> holds the loaded replicas of the NS
+// statistics the transform needs (2: Σ, Σ² for BN_ACT; 4: + Σg·x̂, Σg for BN_DY) and gamma /
+// beta / shift of the thread's first channel — few registers, since they stay live across the
+// operand loads (C = 512's second channel and the running statistics are loaded in the finish).
+// The LDS scratch of the reduction (1024 floats) is passed in: a kernel hands it a region of its
+// operand tiles that is not in use yet, so the table costs no LDS of its own.
+template <int NS>
+struct TabPre {
+  float v[NS][4];
+  float g, be, sh;
+};
+
+template <int NS>
+__device__ __forceinline__ void tab_pre_load(const vae_xform& x, TabPre<NS>& q) {
   const int C = x.channels, R = x.reps > 1 ? x.reps : 1, tid = threadIdx.x;
   const long rs = x.reps > 1 ? x.rstride : 0;
-  const bool dy = x.kind == VAE_X_BN_DY;
   const int total = R * C;
-  float v[4][4];
+  const float* arr[4] = {x.sum, x.sumsq, x.dgamma, x.dbeta};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int f = tid + 256 * k;
     const bool ok = f < total;
     const int r = ok ? f / C : 0, c = ok ? f - r * C : 0;
     const long o = (long)r * rs + c;
-    v[0][k] = ok ? x.sum[o] : 0.f;
-    v[1][k] = ok ? x.sumsq[o] : 0.f;
-    v[2][k] = (ok && dy) ? x.dgamma[o] : 0.f;
-    v[3][k] = (ok && dy) ? x.dbeta[o] : 0.f;
+#pragma unroll
+    for (int a = 0; a < NS; ++a) q.v[a][k] = ok ? arr[a][o] : 0.f;
   }
+  const int ch = tid < C ? tid : C - 1;
+  q.g = x.gamma[ch];
+  q.be = x.beta[ch];
+  q.sh = x.shift ? x.shift[ch] : 0.0f;
+}
+
+template <int NS>
+__device__ __forceinline__ void tab_pre_finish(const vae_xform& x, const TabPre<NS>& q, Tab t, bool epi,
+                                               bool update_running, float* scr) {
+  const int C = x.channels, R = x.reps > 1 ? x.reps : 1, tid = threadIdx.x;
   // channel totals: C <= 256 -> every element of a thread is channel tid % C; C = 256k -> the
   // thread's elements are channels tid + 256j, each complete after summing its replicas
   float tot[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) tot[j][a] = 0.f;
   int nch = 1;
   if (C <= 256) {
 #pragma unroll
-    for (int a = 0; a < 4; ++a) scr[a][tid] = (v[a][0] + v[a][1]) + (v[a][2] + v[a][3]);
+    for (int a = 0; a < NS; ++a) scr[a * 256 + tid] = (q.v[a][0] + q.v[a][1]) + (q.v[a][2] + q.v[a][3]);
     __syncthreads();
     if (tid < C) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
+      for (int a = 0; a < NS; ++a) {
         float acc = 0.f;
-        for (int j = tid; j < 256; j += C) acc += scr[a][j];
+        for (int j = tid; j < 256; j += C) acc += scr[a * 256 + j];
         tot[0][a] = acc;
       }
     }
@@ -332,26 +357,30 @@ __device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, b
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
+      for (int a = 0; a < NS; ++a) {
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc += ((k % per) == j && k / per < R) ? v[a][k] : 0.f;
+        for (int k = 0; k < 4; ++k) acc += ((k % per) == j && k / per < R) ? q.v[a][k] : 0.f;
         tot[j][a] = acc;
       }
     nch = per;
   }
-  for (int j = 0; j < nch && j < 2; ++j) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (j >= nch) break;
     const int ch = C <= 256 ? tid : tid + 256 * j;
+    const float g = j == 0 ? q.g : x.gamma[ch];
+    const float be = j == 0 ? q.be : x.beta[ch];
+    const float sh = j == 0 ? q.sh : (x.shift ? x.shift[ch] : 0.0f);
     const float inv_m = 1.0f / x.count;
     const float s1 = tot[j][0] * inv_m;
     const float var = fmaxf(tot[j][1] * inv_m - s1 * s1, 0.0f);
-    const float mean = s1 + (x.shift ? x.shift[ch] : 0.0f);
+    const float mean = s1 + sh;
     const float invstd = 1.0f / sqrtf(var + x.eps);
-    const float g = x.gamma[ch];
     if (x.kind == VAE_X_BN_ACT) {
       const float sc = g * invstd;
       t.a[ch] = sc;
-      t.b[ch] = x.beta[ch] - mean * sc;
+      t.b[ch] = be - mean * sc;
       if (epi) { t.p[ch] = invstd; t.q[ch] = -mean * invstd; }
       if (update_running && x.running_mean) {
         const float m = x.momentum;
@@ -367,6 +396,25 @@ __device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, b
       t.c[ch] = -A * (mg - mean * invstd * mgx);
     }
   }
+}
+
+// Both halves at once, with the caller's LDS scratch (1024 floats).
+__device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, bool update_running, float* scr) {
+  if (x.kind == VAE_X_BN_DY) {
+    TabPre<4> q;
+    tab_pre_load(x, q);
+    tab_pre_finish(x, q, t, epi, update_running, scr);
+  } else {
+    TabPre<2> q;
+    tab_pre_load(x, q);
+    tab_pre_finish(x, q, t, epi, update_running, scr);
+  }
+}
+
+// ... with a scratch array of its own (kernels without a free LDS region at that point)
+__device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, bool update_running) {
+  __shared__ float scr[4 * 256];
+  tab_build(x, t, epi, update_running, scr);
 }
 
 }  // namespace vae

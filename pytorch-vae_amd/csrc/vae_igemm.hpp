@@ -142,7 +142,8 @@ __device__ __forceinline__ PhaseInfo make_phase(const GemmParams& p, int phase) 
 // ------------------------------------------------------------------ per-channel tables
 // Fill a transform table (vae_common.hpp Tab): a copy of vae_bn_finalize's precomputed table, or
 // built by this workgroup from the producer's replicated statistics (tab_build).
-__device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bool update_running) {
+// scr: 1024 floats of LDS scratch for the replica reduction, free for the duration of the call.
+__device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bool update_running, float* scr) {
   if (x.kind != VAE_X_BN_ACT && x.kind != VAE_X_BN_DY) return;
   if (threadIdx.x < 8) {
     const int z = tab_pad(x.channels) + threadIdx.x;
@@ -164,7 +165,7 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
     return;
   }
   if (blockDim.x == 256 && bn_fast_ok(x)) {
-    tab_build(x, t, epi, update_running);
+    tab_build(x, t, epi, update_running, scr);
     return;
   }
   for (int ch = threadIdx.x; ch < x.channels; ch += blockDim.x) {
@@ -192,6 +193,30 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
       t.c[ch] = -A * (mg - mean * invstd * mgx);
     }
   }
+}
+
+// tab_fill for kernels without a free operand area at that point: a scratch array of its own
+__device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bool update_running) {
+  __shared__ float scr[4 * 256];
+  tab_fill(x, t, epi, update_running, scr);
+}
+
+// Hoisted table build (TabPre): eligible when the table is built in-kernel on the fast path.
+template <int KIND>
+__device__ __forceinline__ bool tab_pre_ok(const vae_xform& x) {
+  return x.kind == KIND && !x.table && blockDim.x == 256 && bn_fast_ok(x);
+}
+// tab_fill with the loads already issued (pre: tab_pre_load ran for x), else the plain fill
+template <int NS>
+__device__ __forceinline__ void tab_fill_pre(const vae_xform& x, const TabPre<NS>& q, bool pre, Tab t, bool epi,
+                                             bool update_running, float* scr) {
+  if (!pre) { tab_fill(x, t, epi, update_running, scr); return; }
+  if (threadIdx.x < 8) {
+    const int z = tab_pad(x.channels) + threadIdx.x;
+    t.a[z] = 0.f; t.b[z] = 0.f;
+    if (x.kind == VAE_X_BN_DY) t.c[z] = 0.f;
+  }
+  tab_pre_finish(x, q, t, epi, update_running, scr);
 }
 
 __host__ __device__ inline int tab_floats(const vae_xform& x, bool epi) {

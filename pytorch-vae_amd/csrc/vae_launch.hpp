@@ -570,6 +570,10 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   const bool one = kps <= ns;
 #define VAE_CG_XA(XA_) (!one ? cg_launch_tile<AM, XA_, EM, 0>(p, t, st) \
                               : kps <= 2 ? cg_launch_tile<AM, XA_, EM, 2>(p, t, st) : cg_launch_tile<AM, XA_, EM, 1>(p, t, st))
+#ifdef VAE_PROBE
+  // diagnostics only (probe build): time the launch without the A-operand transform
+  if (getenv("VAE_PROBE_NOXF")) { VAE_CG_XA(VAE_X_NONE); return check_launch("cgemm"); }
+#endif
   switch (p.a_xf.kind) {
     case VAE_X_NONE: VAE_CG_XA(VAE_X_NONE); break;
     case VAE_X_ACT: VAE_CG_XA(VAE_X_ACT); break;

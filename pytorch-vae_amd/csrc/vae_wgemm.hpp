@@ -136,11 +136,19 @@ __global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
   float* q0 = tabs + (BU ? 3 * cau : 0);
   const Tab tv{q0, q0 + cav, q0 + 2 * cav, nullptr, nullptr};
 
+  // table loads ahead of the ring's; the reductions' LDS scratch is the V tile area (>= 4 KB,
+  // unused until the main loop)
+  TabPre<DU ? 4 : 2> pu;
+  TabPre<DV ? 4 : 2> pv;
+  const bool u_pre = BU && tab_pre_ok<XU>(p.u_xf), v_pre = BV && tab_pre_ok<XV>(p.v_xf);
+  if (u_pre) tab_pre_load(p.u_xf, pu);
+  if (v_pre) tab_pre_load(p.v_xf, pv);
   Stage ring[NS];
 #pragma unroll
   for (int u = 0; u < NS; ++u) issue(u, ring[u]);
-  if constexpr (BU) tab_fill(p.u_xf, tu, false, false);
-  if constexpr (BV) tab_fill(p.v_xf, tv, false, false);
+  float* const scr = reinterpret_cast<float*>(Vs[0]);
+  if constexpr (BU) tab_fill_pre(p.u_xf, pu, u_pre, tu, false, false, scr);
+  if constexpr (BV) tab_fill_pre(p.v_xf, pv, v_pre, tv, false, false, scr);
   if (blockIdx.x == 0) {
     // the BatchNorm whose backward this call applies: dL/dgamma, dL/dbeta (+ conv bias) once
     const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
@@ -347,11 +355,19 @@ __global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
   float* q0 = tabs + (BU ? 3 * cau : 0);
   const Tab tv{q0, q0 + cav, q0 + 2 * cav, nullptr, nullptr};
 
+  // table loads ahead of the ring's; the reductions' LDS scratch is the V tile area (>= 4 KB,
+  // unused until the main loop)
+  TabPre<DU ? 4 : 2> pu;
+  TabPre<DV ? 4 : 2> pv;
+  const bool u_pre = BU && tab_pre_ok<XU>(p.u_xf), v_pre = BV && tab_pre_ok<XV>(p.v_xf);
+  if (u_pre) tab_pre_load(p.u_xf, pu);
+  if (v_pre) tab_pre_load(p.v_xf, pv);
   Stage ring[NS];
 #pragma unroll
   for (int u = 0; u < NS; ++u) issue(u, ring[u]);
-  if constexpr (BU) tab_fill(p.u_xf, tu, false, false);
-  if constexpr (BV) tab_fill(p.v_xf, tv, false, false);
+  float* const scr = reinterpret_cast<float*>(Vs[0][0]);
+  if constexpr (BU) tab_fill_pre(p.u_xf, pu, u_pre, tu, false, false, scr);
+  if constexpr (BV) tab_fill_pre(p.v_xf, pv, v_pre, tv, false, false, scr);
   if (blockIdx.x == 0) {
     const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
     if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
