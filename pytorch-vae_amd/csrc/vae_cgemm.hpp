@@ -112,8 +112,16 @@ template <int BM, int BN, int BK, int NBUF = 2> struct CgSmem {
 // prologue requests all of it and the loop never refills.  OR == 2: at most two K-steps per slice
 // (the big-M maps: K = 72-288), so the ring is cut to two stages — the registers of the unused
 // stages would otherwise halve the workgroups a CU holds while these launches are latency-bound.
+// Waves per SIMD the register allocation must leave room for: the 128 x 128 tiles (VQ-VAE's
+// MFMA-bound convolutions) otherwise take ~300 VGPRs + AGPRs = one workgroup per CU, 4 waves to
+// hide every load; the 64 x 32 BatchNorm-backward dgrad tiles fit 3 workgroups in LDS.
+template <int BM, int BN, int XA> constexpr int cg_waves_per_eu() {
+  return (BM >= 128 && BN >= 128) ? 2 : ((BM == 64 && BN == 32 && XA == VAE_X_BN_DY) ? 3 : 1);
+}
+
 template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
-__global__ void __launch_bounds__(256) cgemm_kernel(const GemmParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg_waves_per_eu<BM, BN, XA>())))
+cgemm_kernel(const GemmParams p) {
   using WG = CgWaves<BM, BN>;
   constexpr int TM = WG::TM, TN = WG::TN, WTM = TM * 16, WTN = TN * 16;
   constexpr int LDK = CgSmem<BM, BN, BK>::LDK;

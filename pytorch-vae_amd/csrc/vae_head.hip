@@ -243,7 +243,9 @@ __device__ __forceinline__ float gseed(const HeadQ& q, int n, const SeedLd& ld, 
 constexpr int NW = NCO * 9 * HC;        // 864 weight-gradient entries
 constexpr int SLAB_COLS = NW + NCO;     // + 3 bias-gradient entries
 
-__global__ void __launch_bounds__(256) head_bwd_mfma(HeadQ q) {
+// Registers capped for 2 workgroups per CU (VAE_HEAD_GRID=512 then runs two tiles in flight per
+// CU; at the default grid of 256 the cap only bounds the allocation).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_bwd_mfma(HeadQ q) {
   __shared__ __attribute__((aligned(16))) char tile[TPIX * HC * 2];
   __shared__ __attribute__((aligned(16))) uint2 gsA[TPIX];               // [pixel][co0..2, 0] bf16
   __shared__ __attribute__((aligned(16))) __bf16 gsT[4][OWN];            // [co][own pixel]
@@ -535,7 +537,9 @@ int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
 // filter partials to reduce and more halo re-reads; fewer leaves CUs idle).
 // Re-swept with the tile-ahead loads: 192 -> 50.4 us, 256 -> 38.5, 320 -> 55.6, 384 -> 49.8,
 // 512 -> 43.9 (scripts/gpu_headgrid.sh): 256 divides the 1024 tiles of B=64 evenly.
-constexpr int kHeadGrid = 256;
+// r2: with the registers capped for 2 workgroups per CU (amdgpu_waves_per_eu(2)), 512 -> 37.2 us
+// (two tiles in flight per CU), 256 -> 45.1 (the cap's spills without the second workgroup).
+constexpr int kHeadGrid = 512;
 // VAE_HEAD_GRID overrides it (tuning sweeps only; read once)
 int head_grid() {
   static const int g = [] {

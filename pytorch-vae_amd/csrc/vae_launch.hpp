@@ -472,7 +472,8 @@ inline bool cg_ok(const GemmParams& p, int em) {
   if (k == VAE_X_BN_DY && !aligned(p.a_xf.aux, 16)) return false;
   if (p.residual && !aligned(p.residual, 16)) return false;
   if (em == E_BNBWD && p.epi_xf.kind != VAE_X_NONE) {
-    if (!aligned(p.epi_xf.aux, 16) || p.epi_xf.channels % 8) return false;
+    // (a plain LeakyReLU epilogue has no per-channel table: its channel count is not read)
+    if (!aligned(p.epi_xf.aux, 16) || (p.epi_xf.kind == VAE_X_BN_ACT && p.epi_xf.channels % 8)) return false;
   }
   return true;
 }

@@ -53,7 +53,8 @@ __device__ __forceinline__ wgm_bf16x4 wgm_tr_read(const char* generic_lds_addr) 
 }
 
 template <int BM, int BJ, int XU, int XV>
-__global__ void __launch_bounds__(256) wgemm_kernel(const WgParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM >= 128 ? 2 : 1)))
+wgemm_kernel(const WgParams p) {
   constexpr int KP = 32;                               // pixels per K-step
   constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int CU = BM / 8, CV = BJ / 8;              // 16-byte chunks per pixel row
@@ -533,6 +534,11 @@ inline void wg2_launch_k(const WgParams& p, unsigned blocks, hipStream_t st) {
     // 32 x 32 tiles of 3x3 kernels: every tap in one workgroup (the grid was sized without the
     // tap factor); larger tiles / kernels would exceed the LDS and register budget
     if (p.R == 3) { VAE_LAUNCH((wgemm_taps_kernel<BM, BJ, XU, XV, 3>), dim3(blocks), dim3(256), lds, st, p); return; }
+    // 4x4 kernels without BatchNorm transforms (VQ-VAE's RGB ends, 8-channel padded side): the
+    // wide operand is read once per K-step for all 16 taps instead of once per tap (wg_taps)
+    if constexpr (XU <= VAE_X_ACT && XV <= VAE_X_ACT) {
+      if (p.R == 4) { VAE_LAUNCH((wgemm_taps_kernel<BM, BJ, XU, XV, 4>), dim3(blocks), dim3(256), lds, st, p); return; }
+    }
   }
   VAE_LAUNCH((wgemm_kernel<BM, BJ, XU, XV>), dim3(blocks), dim3(256), lds, st, p);
 }
@@ -576,7 +582,7 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   // tile: square, the largest whose both sides fit the channel counts
   const int mn = p.M < p.J ? p.M : p.J;
   const int T = mn >= 128 ? 128 : (mn >= 64 ? 64 : 32);
-  const bool taps_in_block = T == 32 && p.R == 3;
+  const bool taps_in_block = T == 32 && (p.R == 3 || (p.R == 4 && p.u_xf.kind <= VAE_X_ACT && p.v_xf.kind <= VAE_X_ACT));
   const long tiles = (long)((p.M + T - 1) / T) * ((p.J + T - 1) / T) * (taps_in_block ? 1 : p.R * p.R);
   const long ksteps = (npix + 31) / 32;
   // K slices: ~2 workgroups per CU, >= 4 K-steps per slice

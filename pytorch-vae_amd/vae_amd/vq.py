@@ -24,7 +24,7 @@ import torch
 
 from . import _lib as L
 from .layout import Layout, default_init, vq_layout, vq_param_spec
-from .net import SLOPE, _pad4, run_calls, size_workspaces
+from .net import SLOPE, _pad4, make_swaps, run_calls, size_workspaces
 
 NRES = 6             # ResidualLayers per stack (vq_vae.py:111, :138)
 
@@ -55,6 +55,8 @@ class VQNet:
         self.lowp = (torch.zeros(self.layout.total, dtype=torch.bfloat16, device=self.device)
                      if dtype == torch.bfloat16 else None)
         self.num_batches_tracked = 0
+        self.wt_t: Dict[str, int] = {}
+        self.swap_descs = None
         self.sync_lowp()
 
     @property
@@ -64,6 +66,40 @@ class VQNet:
     def sync_lowp(self):
         if self.lowp is not None:
             L.call("vae_cast_bf16", self.params.numel(), self.params.data_ptr(), self.lowp.data_ptr(), L.stream_ptr())
+            self.refresh_swaps()
+
+    def ensure_swaps(self, names):
+        """bf16 mode: swapped-axes copies (vaehip.h wt_t) of the named weights — the ones the bf16
+        conv-GEMMs read transposed (every data gradient and transposed-conv forward) — refreshed
+        with the bf16 copy (sync_lowp, FusedAdam.apply) in vae_swap_axes launches of SWAP_MAX
+        weights, instead of one transposition per call per step."""
+        if self.lowp is None:
+            return
+        new = sorted(set(names) - set(self.wt_t))
+        if not new:
+            return
+        # copies already handed out stay where they are (plans built earlier point at them)
+        chunks, bufs = list(self.swap_descs or ()), list(getattr(self, "lowp_t", ()))
+        for i in range(0, len(new), L.SWAP_MAX):
+            d, b = make_swaps(self.layout, self.params, new[i:i + L.SWAP_MAX], self.device, self.wt_t)
+            chunks.append(d)
+            bufs.append(b)
+        self.swap_descs, self.lowp_t = chunks, bufs
+        self.refresh_swaps()
+
+    def refresh_swaps(self, stream=None):
+        for d in self.swap_descs or ():
+            L.call("vae_swap_axes", len(d), ctypes.byref(d), stream if stream is not None else L.stream_ptr())
+
+    def name_of_lowp(self, ptr: int) -> Optional[str]:
+        """Parameter name whose bf16 copy starts at device pointer `ptr` (None: not a bf16 weight)."""
+        if self.lowp is None:
+            return None
+        off = (ptr - self.lowp.data_ptr()) // 2
+        for s in self.layout.params:
+            if s.offset == off:
+                return s.name
+        return None
 
     def load_reference_state_dict(self, sd: Dict[str, torch.Tensor]):
         self.layout.load_reference(self.params, self.running, {k: v.to(self.device) for k, v in sd.items()})
@@ -175,7 +211,25 @@ class VQStepPlan:
         self.bwd_calls: List = []
         self.side = torch.cuda.Stream(device=dev) if concurrent else None     # weight gradients (run_calls)
         self._build()
+        self._attach_swaps()
         size_workspaces(self, [self.fwd_calls, self.bwd_calls])
+
+    def _attach_swaps(self):
+        """Point every data gradient and transposed-conv forward at the net's swapped-axes weight
+        copy (vaehip.h wt_t: read by the bf16 conv-GEMM as k-contiguous rows), so no call
+        transposes its weights itself (one vae_swap_axes pass per SWAP_MAX weights per step)."""
+        net = self.net
+        if net.lowp is None:
+            return
+        use = []
+        for fn, ref in self.fwd_calls + self.bwd_calls:
+            if fn in ("vae_conv2d_bwd_data", "vae_convT2d_fwd") and not isinstance(ref, tuple):
+                name = net.name_of_lowp(ref._obj.wt or 0)
+                if name is not None:
+                    use.append((ref._obj, name))
+        net.ensure_swaps([n for _, n in use])
+        for arg, name in use:
+            arg.wt_t = net.wt_t[name]
 
     # ------------------------------------------------------------------ helpers
     def g(self, name: str) -> int:

@@ -27,12 +27,12 @@ def code_object(obj, tmp):
 
 def kernels(co):
     out = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True, text=True).stdout
-    for blk in out.split("      - .agpr_count:")[1:]:
+    for blk in out.split("- .agpr_count:")[1:]:
         def f(key):
             m = re.search(r"\." + key + r":\s+(\S+)", blk)
             return m.group(1) if m else None
         yield {"name": f("name"), "vgpr": int(f("vgpr_count") or 0), "agpr": int(re.match(r"\s*(\d+)", blk).group(1)),
-               "lds": int(f("group_segment_fixed_size") or 0), "sgpr": int(f("sgpr_count") or 0)}
+               "lds": int(f("group_segment_fixed_size") or 0), "scratch": int(f("private_segment_fixed_size") or 0), "sgpr": int(f("sgpr_count") or 0)}
 
 
 def main():
@@ -47,7 +47,8 @@ def main():
                 regs = ((k["vgpr"] + 7) // 8) * 8 + ((k["agpr"] + 7) // 8) * 8 if k["agpr"] else ((k["vgpr"] + 7) // 8) * 8
                 w_reg = min(8, 512 // max(regs, 1))
                 w_lds = min(8, (163840 // max(k["lds"], 1)) * 4 // 4) if k["lds"] else 8
-                print(f"{k['vgpr']:4d}v {k['agpr']:3d}a {k['lds']:6d}B  waves/SIMD<=reg {w_reg} lds-wg/CU {w_lds}  {k['name']}")
+                name = subprocess.run(["c++filt", k["name"]], capture_output=True, text=True).stdout.strip()
+                print(f"{k['vgpr']:4d}v {k['agpr']:3d}a {k['lds']:6d}B {k['scratch']:4d}S  waves/SIMD<=reg {w_reg} lds-wg/CU {w_lds}  {name[:150]}")
 
 
 if __name__ == "__main__":
