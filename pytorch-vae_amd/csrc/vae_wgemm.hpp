@@ -55,7 +55,9 @@ __device__ __forceinline__ wgm_bf16x4 wgm_tr_read(const char* generic_lds_addr) 
 template <int BM, int BJ, int XU, int XV>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM >= 128 ? 2 : 1)))
 wgemm_kernel(const WgParams p) {
-  constexpr int KP = 32;                               // pixels per K-step
+  // pixels per K-step: 64 for the 128 x 128 tiles (VQ-VAE's residual convs: half the barriers per
+  // MFMA; two workgroups still fit a CU's LDS), 32 below
+  constexpr int KP = BM >= 128 ? 64 : 32;
   constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int CU = BM / 8, CV = BJ / 8;              // 16-byte chunks per pixel row
   constexpr int RPU = 256 / CU, RPV = 256 / CV;        // pixel rows per pass
@@ -206,23 +208,28 @@ wgemm_kernel(const WgParams p) {
     for (int j = 0; j < TJ; ++j) boff[j][h] = row * RSV + (wn * WTJ + j * 16 + 4 * p4) * 2;
   }
   auto compute = [&](int buf) {
-    bf16x8 af[TM], bfr[TJ];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const wgm_bf16x4 a0 = wgm_tr_read(Us[buf] + aoff[i][0]), a1 = wgm_tr_read(Us[buf] + aoff[i][1]);
+    for (int kk = 0; kk < KP / 32; ++kk) {             // MFMA K = 32 pixels
+      bf16x8 af[TM], bfr[TJ];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+      for (int i = 0; i < TM; ++i) {
+        const wgm_bf16x4 a0 = wgm_tr_read(Us[buf] + kk * 32 * RSU + aoff[i][0]);
+        const wgm_bf16x4 a1 = wgm_tr_read(Us[buf] + kk * 32 * RSU + aoff[i][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const wgm_bf16x4 b0 = wgm_tr_read(Vs[buf] + kk * 32 * RSV + boff[j][0]);
+        const wgm_bf16x4 b1 = wgm_tr_read(Vs[buf] + kk * 32 * RSV + boff[j][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bfr[j][e] = b0[e]; bfr[j][4 + e] = b1[e]; }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const wgm_bf16x4 b0 = wgm_tr_read(Vs[buf] + boff[j][0]), b1 = wgm_tr_read(Vs[buf] + boff[j][1]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { bfr[j][e] = b0[e]; bfr[j][4 + e] = b1[e]; }
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   };
 
   // main loop (vae_cgemm.hpp: loads issued on every path, LDS work skipped past the slice)
@@ -269,7 +276,8 @@ template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : wg_sta
 // buffer, two barriers per step) so two workgroups still fit a CU: each memory round trip (the
 // loop is latency-bound, one step in flight per ring slot) now carries twice the MFMA work.
 template <int BM, int BJ, int XU, int XV, int RR>
-__global__ void __launch_bounds__(256) wgemm_taps_kernel(const WgParams p) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR >= 4 ? 2 : 1)))
+wgemm_taps_kernel(const WgParams p) {
   constexpr int TAPS = RR * RR;
   constexpr int CU = BM / 8, CV = BJ / 8;
   constexpr int RPU = 256 / CU, RPV = 256 / CV;
