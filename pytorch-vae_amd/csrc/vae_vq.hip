@@ -17,8 +17,6 @@
 namespace vae {
 namespace {
 
-constexpr int VQ_ROWS = 64;        // latent rows per workgroup (fwd)
-constexpr int VQ_CHUNK = 64;       // codes per LDS chunk
 constexpr int VQB_RUN = 32;        // rows per thread (bwd)
 
 template <class T>
@@ -27,79 +25,160 @@ __device__ __forceinline__ float lat_val(const T* lat, long i, const vae_xform& 
   return xf.kind == VAE_X_ACT ? lrelu(v, xf.slope) : v;
 }
 
+// Distance GEMM on the f32-input MFMA (v_mfma_f32_16x16x4_f32: an exact k-ordered fmaf chain,
+// 64 FLOP/clk/SIMD — 10x what the LDS-fed VALU loop of r1 reached, 15 TF/s).  A workgroup owns
+// 128 latent rows (4 waves x 2 blocks of 16); lane l supplies, for k-step s, dimension
+// (l>>4)*S + s of its row (A) and of its code (B) — any k permutation gives the same dot
+// product's terms, and this one makes both fragments contiguous 16-float runs.  The codebook is
+// staged through LDS in chunks of VQF_CH codes (rows padded to D+4 floats: conflict-free
+// 16-byte reads), the next chunk prefetched into registers while the current one is scored.
+// Output tile: lane l holds code (l&15) of the block for rows 4*(l>>4)+i, so each lane scans its
+// codes in ascending order (strict <: first minimum) and the 16 lanes of a row combine
+// (distance, index) lexicographically: torch.argmin's first-minimum tie-break.
+constexpr int VQF_ROWS = 128;      // latent rows per workgroup
+constexpr int VQF_CH = 128;        // codes per LDS chunk
+
 template <class T, int D>
 __global__ void __launch_bounds__(256) vq_fwd_kernel(vae_vq_args a) {
-  __shared__ __attribute__((aligned(16))) float cb[VQ_CHUNK * D];
-  __shared__ float cn[VQ_CHUNK];
+  constexpr int S = D / 4;                         // k-steps (dims per lane)
+  constexpr int LDC = D + 4;                       // padded codebook row (floats)
+  constexpr int PF = VQF_CH * D / 4 / 256;         // 16-byte codebook vectors per thread per chunk
+  __shared__ __attribute__((aligned(16))) float cb[VQF_CH * LDC];
+  __shared__ float cn[VQF_CH];
+  __shared__ float zzs[VQF_ROWS];
+  __shared__ int bix[VQF_ROWS];
   __shared__ float red[4];
-  const int tid = threadIdx.x;
-  const int lr = tid >> 2, qt = tid & 3;           // local row, quarter
-  const long row = (long)blockIdx.x * VQ_ROWS + lr;
-  const bool ok = row < a.rows;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = lane >> 4, lc = lane & 15;
+  const long row0 = (long)blockIdx.x * VQF_ROWS;
   const T* lat = static_cast<const T*>(a.lat);
-  float z[D];
-  float zz = 0.f;
+  const f32x4* cbg = reinterpret_cast<const f32x4*>(a.codebook);
+  const long cb_vecs = (long)a.codes * D / 4;
+
+  // A fragments: rows row0 + wave*32 + rb*16 + lc, dims kg*S + s
+  float af[2][S];
+  float zp[2];
 #pragma unroll
-  for (int e = 0; e < D; ++e) {
-    z[e] = ok ? lat_val(lat, row * D + e, a.lat_xf) : 0.f;
-    zz = fmaf(z[e], z[e], zz);
+  for (int rb = 0; rb < 2; ++rb) {
+    const long r = row0 + wave * 32 + rb * 16 + lc;
+    const bool ok = r < a.rows;
+    float s2 = 0.f;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      af[rb][s] = ok ? lat_val(lat, r * D + kg * S + s, a.lat_xf) : 0.f;
+      s2 = fmaf(af[rb][s], af[rb][s], s2);
+    }
+    zp[rb] = s2;
   }
-  float best = INFINITY;
-  int bidx = 0x7fffffff;
-  for (int c0 = 0; c0 < a.codes; c0 += VQ_CHUNK) {
-    const int nc = min(VQ_CHUNK, a.codes - c0);
-    __syncthreads();
-    for (int i = tid; i < nc * D; i += 256) cb[i] = a.codebook[(long)c0 * D + i];
-    __syncthreads();
-    if (tid < nc) {
-      float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < D; ++e) s = fmaf(cb[tid * D + e], cb[tid * D + e], s);
-      cn[tid] = s;
+  for (int rb = 0; rb < 2; ++rb) {
+    float s2 = zp[rb];
+    s2 += __shfl_xor(s2, 16);
+    s2 += __shfl_xor(s2, 32);
+    if (kg == 0) zzs[wave * 32 + rb * 16 + lc] = s2;
+  }
+
+  f32x4 pf[PF];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const long v = (long)c0 * D / 4 + tid + 256 * j;
+      pf[j] = v < cb_vecs ? cbg[v] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  fetch(0);
+  __syncthreads();                                  // zzs
+  float zz[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) zz[rb][i] = zzs[wave * 32 + rb * 16 + kg * 4 + i];
+
+  float best[2][4];
+  int bidx[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { best[rb][i] = INFINITY; bidx[rb][i] = 0x7fffffff; }
+
+  for (int c0 = 0; c0 < a.codes; c0 += VQF_CH) {
+    const int nc = min(VQF_CH, a.codes - c0);
+    __syncthreads();                                // previous chunk fully consumed
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int v = tid + 256 * j;                  // vector within the chunk
+      const int code = v / (D / 4), e4 = v - code * (D / 4);
+      *reinterpret_cast<f32x4*>(cb + code * LDC + 4 * e4) = pf[j];
+    }
+    if (c0 + VQF_CH < a.codes) fetch(c0 + VQF_CH);
+    __syncthreads();
+    if (tid < VQF_CH) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < D; ++e) s2 = fmaf(cb[tid * LDC + e], cb[tid * LDC + e], s2);
+      cn[tid] = s2;
     }
     __syncthreads();
-    // codes qt, qt+4, ... of the chunk: the 4 threads of a row interleave, so a run of equal
-    // distances is still scanned in ascending index order by the final combine
-    for (int j = qt; j < nc; j += 4) {
-      const f32x4* cr = reinterpret_cast<const f32x4*>(cb + j * D);
-      float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+    for (int cbk = 0; cbk < nc; cbk += 16) {
+      float bf[S];
+      const float* src = cb + (cbk + lc) * LDC + kg * S;
 #pragma unroll
-      for (int e4 = 0; e4 < D / 4; ++e4) {
-        const f32x4 w = cr[e4];
-        d0 = fmaf(z[4 * e4 + 0], w[0], d0);
-        d1 = fmaf(z[4 * e4 + 1], w[1], d1);
-        d2 = fmaf(z[4 * e4 + 2], w[2], d2);
-        d3 = fmaf(z[4 * e4 + 3], w[3], d3);
+      for (int s4 = 0; s4 < S / 4; ++s4) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(src + 4 * s4);
+        bf[4 * s4 + 0] = w[0]; bf[4 * s4 + 1] = w[1]; bf[4 * s4 + 2] = w[2]; bf[4 * s4 + 3] = w[3];
       }
-      const float dot = (d0 + d1) + (d2 + d3);
-      const float dist = (zz + cn[j]) - 2.f * dot;
-      if (dist < best) { best = dist; bidx = c0 + j; }      // strict: first minimum in this thread
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[0][s], bf[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(af[1][s], bf[s], acc1, 0, 0, 0);
+      }
+      const int code = cbk + lc;
+      if (code < nc) {
+        const float c2 = cn[code];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float d0 = (zz[0][i] + c2) - 2.f * acc0[i];
+          const float d1 = (zz[1][i] + c2) - 2.f * acc1[i];
+          if (d0 < best[0][i]) { best[0][i] = d0; bidx[0][i] = c0 + code; }
+          if (d1 < best[1][i]) { best[1][i] = d1; bidx[1][i] = c0 + code; }
+        }
+      }
     }
   }
-  // combine the 4 threads of the row: smaller distance, ties -> smaller index
+  // combine the 16 lanes of each row: smaller distance, ties -> smaller index
 #pragma unroll
-  for (int off = 1; off < 4; off <<= 1) {
-    const float ob = __shfl_xor(best, off);
-    const int oi = __shfl_xor(bidx, off);
-    if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-  }
-  if (bidx == 0x7fffffff) bidx = 0;                          // all-NaN row: torch returns a NaN's index; keep in range
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float b = best[rb][i];
+      int bi = bidx[rb][i];
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        const float ob = __shfl_xor(b, off);
+        const int oi = __shfl_xor(bi, off);
+        if (ob < b || (ob == b && oi < bi)) { b = ob; bi = oi; }
+      }
+      if (bi == 0x7fffffff) bi = 0;                 // all-NaN row: keep the index in range
+      if (lc == 0) bix[wave * 32 + rb * 16 + kg * 4 + i] = bi;
+    }
+  __syncthreads();
+  // indices, q = E[idx] (coalesced over the tile's rows x D), sum (q - z)^2
   float sse = 0.f;
-  if (ok) {
-    if (qt == 0) a.indices[row] = bidx;
-    T* q = static_cast<T*>(a.q);
-    const float* er = a.codebook + (long)bidx * D;
-#pragma unroll
-    for (int e = 0; e < D; ++e) {
-      if ((e / (D / 4)) != qt) continue;
-      const float v = er[e];
-      q[row * D + e] = cvt<T>(v);
-      const float d = v - z[e];
-      sse = fmaf(d, d, sse);
-    }
+  if (tid < VQF_ROWS && row0 + tid < a.rows) a.indices[row0 + tid] = bix[tid];
+  T* q = static_cast<T*>(a.q);
+#pragma unroll 4
+  for (int j = tid; j < VQF_ROWS * D; j += 256) {
+    const int lr = j / D, e = j - lr * D;
+    const long r = row0 + lr;
+    if (r >= a.rows) break;
+    const float v = a.codebook[(long)bix[lr] * D + e];
+    q[r * D + e] = cvt<T>(v);
+    const float d = v - lat_val(lat, r * D + e, a.lat_xf);
+    sse = fmaf(d, d, sse);
   }
   for (int off = 32; off > 0; off >>= 1) sse += __shfl_xor(sse, off);
-  if ((tid & 63) == 0) red[tid >> 6] = sse;
+  if (lane == 0) red[wave] = sse;
   __syncthreads();
   if (tid == 0) atomicAdd(a.sse, (red[0] + red[1]) + (red[2] + red[3]));
 }
@@ -191,7 +270,7 @@ int vq_check(const vae_vq_args* a, const char* what) {
 
 template <int D>
 int vq_fwd_launch(const vae_vq_args* a, hipStream_t st) {
-  const dim3 grid((a->rows + VQ_ROWS - 1) / VQ_ROWS);
+  const dim3 grid((a->rows + VQF_ROWS - 1) / VQF_ROWS);
   if (a->dtype == VAE_F32) VAE_LAUNCH((vq_fwd_kernel<float, D>), grid, dim3(256), 0, st, *a);
   else VAE_LAUNCH((vq_fwd_kernel<__bf16, D>), grid, dim3(256), 0, st, *a);
   return check_launch("vq_fwd");
@@ -274,6 +353,7 @@ extern "C" int vae_vq_fwd(const vae_vq_args* a, void* stream) {
   int rc = vq_check(a, "vq_fwd");
   if (rc) return rc;
   if (!a->indices || !a->q || !a->sse) return fail(VAE_E_BADARG, "vq_fwd: indices / q / sse");
+  if (reinterpret_cast<uintptr_t>(a->codebook) % 16) return fail(VAE_E_BADARG, "vq_fwd: codebook not 16-byte aligned");
   const hipStream_t st = (hipStream_t)stream;
   if (a->dim == 64) return vq_fwd_launch<64>(a, st);
   if (a->dim == 32) return vq_fwd_launch<32>(a, st);
