@@ -593,9 +593,14 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   const bool taps_in_block = T == 32 && (p.R == 3 || (p.R == 4 && p.u_xf.kind <= VAE_X_ACT && p.v_xf.kind <= VAE_X_ACT));
   const long tiles = (long)((p.M + T - 1) / T) * ((p.J + T - 1) / T) * (taps_in_block ? 1 : p.R * p.R);
   const long ksteps = (npix + 31) / 32;
-  // K slices: ~2 workgroups per CU, >= 4 K-steps per slice
+  // K slices: ~2 workgroups per CU, >= 4 K-steps per slice (16 for 1x1 kernels: their few output
+  // tiles would otherwise be split hundreds of ways and every slice adds its whole tile into dw
+  // with fp32 atomics — measured on the VQ-VAE residual 1x1 (M = J = 256, 32768 pixels): 128
+  // slices 44.4 us, 64 slices 32.7 us, 32 slices 32.5 us, 16 slices 48.7 us; the 3x3 layers and
+  // VanillaVAE's are slower with the higher floor, scripts/gpu_r2_wgsweep2.sh)
   static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
-  static const int mink = tune_env("VAE_WG_MINK", 4);
+  static const int mink_env = tune_env("VAE_WG_MINK", 0);
+  const int mink = mink_env > 0 ? mink_env : (p.R == 1 ? 16 : 4);
   long split = ((long)wgpercu * kCUs + tiles - 1) / tiles;
   if (split > ksteps / mink) split = ksteps / mink;
   if (split < 1) split = 1;
