@@ -601,8 +601,13 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
   static const int mink_env = tune_env("VAE_WG_MINK", 0);
   const int mink = mink_env > 0 ? mink_env : (p.R == 1 ? 16 : 4);
-  long split = ((long)wgpercu * kCUs + tiles - 1) / tiles;
+  const long slots = (long)wgpercu * kCUs;
+  long split = (slots + tiles - 1) / tiles;
   if (split > ksteps / mink) split = ksteps / mink;
+  // one round of workgroups: ceil(slots / tiles) slices overfill the slots by up to tiles - 1
+  // workgroups, which then run as a second round on a few CUs (VQ-VAE 3x3: 36 tiles x 15 slices
+  // = 540 workgroups for 512 slots) — take floor(slots / tiles) slices instead
+  if (tiles * split > slots && tiles <= slots && !getenv("VAE_WG_NOQUANT")) split = slots / tiles;
   if (split < 1) split = 1;
   p.kper = (int)(((ksteps + split - 1) / split) * 32);
   split = (npix + p.kper - 1) / p.kper;
