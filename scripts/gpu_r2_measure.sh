@@ -6,7 +6,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out
 mkdir -p $O
 cd $R
-timeout -k 10 300 python3 -u bench.py --steps 200 --warmup 20 > $O/${TAG}_vanilla.log 2>&1 || exit $?
+timeout -k 10 300 python3 -u bench.py --steps 200 --warmup 20 --kernel-breakdown > $O/${TAG}_vanilla.log 2>&1 || exit $?
 timeout -k 10 240 python3 -u bench.py --arch betaH --batch 32 --steps 200 --warmup 20 --no-cpu-baseline > $O/${TAG}_betaH.log 2>&1 || exit $?
 timeout -k 10 240 python3 -u bench.py --arch iwae --batch 64 --steps 100 --warmup 10 --no-cpu-baseline > $O/${TAG}_iwae.log 2>&1 || exit $?
 timeout -k 10 300 python3 -u bench.py --arch vq --batch 128 --steps 50 --warmup 5 --no-cpu-baseline --kernel-breakdown > $O/${TAG}_vq.log 2>&1 || exit $?
