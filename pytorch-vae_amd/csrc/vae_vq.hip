@@ -36,6 +36,7 @@ __device__ __forceinline__ float lat_val(const T* lat, long i, const vae_xform& 
 // codes in ascending order (strict <: first minimum) and the 16 lanes of a row combine
 // (distance, index) lexicographically: torch.argmin's first-minimum tie-break.
 constexpr int VQF_CH = 128;        // codes per LDS chunk
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 // RB: 16-row blocks per wave (workgroup = 4 waves x RB x 16 rows)
 template <class T, int D, int RB>
@@ -230,9 +231,21 @@ __global__ void __launch_bounds__(256) recon_kernel(vae_recon_args a, int bwd) {
   const long img = pix / hw, sp = pix - img * hw;
   const T* y = static_cast<const T*>(a.y);
   const int ld = a.ld > 0 ? a.ld : C;
+  // bf16 rows of 8 (the packed RGB ends): one 16-byte load of y and one 16-byte store of dy per pixel
+  const bool pk = sizeof(T) == 2 && ld == 8 && ((uintptr_t)a.y & 15) == 0 && ((uintptr_t)a.dy & 15) == 0;
+  float yv[C];
+  if (!bwd) {
+    if (pk) {
+      const u32x4v w = *reinterpret_cast<const u32x4v*>(y + pix * 8);
+#pragma unroll
+      for (int c = 0; c < C; ++c) yv[c] = __uint_as_float(((c & 1) ? (w[c >> 1] >> 16) : (w[c >> 1] & 0xffffu)) << 16);
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) yv[c] = ld_f(y + pix * ld + c);
+    }
+  }
   float sse = 0.f;
-  if (a.dy)
-    for (int c = C; c < ld; ++c) static_cast<T*>(a.dy)[pix * ld + c] = cvt<T>(0.f);
+  float gv[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const long o = (img * C + c) * hw + sp;                  // NCHW
@@ -240,14 +253,27 @@ __global__ void __launch_bounds__(256) recon_kernel(vae_recon_args a, int bwd) {
     if (bwd) {
       r = a.recon[o];
     } else {
-      r = tanhf(ld_f(y + pix * ld + c));
+      r = tanhf(yv[c]);
       a.recon[o] = r;
     }
     const float d = r - a.target[o];
     sse = fmaf(d, d, sse);
-    if (a.dy) {
-      const float g = a.grad_recon ? a.grad_recon[o] : a.grad_scale * 2.f * d;
-      static_cast<T*>(a.dy)[pix * ld + c] = cvt<T>(g * (1.f - r * r));
+    gv[c] = 0.f;
+    if (a.dy) gv[c] = (a.grad_recon ? a.grad_recon[o] : a.grad_scale * 2.f * d) * (1.f - r * r);
+  }
+  if (a.dy) {
+    if (pk) {
+      u32x4v w = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const uint32_t b = (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)gv[c]);
+        w[c >> 1] |= (c & 1) ? (b << 16) : b;
+      }
+      *reinterpret_cast<u32x4v*>(static_cast<T*>(a.dy) + pix * 8) = w;
+    } else {
+      for (int c = C; c < ld; ++c) static_cast<T*>(a.dy)[pix * ld + c] = cvt<T>(0.f);
+#pragma unroll
+      for (int c = 0; c < C; ++c) static_cast<T*>(a.dy)[pix * ld + c] = cvt<T>(gv[c]);
     }
   }
   if (bwd || !a.sse) return;

@@ -143,22 +143,28 @@ def test_vq_kernel_vs_torch(rows, codes, dim):
     np.testing.assert_allclose(dE.cpu().numpy(), Ew.grad.numpy(), rtol=1e-4, atol=1e-9)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_recon_kernel(dtype):
-    """vae_recon_fwd / vae_recon_bwd: tanh, per-image SSE, d/dy of mse(tanh(y), x)."""
+@pytest.mark.parametrize("dtype,ld", [(torch.float32, 0), (torch.bfloat16, 0), (torch.float32, 8), (torch.bfloat16, 8)])
+def test_recon_kernel(dtype, ld):
+    """vae_recon_fwd / vae_recon_bwd: tanh, per-image SSE, d/dy of mse(tanh(y), x); ld 8 = the
+    packed RGB ends (3 channels in rows of 8: padding ignored on load, written as zeros in dy)."""
     from vae_amd import _lib as L
     g = torch.Generator().manual_seed(3)
     n, hw = 3, 32
-    y = torch.randn(n, hw, hw, 3, generator=g).to(dtype)
+    row = ld if ld else 3
+    y_full = torch.randn(n, hw, hw, row, generator=g).to(dtype)
+    y = y_full[..., :3]
     x = torch.rand(n, 3, hw, hw, generator=g)
-    y_d, x_d = y.cuda(), x.cuda()
+    y_d, x_d = y_full.cuda(), x.cuda()
     recon = torch.empty(n, 3, hw, hw, device="cuda")
     sse = torch.zeros(n, device="cuda")
-    dy = torch.empty(n, hw, hw, 3, dtype=dtype, device="cuda")
-    a = L.ReconArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=3, grad_scale=1.0 / x.numel())
-    a.y, a.target, a.recon, a.sse, a.dy = y_d.data_ptr(), x_d.data_ptr(), recon.data_ptr(), sse.data_ptr(), dy.data_ptr()
+    dy_full = torch.full((n, hw, hw, row), 7.0, dtype=dtype, device="cuda")
+    dy = dy_full[..., :3]
+    a = L.ReconArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=3, ld=ld, grad_scale=1.0 / x.numel())
+    a.y, a.target, a.recon, a.sse, a.dy = y_d.data_ptr(), x_d.data_ptr(), recon.data_ptr(), sse.data_ptr(), dy_full.data_ptr()
     L.call("vae_recon_fwd", a, L.stream_ptr())
     torch.cuda.synchronize()
+    if ld:
+        assert float(dy_full[..., 3:].float().abs().max()) == 0.0
     yr = y.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
     r = torch.tanh(yr)
     loss = torch.nn.functional.mse_loss(r, x)
@@ -171,8 +177,8 @@ def test_recon_kernel(dtype):
     # bwd from a caller-supplied dL/drecon
     gr = torch.randn(n, 3, hw, hw, generator=g)
     gr_d = gr.cuda()
-    b = L.ReconArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=3)
-    b.target, b.recon, b.dy, b.grad_recon = x_d.data_ptr(), recon.data_ptr(), dy.data_ptr(), gr_d.data_ptr()
+    b = L.ReconArgs(dtype=L.dtype_code(dtype), n=n, h=hw, w=hw, c=3, ld=ld)
+    b.target, b.recon, b.dy, b.grad_recon = x_d.data_ptr(), recon.data_ptr(), dy_full.data_ptr(), gr_d.data_ptr()
     L.call("vae_recon_bwd", b, L.stream_ptr())
     torch.cuda.synchronize()
     want = (gr * (1 - r.detach() ** 2)).permute(0, 2, 3, 1)
