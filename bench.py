@@ -454,7 +454,7 @@ def main():
     step_flops = sum(r[2] for r in rows)
 
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:     # the CPU baseline is an N=1 figure (rank 0)
         cpu = cpu_baseline(args.batch, args.cpu_seconds, args.arch)
 
     ms = elapsed / args.steps * 1e3
