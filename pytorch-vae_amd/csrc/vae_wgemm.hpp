@@ -589,7 +589,9 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   p.v_bytes = (uint32_t)((long)p.n * p.hv * p.wv * p.J * 2);
   // tile: square, the largest whose both sides fit the channel counts
   const int mn = p.M < p.J ? p.M : p.J;
-  const int T = mn >= 128 ? 128 : (mn >= 64 ? 64 : 32);
+  int T = mn >= 128 ? 128 : (mn >= 64 ? 64 : 32);
+  static const int t1 = tune_env("VAE_WG_T1X1", 0);            // tile override for 1x1 kernels (sweeps)
+  if (p.R == 1 && (t1 == 64 || t1 == 32) && t1 < T) T = t1;
   const bool taps_in_block = T == 32 && (p.R == 3 || (p.R == 4 && p.u_xf.kind <= VAE_X_ACT && p.v_xf.kind <= VAE_X_ACT));
   const long tiles = (long)((p.M + T - 1) / T) * ((p.J + T - 1) / T) * (taps_in_block ? 1 : p.R * p.R);
   const long ksteps = (npix + 31) / 32;
