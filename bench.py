@@ -160,6 +160,10 @@ def kernel_costs(plan, dsz):
         if isinstance(ref, tuple) or ref is None:
             out.append((fn, None, 0, 0))
             continue
+        if isinstance(ref, L.FilterBatch):          # several layers' weight gradients in one call
+            fb = [conv_cost(f, r._obj, dsz) for f, r in ref.calls]
+            out.append((fn, ref, sum(c[0] for c in fb), sum(c[1] for c in fb)))
+            continue
         a = ref._obj
         if isinstance(a, L.ConvArgs):
             f, b = conv_cost(fn, a, dsz)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 9
+#define VAE_ABI_VERSION 10
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -375,6 +375,19 @@ int vae_conv2d_workspace_size(const vae_conv_args* a, int32_t op, size_t* bytes)
 int vae_convT2d_workspace_size(const vae_conv_args* a, int32_t op, size_t* bytes);
 int vae_linear_workspace_size(const vae_linear_args* a, int32_t op, size_t* bytes);
 int vae_head_workspace_size(const vae_head_args* a, int32_t op, size_t* bytes);
+/* --- weight gradients of several layers in one call ------------------------------------
+ * The vae_conv2d_bwd_filter / vae_convT2d_bwd_filter calls of one gradient bucket of the
+ * backward (the reference's loss.backward() over models/vanilla_vae.py:25-75, experiment.py:45-86):
+ * items[i] holds the arguments that call would get, kinds[i] says which entry point.  The results
+ * equal the calls made one after another; the bf16 GEMMs of layers sharing a tile class run as one
+ * grouped launch (a layer's weight gradient is read only by the optimizer, so the layers of a
+ * bucket can run concurrently).  The items' own workspace fields are ignored: `workspace` holds
+ * every item's workspace back to back (vae_conv_bwd_filter_batch_workspace_size). */
+enum vae_layer_kind { VAE_LAYER_CONV2D = 0, VAE_LAYER_CONVT2D = 1 };
+int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
+                              void* workspace, int64_t workspace_bytes, void* stream);
+int vae_conv_bwd_filter_batch_workspace_size(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
+                                             size_t* bytes);
 /* --- start of a training step: zero `bytes` at `zero` and ++*step ------------------ */
 int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream);
 

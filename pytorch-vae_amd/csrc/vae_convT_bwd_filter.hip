@@ -10,18 +10,15 @@ extern "C" int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "convT2d_bwd_filter") || !a->dy || !a->x || !a->dw) return fail(VAE_E_BADARG, "convT2d_bwd_filter: null tensor");
   if (!xf_ok(a->dy_xf, "convT2d_bwd_filter.dy") || !xf_ok(a->x_xf, "convT2d_bwd_filter.x")) return VAE_E_BADARG;
   const bool closed = a->db && a->dy_xf.kind == VAE_X_BN_DY;
-  if (wg2_ok(a->dtype, a->x_xf, a->dy_xf, (long)a->n * a->h * a->w * a->c, (long)a->n * a->p * a->q * a->k, a->c, a->k,
-             a->x, a->dy)) {
-    // bf16 weight-gradient GEMM: U = x (input grid, m = c), V = dy (output grid, j = k)
+  {
+    // bf16 weight-gradient GEMM (vae_wgemm.hpp)
     WgParams w;
-    memset(&w, 0, sizeof(w));
-    w.u = a->x; w.u_xf = sanitize(a->x_xf); w.v = a->dy; w.v_xf = sanitize(a->dy_xf);
-    w.n = a->n; w.hu = a->h; w.wu = a->w; w.M = a->c; w.hv = a->p; w.wv = a->q; w.J = a->k;
-    w.R = a->r; w.S = a->stride; w.P = a->pad; w.dw = a->dw;
-    w.db = closed ? a->db : nullptr; w.dy_is_v = 1;
-    int rc = wg2_launch(w, a->workspace, a->workspace_bytes, (hipStream_t)stream);
-    if (rc || !a->db || closed) return rc;
-    return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
+    bool closed_wg;
+    if (conv_wg_params(a, true, &w, &closed_wg)) {
+      int rc = wg2_launch(w, a->workspace, a->workspace_bytes, (hipStream_t)stream);
+      if (rc || !a->db || closed_wg) return rc;
+      return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
+    }
   }
   if (!closed &&
       wgrad_ok(a->dtype, a->x_xf, a->dy_xf, (long)a->n * a->h * a->w * a->c, (long)a->n * a->p * a->q * a->k, a->c, a->k)) {

@@ -10,19 +10,15 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "conv2d_bwd_filter") || !a->dy || !a->x || !a->dw) return fail(VAE_E_BADARG, "conv2d_bwd_filter: null tensor");
   if (!xf_ok(a->dy_xf, "conv2d_bwd_filter.dy") || !xf_ok(a->x_xf, "conv2d_bwd_filter.x")) return VAE_E_BADARG;
   const bool closed = a->db && a->dy_xf.kind == VAE_X_BN_DY;   // Σdy from the BN sums
-  if (!a->x_nchw_f32 &&
-      wg2_ok(a->dtype, a->dy_xf, a->x_xf, (long)a->n * a->p * a->q * a->k, (long)a->n * a->h * a->w * a->c, a->k, a->c,
-             a->dy, a->x)) {
-    // bf16 weight-gradient GEMM: U = dy (output grid, m = k), V = x (input grid, j = c)
+  {
+    // bf16 weight-gradient GEMM (vae_wgemm.hpp)
     WgParams w;
-    memset(&w, 0, sizeof(w));
-    w.u = a->dy; w.u_xf = sanitize(a->dy_xf); w.v = a->x; w.v_xf = sanitize(a->x_xf);
-    w.n = a->n; w.hu = a->p; w.wu = a->q; w.M = a->k; w.hv = a->h; w.wv = a->w; w.J = a->c;
-    w.R = a->r; w.S = a->stride; w.P = a->pad; w.dw = a->dw;
-    w.db = closed ? a->db : nullptr; w.dy_is_v = 0;
-    int rc = wg2_launch(w, a->workspace, a->workspace_bytes, (hipStream_t)stream);
-    if (rc || !a->db || closed) return rc;
-    return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
+    bool closed_wg;
+    if (conv_wg_params(a, false, &w, &closed_wg)) {
+      int rc = wg2_launch(w, a->workspace, a->workspace_bytes, (hipStream_t)stream);
+      if (rc || !a->db || closed_wg) return rc;
+      return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
+    }
   }
   if (!a->x_nchw_f32 && !closed &&
       wgrad_ok(a->dtype, a->dy_xf, a->x_xf, (long)a->n * a->p * a->q * a->k, (long)a->n * a->h * a->w * a->c, a->k, a->c)) {

@@ -52,12 +52,18 @@ __device__ __forceinline__ wgm_bf16x4 wgm_tr_read(const char* generic_lds_addr) 
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((wgm_lds_bf16x4*)(uintptr_t)off);
 }
 
+// pixels per K-step: 64 for the 128 x 128 tiles (VQ-VAE's residual convs: half the barriers per
+// MFMA; two workgroups still fit a CU's LDS), 32 below
+template <int BM> constexpr int wg_kp() { return BM >= 128 ? 64 : 32; }
+// operand tiles of one workgroup (bytes of LDS): 2 buffers x (U + V) rows of KP pixels
+template <int BM, int BJ> constexpr int wgemm_lds_bytes() { return 2 * wg_kp<BM>() * (wg_rs<BM>() + wg_rs<BJ>()); }
+
+// The per-tap weight-gradient GEMM of workgroup `bid` of its problem, operand tiles at `lds`
+// (wgemm_lds_bytes) — called by wgemm_kernel (one problem per launch) and by wg_group_kernel
+// (several layers' weight gradients in one launch, vae_wgrad_batch.hip).
 template <int BM, int BJ, int XU, int XV>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM >= 128 ? 2 : 1)))
-wgemm_kernel(const WgParams p) {
-  // pixels per K-step: 64 for the 128 x 128 tiles (VQ-VAE's residual convs: half the barriers per
-  // MFMA; two workgroups still fit a CU's LDS), 32 below
-  constexpr int KP = BM >= 128 ? 64 : 32;
+__device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, char* lds) {
+  constexpr int KP = wg_kp<BM>();
   constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int CU = BM / 8, CV = BJ / 8;              // 16-byte chunks per pixel row
   constexpr int RPU = 256 / CU, RPV = 256 / CV;        // pixel rows per pass
@@ -69,8 +75,8 @@ wgemm_kernel(const WgParams p) {
   constexpr int WTM = BM / 2, WTJ = BJ / 2;            // 2 x 2 waves
   constexpr int TM = WTM / 16, TJ = WTJ / 16;
 
-  __shared__ __attribute__((aligned(16))) char Us[2][KP * RSU];
-  __shared__ __attribute__((aligned(16))) char Vs[2][KP * RSV];
+  char (*Us)[KP * RSU] = reinterpret_cast<char (*)[KP * RSU]>(lds);
+  char (*Vs)[KP * RSV] = reinterpret_cast<char (*)[KP * RSV]>(lds + 2 * KP * RSU);
   extern __shared__ float tabs[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -78,8 +84,8 @@ wgemm_kernel(const WgParams p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int gm = (p.M + BM - 1) / BM, gj = (p.J + BJ - 1) / BJ;
   const int per_slice = gm * gj * p.R * p.R;
-  const int slice = blockIdx.x / per_slice;
-  int t = blockIdx.x - slice * per_slice;
+  const int slice = bid / per_slice;
+  int t = bid - slice * per_slice;
   const int tj = t % gj; t /= gj;
   const int tmi = t % gm;
   const int tap = t / gm;
@@ -152,7 +158,7 @@ wgemm_kernel(const WgParams p) {
   float* const scr = reinterpret_cast<float*>(Vs[0]);
   if constexpr (BU) tab_fill_pre(p.u_xf, pu, u_pre, tu, false, false, scr);
   if constexpr (BV) tab_fill_pre(p.v_xf, pv, v_pre, tv, false, false, scr);
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     // the BatchNorm whose backward this call applies: dL/dgamma, dL/dbeta (+ conv bias) once
     const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
     if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
@@ -265,6 +271,13 @@ wgemm_kernel(const WgParams p) {
     }
 }
 
+template <int BM, int BJ, int XU, int XV>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM >= 128 ? 2 : 1)))
+wgemm_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[wgemm_lds_bytes<BM, BJ>()];
+  wgemm_body<BM, BJ, XU, XV>(p, (int)blockIdx.x, lds);
+}
+
 // All R x R taps in one workgroup (small tiles): the U tile of a K-step is loaded and
 // transformed once and reused by every tap (per-tap workgroups did it R*R times), V is gathered
 // per tap from the pixel decomposition computed once per row.  Accumulators: R*R x the
@@ -275,14 +288,22 @@ template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : wg_sta
 // 32-channel tiles (128 of the 256 threads idled at 32) — and the LDS holds one step (single
 // buffer, two barriers per step) so two workgroups still fit a CU: each memory round trip (the
 // loop is latency-bound, one step in flight per ring slot) now carries twice the MFMA work.
+template <int BM, int BJ> constexpr int wgt_kp() {
+  constexpr int RPU = 256 / (BM / 8), RPV = 256 / (BJ / 8);
+  return RPU < RPV ? (RPU < 32 ? 32 : (RPU > 64 ? 64 : RPU)) : (RPV < 32 ? 32 : (RPV > 64 ? 64 : RPV));
+}
+template <int BM, int BJ> constexpr int wgt_nb() { return wgt_kp<BM, BJ>() > 32 ? 1 : 2; }   // LDS buffers
+template <int BM, int BJ, int RR> constexpr int wgemm_taps_lds_bytes() {
+  return wgt_nb<BM, BJ>() * wgt_kp<BM, BJ>() * (wg_rs<BM>() + RR * RR * wg_rs<BJ>());
+}
+
 template <int BM, int BJ, int XU, int XV, int RR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR >= 4 ? 2 : 1)))
-wgemm_taps_kernel(const WgParams p) {
+__device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid, char* lds) {
   constexpr int TAPS = RR * RR;
   constexpr int CU = BM / 8, CV = BJ / 8;
   constexpr int RPU = 256 / CU, RPV = 256 / CV;
-  constexpr int KP = RPU < RPV ? (RPU < 32 ? 32 : (RPU > 64 ? 64 : RPU)) : (RPV < 32 ? 32 : (RPV > 64 ? 64 : RPV));
-  constexpr int NB = KP > 32 ? 1 : 2;                  // LDS buffers
+  constexpr int KP = wgt_kp<BM, BJ>();
+  constexpr int NB = wgt_nb<BM, BJ>();
   constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int UPT = RPU >= KP ? 1 : KP / RPU, VPT = RPV >= KP ? 1 : KP / RPV;
   constexpr bool DU = XU == VAE_X_BN_DY, DV = XV == VAE_X_BN_DY;
@@ -292,8 +313,8 @@ wgemm_taps_kernel(const WgParams p) {
   constexpr int WTM = BM / 2, WTJ = BJ / 2;
   constexpr int TM = WTM / 16, TJ = WTJ / 16;
 
-  __shared__ __attribute__((aligned(16))) char Us[NB][KP * RSU];
-  __shared__ __attribute__((aligned(16))) char Vs[NB][TAPS][KP * RSV];
+  char (*Us)[KP * RSU] = reinterpret_cast<char (*)[KP * RSU]>(lds);
+  char (*Vs)[TAPS][KP * RSV] = reinterpret_cast<char (*)[TAPS][KP * RSV]>(lds + NB * KP * RSU);
   extern __shared__ float tabs[];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -301,8 +322,8 @@ wgemm_taps_kernel(const WgParams p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int gm = (p.M + BM - 1) / BM, gj = (p.J + BJ - 1) / BJ;
   const int per_slice = gm * gj;
-  const int slice = blockIdx.x / per_slice;
-  const int t0 = blockIdx.x - slice * per_slice;
+  const int slice = bid / per_slice;
+  const int t0 = bid - slice * per_slice;
   const int tj = t0 % gj, tmi = t0 / gj;
   const int m0 = tmi * BM, j0 = tj * BJ;
   const long npix = (long)p.n * p.hu * p.wu;
@@ -377,7 +398,7 @@ wgemm_taps_kernel(const WgParams p) {
   float* const scr = reinterpret_cast<float*>(Vs[0][0]);
   if constexpr (BU) tab_fill_pre(p.u_xf, pu, u_pre, tu, false, false, scr);
   if constexpr (BV) tab_fill_pre(p.v_xf, pv, v_pre, tv, false, false, scr);
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
     if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
   }
@@ -497,6 +518,13 @@ wgemm_taps_kernel(const WgParams p) {
       }
 }
 
+template <int BM, int BJ, int XU, int XV, int RR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR >= 4 ? 2 : 1)))
+wgemm_taps_kernel(const WgParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[wgemm_taps_lds_bytes<BM, BJ, RR>()];
+  wgemm_taps_body<BM, BJ, XU, XV, RR>(p, (int)blockIdx.x, lds);
+}
+
 // dw[c] += sum over the K slices of slab[s][c]: blockIdx.y takes a contiguous run of slices, one
 // float4 of columns per thread, one atomic per column per run (cols % 4 == 0, 16-byte aligned).
 static __global__ void __launch_bounds__(256) wg_slab_reduce(const float* slab, long cols, int slices, int per_part,
@@ -580,7 +608,18 @@ inline void wg2_launch_u(const WgParams& p, unsigned blocks, hipStream_t st) {
 constexpr int kWgSlabMin = 384;
 constexpr long kWgSlabMaxBytes = 32l << 20;
 
-inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
+// A planned weight-gradient GEMM: tile, kernel kind, grid and K slices of one layer.
+struct WgPlan {
+  WgParams p;
+  int T;            // square tile BM = BJ
+  int taps;         // RR of the all-taps kernel (wgemm_taps_kernel), 0: one tap per workgroup
+  unsigned blocks;
+  long split;       // K slices
+  long cols;        // dW elements (M * R * R * J)
+};
+
+// Plan one layer (tile, K slices, partial slab in `ws` when it pays); launches nothing.
+inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out) {
   p.fd_wu = make_fastdiv(p.wu);
   p.fd_hu = make_fastdiv(p.hu);
   p.fd_r = make_fastdiv(p.R);
@@ -599,7 +638,7 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   // tiles would otherwise be split hundreds of ways and every slice adds its whole tile into dw
   // with fp32 atomics — measured on the VQ-VAE residual 1x1 (M = J = 256, 32768 pixels): 128
   // slices 44.4 us, 64 slices 32.7 us, 32 slices 32.5 us, 16 slices 48.7 us; the 3x3 layers and
-  // VanillaVAE's are slower with the higher floor, scripts/gpu_r2_wgsweep2.sh)
+  // VanillaVAE's are slower with the higher floor)
   static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
   static const int mink_env = tune_env("VAE_WG_MINK", 0);
   const int mink = mink_env > 0 ? mink_env : (p.R == 1 ? 16 : 4);
@@ -613,7 +652,6 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
   if (split < 1) split = 1;
   p.kper = (int)(((ksteps + split - 1) / split) * 32);
   split = (npix + p.kper - 1) / p.kper;
-  const unsigned blocks = (unsigned)(tiles * split);
   const long cols = (long)p.M * p.R * p.R * p.J;
   const int slab_min = tune_env("VAE_WG_SLAB_MIN", kWgSlabMin);      // read per call (tests lower it)
   p.slab = nullptr;
@@ -623,16 +661,63 @@ inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
     if (!ws_fits(split * cols * 4, ws_bytes, "wgemm K-slice partials")) return VAE_E_BADARG;
     p.slab = static_cast<float*>(ws);
   }
-  if (T == 128) wg2_launch_u<128, 128>(p, blocks, st);
-  else if (T == 64) wg2_launch_u<64, 64>(p, blocks, st);
-  else wg2_launch_u<32, 32>(p, blocks, st);
-  int rc = check_launch("wgemm");
-  if (rc || !p.slab) return rc;
+  out->p = p;
+  out->T = T;
+  out->taps = taps_in_block ? p.R : 0;
+  out->blocks = (unsigned)(tiles * split);
+  out->split = split;
+  out->cols = cols;
+  return VAE_OK;
+}
+
+inline void wg2_launch_main(const WgPlan& w, hipStream_t st) {
+  if (w.T == 128) wg2_launch_u<128, 128>(w.p, w.blocks, st);
+  else if (w.T == 64) wg2_launch_u<64, 64>(w.p, w.blocks, st);
+  else wg2_launch_u<32, 32>(w.p, w.blocks, st);
+}
+
+// dw += the K slices' partials (a layer whose plan took a slab)
+inline int wg2_reduce(const WgPlan& w, hipStream_t st) {
+  if (!w.p.slab) return VAE_OK;
+  const long split = w.split, cols = w.cols;
   const int parts = split < 32 ? (int)split : 32;
   const int per = (int)((split + parts - 1) / parts);
   const dim3 grid((unsigned)((cols / 4 + 255) / 256), (unsigned)((split + per - 1) / per));
-  VAE_LAUNCH(wg_slab_reduce, grid, dim3(256), 0, st, (const float*)p.slab, cols, (int)split, per, p.dw);
+  VAE_LAUNCH(wg_slab_reduce, grid, dim3(256), 0, st, (const float*)w.p.slab, cols, (int)split, per, w.p.dw);
   return check_launch("wg_slab_reduce");
+}
+
+inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
+  WgPlan w;
+  if (int rc = wg2_plan(p, ws, ws_bytes, &w)) return rc;
+  wg2_launch_main(w, st);
+  if (int rc = check_launch("wgemm")) return rc;
+  return wg2_reduce(w, st);
+}
+
+// The bf16 weight-gradient GEMM parameters of a Conv2d / ConvTranspose2d bwd_filter call, when
+// the call takes that path (bf16 NHWC operands, channels % 8, 16-byte aligned tensors):
+//   Conv2d:          U = dy (output grid, m = k), V = x  (input grid, j = c)
+//   ConvTranspose2d: U = x  (input grid,  m = c), V = dy (output grid, j = k)
+// The bias gradient goes through the GEMM only in closed form (dy_xf BN_DY); *closed says so.
+inline bool conv_wg_params(const vae_conv_args* a, bool transposed, WgParams* w, bool* closed) {
+  *closed = a->db && a->dy_xf.kind == VAE_X_BN_DY;
+  const long xe = (long)a->n * a->h * a->w * a->c, ye = (long)a->n * a->p * a->q * a->k;
+  if (a->x_nchw_f32) return false;
+  if (!transposed ? !wg2_ok(a->dtype, a->dy_xf, a->x_xf, ye, xe, a->k, a->c, a->dy, a->x)
+                  : !wg2_ok(a->dtype, a->x_xf, a->dy_xf, xe, ye, a->c, a->k, a->x, a->dy)) return false;
+  memset(w, 0, sizeof(*w));
+  if (!transposed) {
+    w->u = a->dy; w->u_xf = sanitize(a->dy_xf); w->v = a->x; w->v_xf = sanitize(a->x_xf);
+    w->n = a->n; w->hu = a->p; w->wu = a->q; w->M = a->k; w->hv = a->h; w->wv = a->w; w->J = a->c;
+  } else {
+    w->u = a->x; w->u_xf = sanitize(a->x_xf); w->v = a->dy; w->v_xf = sanitize(a->dy_xf);
+    w->n = a->n; w->hu = a->h; w->wu = a->w; w->M = a->c; w->hv = a->p; w->wv = a->q; w->J = a->k;
+  }
+  w->R = a->r; w->S = a->stride; w->P = a->pad; w->dw = a->dw;
+  w->db = *closed ? a->db : nullptr;
+  w->dy_is_v = transposed ? 1 : 0;
+  return true;
 }
 
 }  // namespace vae

@@ -1,0 +1,197 @@
+// C-ABI entry point: the weight gradients of several Conv2d / ConvTranspose2d layers in one call
+// (the bwd_filter calls of one gradient bucket of the backward, models/vanilla_vae.py:25-75 via
+// experiment.py:45-86's loss.backward()).
+//
+// Why: a layer's weight gradient is off the backward's critical path (only the optimizer reads
+// it), and each one alone is a latency-bound launch of 15-30 us at B=64 (profiles/r2_v3_*).
+// Launched one per layer they serialise behind the data-gradient chain; here the layers that
+// share a tile class run as ONE grouped launch (wg_group_kernel): workgroup b finds its layer by
+// the prefix of block counts and runs that layer's body (vae_wgemm.hpp wgemm_body /
+// wgemm_taps_body) — every layer's planning (tile, K slices, slab) is exactly that of its own
+// call, so the results are those of the calls made one after another.
+#include "vae_launch.hpp"
+#include "vae_wgrad.hpp"
+#include "vae_wgemm.hpp"
+
+using namespace vae;
+
+namespace {
+
+constexpr int kWgGroupMax = 6;
+
+struct WgGroup {
+  int n;
+  int start[kWgGroupMax + 1];      // first workgroup of each layer; start[n] = total
+  int var[kWgGroupMax];            // body variant: 2 * dy_is_v + (x operand BatchNorm+LeakyReLU)
+  WgParams p[kWgGroupMax];
+};
+static_assert(sizeof(WgGroup) <= 3584, "kernel argument block");
+
+template <int T, int RR, int XU, int XV>
+__device__ __forceinline__ void wg_group_body(const WgParams& p, int bid, char* lds) {
+  if constexpr (RR > 0) wgemm_taps_body<T, T, XU, XV, RR>(p, bid, lds);
+  else wgemm_body<T, T, XU, XV>(p, bid, lds);
+}
+
+template <int T, int RR> constexpr int wg_group_lds() {
+  if constexpr (RR > 0) return wgemm_taps_lds_bytes<T, T, RR>();
+  else return wgemm_lds_bytes<T, T>();
+}
+
+// The dy operand carries the BatchNorm backward (BN_DY), the other one is the layer input with
+// no transform or its BatchNorm+LeakyReLU (the VanillaVAE family and the Autoencoder).
+template <int T, int RR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T >= 128 ? 2 : 1)))
+wg_group_kernel(const WgGroup g) {
+  __shared__ __attribute__((aligned(16))) char lds[wg_group_lds<T, RR>()];
+  // The group is read in place from the kernel-argument segment (scalar loads at a uniform
+  // dynamic offset): indexing the by-value parameter with a runtime layer index makes the
+  // compiler copy all of it to scratch first (2.5 KB per workgroup, measured 10x slower).
+  (void)g;
+  const WgGroup* gk = (const WgGroup*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = (int)blockIdx.x;
+  const int n = gk->n;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < kWgGroupMax; ++j) i = (j < n && b >= gk->start[j]) ? j : i;
+  i = __builtin_amdgcn_readfirstlane(i);
+  const int bid = b - gk->start[i];
+  const WgParams& p = gk->p[i];
+  switch (gk->var[i]) {
+    case 0: wg_group_body<T, RR, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
+    case 1: wg_group_body<T, RR, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds); break;
+    case 2: wg_group_body<T, RR, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds); break;
+    default: wg_group_body<T, RR, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds); break;
+  }
+}
+
+// group classes: 0 = 32 x 32 tiles with all 3x3 taps per workgroup, 1 = 64 x 64, 2 = 128 x 128
+constexpr int kClasses = 3;
+inline int wg_class(const WgPlan& w) {
+  if (w.T == 32) return w.taps == 3 ? 0 : -1;
+  return w.taps ? -1 : (w.T == 64 ? 1 : 2);
+}
+
+inline int wg_variant(const WgParams& p) {
+  const vae_xform& dy = p.dy_is_v ? p.v_xf : p.u_xf;
+  const vae_xform& x = p.dy_is_v ? p.u_xf : p.v_xf;
+  if (dy.kind != VAE_X_BN_DY) return -1;
+  if (x.kind != VAE_X_NONE && x.kind != VAE_X_BN_ACT) return -1;
+  return 2 * p.dy_is_v + (x.kind == VAE_X_BN_ACT ? 1 : 0);
+}
+
+inline int group_launch(int cls, const WgGroup& g, size_t lds, hipStream_t st) {
+  const dim3 grid((unsigned)g.start[g.n]);
+  switch (cls) {
+    case 0: VAE_LAUNCH((wg_group_kernel<32, 3>), grid, dim3(256), lds, st, g); break;
+    case 1: VAE_LAUNCH((wg_group_kernel<64, 0>), grid, dim3(256), lds, st, g); break;
+    default: VAE_LAUNCH((wg_group_kernel<128, 0>), grid, dim3(256), lds, st, g); break;
+  }
+  return check_launch("wg_group");
+}
+
+// workspace a single call of item i needs (the thread's query state is saved around it)
+inline long item_need(int kind, const vae_conv_args* a) {
+  WsQuery& q = ws_query();
+  const WsQuery saved = q;
+  size_t b = 0;
+  const int rc = kind == VAE_LAYER_CONVT2D ? vae_convT2d_workspace_size(a, VAE_OP_BWD_FILTER, &b)
+                                           : vae_conv2d_workspace_size(a, VAE_OP_BWD_FILTER, &b);
+  q = saved;
+  return rc ? -1 : (long)((b + 255) / 256 * 256);
+}
+
+}  // namespace
+
+extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
+                                         void* workspace, int64_t workspace_bytes, void* stream) {
+  if (n < 0 || (n > 0 && (!kinds || !items))) return fail(VAE_E_BADARG, "conv_bwd_filter_batch: null arrays");
+  hipStream_t st = (hipStream_t)stream;
+  // every item's own workspace, back to back (the grouped layers run concurrently)
+  long total = 0;
+  long off[64];
+  if (n > 64) return fail(VAE_E_BADARG, "conv_bwd_filter_batch: %d items > 64", n);
+  for (int i = 0; i < n; ++i) {
+    const vae_conv_args* a = items[i];
+    if (!a || (kinds[i] != VAE_LAYER_CONV2D && kinds[i] != VAE_LAYER_CONVT2D))
+      return fail(VAE_E_BADARG, "conv_bwd_filter_batch: item %d", i);
+    const long need = item_need(kinds[i], a);
+    if (need < 0) return VAE_E_BADARG;                        // (the item's own error message)
+    off[i] = total;
+    total += need;
+  }
+  if (!ws_fits(total, workspace ? workspace_bytes : 0, "conv_bwd_filter_batch")) return VAE_E_BADARG;
+  auto region = [&](int i) -> void* {
+    const long need = (i + 1 < n ? off[i + 1] : total) - off[i];
+    return need > 0 ? static_cast<char*>(workspace) + off[i] : nullptr;
+  };
+  auto region_bytes = [&](int i) -> long { return (i + 1 < n ? off[i + 1] : total) - off[i]; };
+
+  WgPlan plans[64];
+  int cls[64];
+  for (int i = 0; i < n; ++i) {
+    const vae_conv_args* a = items[i];
+    const bool tr = kinds[i] == VAE_LAYER_CONVT2D;
+    cls[i] = -1;
+    WgParams w;
+    bool closed = false;
+    const bool valid = geom_ok(a, "conv_bwd_filter_batch") && a->dy && a->x && a->dw &&
+                       xf_ok(a->dy_xf, "conv_bwd_filter_batch.dy") && xf_ok(a->x_xf, "conv_bwd_filter_batch.x");
+    if (valid && conv_wg_params(a, tr, &w, &closed) && (!a->db || closed) && wg_variant(w) >= 0) {
+      if (int rc = wg2_plan(w, querying() ? workspace : region(i), region_bytes(i), &plans[i])) return rc;
+      cls[i] = wg_class(plans[i]);
+    }
+    if (cls[i] < 0) {
+      // not groupable: the call on its own (validation and error messages included)
+      vae_conv_args c = *a;
+      c.workspace = querying() ? workspace : region(i);
+      c.workspace_bytes = region_bytes(i);
+      const int rc = tr ? vae_convT2d_bwd_filter(&c, stream) : vae_conv2d_bwd_filter(&c, stream);
+      if (rc) return rc;
+    }
+  }
+  // one launch per tile class (chunks of kWgGroupMax layers)
+  for (int c = 0; c < kClasses; ++c) {
+    WgGroup g;
+    memset(&g, 0, sizeof(g));
+    size_t lds = 0;
+    for (int i = 0; i <= n; ++i) {
+      const bool take = i < n && cls[i] == c;
+      if (take) {
+        const WgPlan& w = plans[i];
+        g.p[g.n] = w.p;
+        g.var[g.n] = wg_variant(w.p);
+        g.start[g.n + 1] = g.start[g.n] + (int)w.blocks;
+        g.n++;
+        const bool bu = w.p.u_xf.kind == VAE_X_BN_ACT || w.p.u_xf.kind == VAE_X_BN_DY;
+        const bool bv = w.p.v_xf.kind == VAE_X_BN_ACT || w.p.v_xf.kind == VAE_X_BN_DY;
+        const size_t l = (size_t)((bu ? 3 * tab_stride(w.p.u_xf.channels) : 0) +
+                                  (bv ? 3 * tab_stride(w.p.v_xf.channels) : 0)) * 4;
+        lds = l > lds ? l : lds;
+      }
+      if (g.n > 0 && (g.n == kWgGroupMax || i == n)) {
+        if (int rc = group_launch(c, g, lds, st)) return rc;
+        memset(&g, 0, sizeof(g));
+        lds = 0;
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    if (cls[i] >= 0)
+      if (int rc = wg2_reduce(plans[i], st)) return rc;
+  return VAE_OK;
+}
+
+extern "C" int vae_conv_bwd_filter_batch_workspace_size(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
+                                                        size_t* bytes) {
+  if (!bytes) return fail(VAE_E_BADARG, "conv_bwd_filter_batch_workspace_size: null bytes");
+  WsQuery& q = ws_query();
+  q.on = 1;
+  q.need = 0;
+  const int rc = vae_conv_bwd_filter_batch(n, kinds, items, reinterpret_cast<void*>(uintptr_t(1) << 40),
+                                           int64_t(1) << 50, nullptr);
+  *bytes = rc ? 0 : (size_t)q.need;
+  q.on = 0;
+  q.need = 0;
+  return rc;
+}

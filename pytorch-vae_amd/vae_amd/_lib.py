@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -142,6 +142,8 @@ _SIGS = {
     "vae_convT2d_workspace_size": [POINTER(ConvArgs), c_int32, POINTER(ctypes.c_size_t)],
     "vae_linear_workspace_size": [POINTER(LinearArgs), c_int32, POINTER(ctypes.c_size_t)],
     "vae_head_workspace_size": [POINTER(HeadArgs), c_int32, POINTER(ctypes.c_size_t)],
+    "vae_conv_bwd_filter_batch": [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
+    "vae_conv_bwd_filter_batch_workspace_size": [c_int32, c_void_p, c_void_p, POINTER(ctypes.c_size_t)],
 }
 EXPORTED = tuple(_SIGS)
 
@@ -176,6 +178,7 @@ def call(name: str, *args):
 
 
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER, OP_BWD = 0, 1, 2, 3          # vaehip.h enum vae_op
+LAYER_CONV2D, LAYER_CONVT2D = 0, 1                               # vaehip.h enum vae_layer_kind
 
 # entry point -> (its workspace query, op)
 WS_QUERY = {
@@ -221,3 +224,31 @@ def dtype_code(dt: torch.dtype) -> int:
     if dt == torch.bfloat16:
         return BF16
     raise VaeHipError(f"unsupported dtype {dt}")
+
+
+class FilterBatch:
+    """Argument block of one vae_conv_bwd_filter_batch call: the weight-gradient calls
+    (vae_conv2d_bwd_filter / vae_convT2d_bwd_filter, each with its ConvArgs) of one backward
+    segment, run as grouped launches (vaehip.h).  Keeps the item structs alive."""
+
+    FNS = {"vae_conv2d_bwd_filter": LAYER_CONV2D, "vae_convT2d_bwd_filter": LAYER_CONVT2D}
+
+    def __init__(self, calls):
+        self.calls = list(calls)                   # [(fn, byref(ConvArgs))]
+        n = len(self.calls)
+        self.kinds = (c_int32 * n)(*[self.FNS[fn] for fn, _ in self.calls])
+        self.items = (c_void_p * n)(*[ctypes.addressof(ref._obj) for _, ref in self.calls])
+        self.workspace, self.workspace_bytes = None, 0
+
+    @property
+    def args(self):
+        return [ref._obj for _, ref in self.calls]
+
+    def workspace_size(self) -> int:
+        out = ctypes.c_size_t(0)
+        call("vae_conv_bwd_filter_batch_workspace_size", len(self.calls), self.kinds, self.items, ctypes.byref(out))
+        return int(out.value)
+
+    def __call__(self, stream):
+        call("vae_conv_bwd_filter_batch", len(self.calls), self.kinds, self.items, self.workspace,
+             self.workspace_bytes, stream)

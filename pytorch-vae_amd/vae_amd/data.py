@@ -170,6 +170,22 @@ class VAEDataset:
         else:
             self.test_set = self.val_set
 
+    def _eval_batches(self, s: ImageSet, bs: int) -> Iterable:
+        """val / test loaders: every image is evaluated.  One rank: in order, the last batch
+        partial.  Several ranks: DistributedSampler(shuffle=False) semantics — the index list
+        padded by wrap-around to a multiple of world, rank r taking r, r+world, ... — so every rank
+        runs the same number of batches (their collectives stay matched) and none is dropped."""
+        n = len(s)
+        if self.world <= 1:
+            yield from self._batches(s, range(n), bs)
+            return
+        per = -(-n // self.world)
+        order = list(range(n))
+        order += order[:per * self.world - n] if n else []
+        mine = order[self.rank::self.world]
+        for i in range(0, len(mine), bs):
+            yield s.batch(mine[i:i + bs])
+
     def _batches(self, s: ImageSet, order: Sequence[int], bs: int) -> Iterable:
         gbs = bs * self.world
         n = len(order)
@@ -190,10 +206,10 @@ class VAEDataset:
         return self._batches(s, order, self.train_batch_size)
 
     def val_dataloader(self) -> Iterable:
-        return self._batches(self.val_set, range(len(self.val_set)), self.val_batch_size)
+        return self._eval_batches(self.val_set, self.val_batch_size)
 
     def test_dataloader(self) -> Iterable:
-        return self._batches(self.test_set, range(len(self.test_set)), self.test_batch_size)
+        return self._eval_batches(self.test_set, self.test_batch_size)
 
     def record_img_losses(self, img_names, losses):
         """dataset.py:130-136."""

@@ -58,7 +58,9 @@ def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4
     for i, (fn, ref) in enumerate(calls):
         if ref is None:
             continue
-        if isinstance(ref, tuple):              # scalar-argument entry points
+        if hasattr(ref, "args"):                # a batch of weight-gradient calls (net.FilterBatch)
+            ptrs = [p for a in ref.args for p in _written_grad_ptrs(a)]
+        elif isinstance(ref, tuple):            # scalar-argument entry points
             ptrs = [ref[4]] if fn == "vae_unpad_accumulate" else []
         else:
             ptrs = _written_grad_ptrs(ref._obj if hasattr(ref, "_obj") else ref)

@@ -23,10 +23,13 @@ class FusedAdam:
     """torch.optim.Adam semantics (lerp first moment, bias-corrected) over the flat buffer;
     also refreshes the bf16 weight copy in the same pass.  step and lr are device scalars."""
 
-    def __init__(self, net: VAENet, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0):
+    def __init__(self, net: VAENet, lr: float, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 m: Optional[torch.Tensor] = None, v: Optional[torch.Tensor] = None):
         self.net = net
-        self.m = torch.zeros_like(net.params)
-        self.v = torch.zeros_like(net.params)
+        # m / v may be given: a torch.optim.Adam's exp_avg / exp_avg_sq of the same flat
+        # parameter, so that optimizer's state (checkpoints) IS this one (experiment.GraphedSteps)
+        self.m = m if m is not None else torch.zeros_like(net.params)
+        self.v = v if v is not None else torch.zeros_like(net.params)
         self.step = torch.zeros(1, dtype=torch.int32, device=net.device)
         self.lr = torch.full((1,), float(lr), dtype=torch.float32, device=net.device)
         self.betas, self.eps, self.weight_decay = betas, eps, weight_decay
@@ -62,7 +65,12 @@ class TrainStep:
         self.use_graph = graph
         self.segments = []                      # (call range) of the backward per bucket
         if self.world > 1:
-            self.buckets = plan_buckets(plan.bwd_calls, plan.grads, net.layout, nbuckets)
+            raw = getattr(plan, "bwd_calls_raw", plan.bwd_calls)
+            self.buckets = plan_buckets(raw, plan.grads, net.layout, nbuckets)
+            if hasattr(plan, "batch_wgrads"):
+                # the weight gradients of each bucket's segment as one batch at its end
+                ends = plan.batch_wgrads([b[0] for b in self.buckets])
+                self.buckets = [(e, s, t) for e, (_, s, t) in zip(ends, self.buckets)]
             # the last bucket also carries the loss terms (plan.metrics sits right after the
             # gradients): their rank mean is the reference's log_dict(sync_dist=True) at no extra
             # collective (experiment.py:55)

@@ -52,13 +52,17 @@ class VAEXperiment:
 
     def log_dict(self, d: Dict[str, Tensor]):
         """Lightning's log_dict(..., sync_dist=True) without the per-term host sync: values stay
-        device tensors (detached); averaged over ranks when torch.distributed is initialised."""
-        for k, v in d.items():
-            v = v.detach() if torch.is_tensor(v) else torch.tensor(float(v))
-            if torch.distributed.is_available() and torch.distributed.is_initialized():
-                v = v.clone().float()
-                torch.distributed.all_reduce(v)
-                v /= torch.distributed.get_world_size()
+        device tensors (detached); averaged over ranks when torch.distributed is initialised — all
+        terms of the dict in ONE all-reduce (a stacked vector), not one collective per term."""
+        keys = list(d)
+        vals = [d[k].detach() if torch.is_tensor(d[k]) else torch.tensor(float(d[k])) for k in keys]
+        if keys and torch.distributed.is_available() and torch.distributed.is_initialized():
+            dev = vals[0].device
+            vec = torch.stack([v.to(dev).float().reshape(()) for v in vals])
+            torch.distributed.all_reduce(vec)
+            vec /= torch.distributed.get_world_size()
+            vals = list(vec.unbind(0))
+        for k, v in zip(keys, vals):
             self.logged[k] = v
 
     @staticmethod
@@ -197,17 +201,49 @@ class VAEXperiment:
 class GraphedSteps:
     """The graph path of VAEXperiment.training_step + loss.backward() + optimizer.step(): one
     engine.TrainStep per batch size (HIP graphs of forward, vae_elbo_fwd, backward, Adam on the
-    model's own parameters, model.fused_train_step), with the experiment's logging — the loss
-    terms as device tensors in experiment.logged, per-image MSE to the data module and the
-    extreme-image tracking — and the torch optimizer's learning rate (so its schedulers keep
-    their semantics) copied into the fused Adam before every step."""
+    model's own parameters, model.fused_train_step), with the experiment's logging.
+
+    One optimizer state, as the reference's single torch.optim.Adam: every batch size's step
+    shares ONE FusedAdam, whose first / second moments are the torch optimizer's own exp_avg /
+    exp_avg_sq tensors of the model's flat parameter (its `step` is kept in the torch state too),
+    so a checkpoint's optimizer_states and a resumed run see the state the fused steps built.
+    The torch optimizer's learning rate (its schedulers keep their semantics) is copied in before
+    every step.
+
+    No host synchronisation per step: the loss terms stay device tensors in experiment.logged;
+    per-image MSE and the extreme-image candidates are kept on the device and handed to the data
+    module / experiment.extreme_images by flush() (fit() calls it once per epoch)."""
 
     def __init__(self, experiment: VAEXperiment, optimizer):
         self.exp, self.opt = experiment, optimizer
         self.steps: Dict[int, Any] = {}
         p = experiment.params
-        self.kw = dict(kld_weight=p['kld_weight'], lr=optimizer.param_groups[0]['lr'],
-                       weight_decay=p.get('weight_decay', 0.0), betas=optimizer.param_groups[0]['betas'])
+        g = optimizer.param_groups[0]
+        self.kw = dict(kld_weight=p['kld_weight'], lr=g['lr'], weight_decay=p.get('weight_decay', 0.0),
+                       betas=g['betas'])
+        self.fused = None
+        self.nstep = 0
+        self._per: List[Tensor] = []                 # per-image losses of the epoch (device)
+        self._names: List[Any] = []
+        self._ext = None                             # device extreme-image state
+
+    def _shared_adam(self):
+        from .engine import FusedAdam
+        model = self.exp.model
+        flat = model.flat
+        g = self.opt.param_groups[0]
+        if not any(q is flat for q in g['params']):
+            raise ValueError("engine='graph' needs the optimizer over model.parameters() (the flat parameter)")
+        st = self.opt.state[flat]
+        if 'exp_avg' not in st:
+            st['step'] = torch.tensor(0.0)
+            st['exp_avg'] = torch.zeros_like(flat, memory_format=torch.preserve_format)
+            st['exp_avg_sq'] = torch.zeros_like(flat, memory_format=torch.preserve_format)
+        fused = FusedAdam(model.net, lr=g['lr'], betas=g['betas'], eps=g['eps'], weight_decay=g['weight_decay'],
+                          m=st['exp_avg'].data, v=st['exp_avg_sq'].data)
+        self.nstep = int(float(st['step']))
+        fused.step.fill_(self.nstep)
+        return fused
 
     def __call__(self, batch, batch_idx):
         imgs, labels, names = batch
@@ -215,8 +251,10 @@ class GraphedSteps:
         B = imgs.shape[0]
         step = self.steps.get(B)
         if step is None:
-            step = self.steps[B] = model.fused_train_step(B, **self.kw)
-        step.opt.set_lr(self.opt.param_groups[0]['lr'])
+            if self.fused is None:
+                self.fused = self._shared_adam()
+            step = self.steps[B] = model.fused_train_step(B, opt=self.fused, **self.kw)
+        self.fused.set_lr(self.opt.param_groups[0]['lr'])
         exp.curr_device = imgs.device
         plan = step.plan
         eps = None
@@ -224,29 +262,81 @@ class GraphedSteps:
             eps = (torch.zeros(plan.eps.shape, device=imgs.device) if getattr(step, "zero_eps", False)
                    else torch.randn(plan.eps.shape, device=imgs.device))
         step(imgs, eps)
+        self.nstep += 1
+        self.opt.state[model.flat]['step'] = torch.tensor(float(self.nstep))
         if hasattr(model, "num_iter"):
             model.num_iter += 1                       # BetaVAE: the loss_function's counter
-        out = plan.out
+        # loss terms: the rank mean when distributed (TrainStep reduces them with the last gradient
+        # bucket, experiment.py:55 sync_dist) — no collective of their own here
+        out = plan.metrics if step.world > 1 else plan.out
         third = "VQ_Loss" if not hasattr(plan, "eps") else "KLD"
-        terms = {'loss': out[0], 'Reconstruction_Loss': out[1], third: out[2]}
+        terms = {'loss': out[0].clone(), 'Reconstruction_Loss': out[1].clone(), third: out[2].clone()}
         if getattr(step, "zero_eps", False):                  # Autoencoder: no KL, no feature loss
             terms.update(KLD=torch.zeros_like(out[2]), feature_loss=torch.zeros_like(out[2]))
-        exp.log_dict(terms)
-        per = plan.per_img.view(B, -1).mean(dim=1).cpu()
-        if exp.datamodule is not None and hasattr(exp.datamodule, "record_img_losses"):
-            exp.datamodule.record_img_losses(names, per)
+        exp.logged.update(terms)
+        per = plan.per_img.view(B, -1).mean(dim=1)
         recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:, 0]
-        exp._track_extremes(per, imgs, recon, names)
+        self._per.append(per)
+        self._names.append(names)
+        self._extremes(per, imgs, recon, len(self._names) - 1)
         return exp.logged['loss']
+
+    def _extremes(self, per: Tensor, imgs: Tensor, recon: Tensor, k: int):
+        """experiment.py:65-84 on the device: the running highest / lowest per-image loss with its
+        image, reconstruction and (step, index) — first index wins ties, as the strict comparisons."""
+        dev = per.device
+        if self._ext is None:
+            self._ext = {key: {'loss': torch.full((), init, device=dev), 'img': torch.zeros_like(imgs[:1]),
+                               'recon': torch.zeros_like(recon[:1]), 'at': torch.full((2,), -1, dtype=torch.int64, device=dev)}
+                         for key, init in (('highest', float('-inf')), ('lowest', float('inf')))}
+        for key, i in (('highest', torch.argmax(per)), ('lowest', torch.argmin(per))):
+            e = self._ext[key]
+            v = per[i]
+            better = v > e['loss'] if key == 'highest' else v < e['loss']
+            e['loss'] = torch.where(better, v, e['loss'])
+            e['img'] = torch.where(better, imgs[i].unsqueeze(0), e['img'])
+            e['recon'] = torch.where(better, recon[i].unsqueeze(0).detach(), e['recon'])
+            at = torch.stack([torch.tensor(k, device=dev), i.to(torch.int64)])
+            e['at'] = torch.where(better, at, e['at'])
+
+    def flush(self):
+        """Hand the epoch's device-side records to the host (one synchronisation): per-image
+        losses to the data module (dataset.py:130-136), extreme images to the experiment."""
+        exp = self.exp
+        if self._per:
+            per = torch.cat(self._per).cpu().tolist()
+            if exp.datamodule is not None and hasattr(exp.datamodule, "record_img_losses"):
+                o = 0
+                for names in self._names:
+                    exp.datamodule.record_img_losses(names, per[o:o + len(names)])
+                    o += len(names)
+        if self._ext is not None:
+            for key, e in self._ext.items():
+                k, i = e['at'].tolist()
+                if k < 0:
+                    continue
+                v = float(e['loss'])
+                better = v > exp.extreme_images[key]['loss'] if key == 'highest' else v < exp.extreme_images[key]['loss']
+                if better:
+                    exp.extreme_images[key] = {'loss': v, 'img': e['img'].cpu(), 'recon': e['recon'].cpu(),
+                                               'name': self._names[k][i]}
+        self._per, self._names, self._ext = [], [], None
+
+
+def _fusable(model) -> bool:
+    """Models whose whole step the fused engine computes (the centre-weighted Autoencoder loss
+    runs through loss_function instead)."""
+    return getattr(model, "center_focus_sigma", None) is None
 
 
 def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=None,
-        engine: str = "eager") -> List[Dict[str, float]]:
+        engine: str = "graph") -> List[Dict[str, float]]:
     """Minimal Trainer loop over an iterable of (imgs, labels, names) batches: the reference's
     Lightning fit() for one optimizer (zero_grad, training_step, backward, step, epoch-interval
     schedulers).  Returns the per-epoch mean of each logged term (host values, synced once per
-    epoch).  engine="graph": each training step is one GraphedSteps replay (models with
-    fused_train_step; plain Adam on model.parameters())."""
+    epoch).  engine="graph" (default): each training step is one GraphedSteps replay (models with
+    fused_train_step; plain Adam on model.parameters()); models without it (or several optimizers)
+    run the eager path.  engine="eager": training_step + loss.backward() + optimizer.step()."""
     opt_cfg = experiment.configure_optimizers()
     sched, plateau = [], None
     if isinstance(opt_cfg, dict):
@@ -258,9 +348,8 @@ def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=No
         optims = opt_cfg
     graphed = None
     if engine == "graph":
-        if not hasattr(experiment.model, "fused_train_step") or len(optims) != 1:
-            raise ValueError("engine='graph' needs a vae_amd model and a single optimizer")
-        graphed = GraphedSteps(experiment, optims[0])
+        if hasattr(experiment.model, "fused_train_step") and len(optims) == 1 and _fusable(experiment.model):
+            graphed = GraphedSteps(experiment, optims[0])
     elif engine != "eager":
         raise ValueError(f"engine {engine!r}")
     history = []
@@ -283,6 +372,8 @@ def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=No
             loss.backward()
             optims[0].step()
             acc()
+        if graphed is not None:
+            graphed.flush()
         if val_batches is not None:
             was_training = getattr(experiment.model, "training", True)
             if hasattr(experiment.model, "eval"):

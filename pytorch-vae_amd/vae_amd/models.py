@@ -150,6 +150,8 @@ class _HipELBO(torch.autograd.Function):
     def forward(ctx, flat: Tensor, recons: Tensor, mu: Tensor, log_var: Tensor, plan, loss_kw: dict):
         plan.run_elbo(L.stream_ptr(), **loss_kw)
         ctx.plan = plan
+        # the unscaled backward seeds of this loss (a repeated backward rescales from these)
+        ctx.seeds = (plan.head_coef.clone(), plan.kl_coef.clone())
         loss, rl, kld = plan.out[0].clone(), plan.out[1].clone(), plan.out[2].clone()
         ctx.mark_non_differentiable(rl, kld)
         return loss, rl, kld
@@ -162,8 +164,8 @@ class _HipELBO(torch.autograd.Function):
         if plan.backward_done:
             plan.reset_backward()
         plan.backward_done = True
-        plan.head_coef.mul_(g_loss)
-        plan.kl_coef.mul_(g_loss)
+        torch.mul(ctx.seeds[0], g_loss, out=plan.head_coef)
+        torch.mul(ctx.seeds[1], g_loss, out=plan.kl_coef)
         plan.seed_fused(True)
         try:
             plan.backward(L.stream_ptr())
@@ -194,14 +196,16 @@ class _HipVAE(BaseVAE):
         return dict(loss="iwae" if self.samples > 1 else "vanilla", samples=self.samples)
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
-                         betas=(0.9, 0.999), graph: bool = True, process_group=None):
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
         """The whole training step of this model — forward, loss_function (vae_elbo_fwd), backward,
         [gradient all-reduce], Adam — as one engine.TrainStep on the model's own parameters,
         replayed from HIP graphs: the graph path of VAEXperiment.training_step + backward +
-        optimizer.step (experiment.fit(..., engine="graph"))."""
+        optimizer.step (experiment.fit(..., engine="graph")).  `opt`: an engine.FusedAdam to share
+        (one Adam state for the steps of every batch size, as the reference's single optimizer)."""
         from .engine import FusedAdam, TrainStep
         plan = StepPlan(self.net, batch, kld_weight=kld_weight, **self._loss_config())
-        opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
+        if opt is None:
+            opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
         return TrainStep(self.net, plan, opt, graph=graph, process_group=process_group)
 
     def _gpu_loss(self, args, loss: str, **kw):
@@ -498,11 +502,11 @@ class Autoencoder(_HipVAE):
         return dict(loss="vanilla", samples=1)
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
-                         betas=(0.9, 0.999), graph: bool = True, process_group=None):
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
         if self.center_focus_sigma is not None:
             raise NotImplementedError("the fused step computes the plain MSE; the centre-weighted loss runs "
                                       "through loss_function (torch loss, HIP backward)")
-        step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group)
+        step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group, opt)
         step.plan.eps.zero_()
         step.zero_eps = True
         return step
@@ -646,12 +650,13 @@ class VQVAE(BaseVAE):
         return [recon, input, vq_loss]
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
-                         betas=(0.9, 0.999), graph: bool = True, process_group=None):
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
         """See _HipVAE.fused_train_step (the VQ-VAE loss ignores kld_weight, vq_vae.py:194-211)."""
         from .engine import FusedAdam, TrainStep
         from .vq import VQStepPlan
         plan = VQStepPlan(self.net, batch, beta=self.beta)
-        opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
+        if opt is None:
+            opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
         return TrainStep(self.net, plan, opt, graph=graph, process_group=process_group)
 
     def loss_function(self, *args, **kwargs) -> dict:

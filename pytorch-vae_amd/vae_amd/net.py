@@ -226,6 +226,9 @@ class StepPlan:
         # side stream for the weight gradients (run_calls); None: one stream
         self.side = torch.cuda.Stream(device=dev) if (concurrent and training) else None
         self._build()
+        # the backward as built, one call per op; bwd_calls batches its weight gradients
+        # (batch_wgrads: one vae_conv_bwd_filter_batch per backward segment)
+        self.bwd_calls_raw = list(self.bwd_calls)
         if fuse_bn and training:
             # each BatchNorm finalisation carried by the call that produces its statistics
             # (vaehip.h bn_finalize).  The library runs it as its own launch right after the
@@ -233,7 +236,17 @@ class StepPlan:
             # agent-scope release in every workgroup, and lower GEMM occupancy).
             self._fuse_finalize(self.fwd_calls)
             self._fuse_finalize(self.bwd_calls)
+            self.bwd_calls_raw = list(self.bwd_calls)
+        self.batch_wgrads([len(self.bwd_calls_raw)])
+
+    def batch_wgrads(self, ends):
+        """Rebuild bwd_calls from bwd_calls_raw with the conv / convT weight gradients of each
+        backward segment (calls [ends[k-1], ends[k]) of the raw list) moved into one
+        vae_conv_bwd_filter_batch call at the segment's end, and size the workspaces.  Returns the
+        segment ends as indices into the new list.  VAE_NO_WG_BATCH=1 keeps one call per layer."""
+        self.bwd_calls, new_ends = batch_filter_calls(self.bwd_calls_raw, ends)
         size_workspaces(self, [self.fwd_calls, self.bwd_calls])
+        return new_ends
 
     # ------------------------------------------------------------------ helpers
     def g(self, name: str) -> int:
@@ -648,6 +661,38 @@ class StepPlan:
         self.dw8.zero_()
 
 
+BATCH_FN = "vae_conv_bwd_filter_batch"
+DEFERRED_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_unpad_accumulate"))
+
+
+def batch_filter_calls(calls, ends):
+    """Weight gradients are read only by the optimizer, so within a backward segment they can
+    run after the segment's data-gradient chain and together: the conv / convT bwd_filter calls
+    of each segment become one vae_conv_bwd_filter_batch call (grouped launches) at its end,
+    followed by the calls that must follow them (vae_unpad_accumulate reads the padded first-layer
+    weight gradient).  Returns (new call list, new segment ends)."""
+    if os.environ.get("VAE_NO_WG_BATCH"):
+        return list(calls), list(ends)
+    out, new_ends, lo = [], [], 0
+    for end in ends:
+        deferred, wg = [], []
+        for fn, ref in calls[lo:end]:
+            if fn in DEFERRED_FNS:
+                deferred.append((fn, ref))
+                if fn != "vae_unpad_accumulate":
+                    wg.append((fn, ref))
+            else:
+                out.append((fn, ref))
+        if len(wg) > 1:
+            out.append((BATCH_FN, L.FilterBatch(wg)))
+            out.extend((fn, ref) for fn, ref in deferred if fn == "vae_unpad_accumulate")
+        else:
+            out.extend(deferred)
+        new_ends.append(len(out))
+        lo = end
+    return out, new_ends
+
+
 # Weight-gradient calls: nothing later in the backward reads their output (only the optimizer),
 # so they run on a side stream, concurrent with the data-gradient chain that is the critical path.
 def size_workspaces(plan, call_lists):
@@ -663,10 +708,14 @@ def size_workspaces(plan, call_lists):
     sized = []
     for calls in call_lists:
         for fn, ref in calls:
-            if fn not in L.WS_QUERY:
+            if fn == BATCH_FN:
+                arg = ref
+                b = ref.workspace_size()
+            elif fn not in L.WS_QUERY:
                 continue
-            arg = ref._obj
-            b = L.workspace_size(fn, arg)
+            else:
+                arg = ref._obj
+                b = L.workspace_size(fn, arg)
             chain = "side" if side_on and fn in SIDE_FNS else "main"
             need[chain] = max(need[chain], b)
             sized.append((arg, b, chain))
@@ -707,8 +756,11 @@ def run_calls(plan, calls, stream):
 
 
 def call_one(fn, arg, stream):
-    """One entry of a plan's call list (struct argument or scalar-argument tuple) on `stream`."""
-    if isinstance(arg, tuple):
+    """One entry of a plan's call list (struct argument, scalar-argument tuple or a batch of
+    weight-gradient calls) on `stream`."""
+    if fn == BATCH_FN:
+        arg(stream)
+    elif isinstance(arg, tuple):
         L.call(fn, *arg, stream)
     else:
         L.call(fn, arg, stream)

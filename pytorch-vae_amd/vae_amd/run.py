@@ -21,6 +21,7 @@ import os
 import random
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 
 LIGHTNING_VERSION = "1.5.6"          # the reference's pin (requirements.txt:1), recorded in checkpoints
@@ -42,6 +43,9 @@ def build_parser() -> argparse.ArgumentParser:
     # MI355X-path options
     p.add_argument('--dtype', choices=['f32', 'bf16'], default='f32')
     p.add_argument('--synthetic', type=int, default=0, help='train/test on N synthetic U[0,1) images')
+    p.add_argument('--engine', choices=['graph', 'eager'], default='graph',
+                   help='graph: each training step is one replay of the fused HIP-graph step '
+                        '(experiment.GraphedSteps); eager: training_step + loss.backward() + optimizer.step()')
     p.add_argument('--max_epochs', type=int, help='override trainer_params.max_epochs')
     return p
 
@@ -136,8 +140,8 @@ def main(argv=None) -> Dict[str, float]:
     config = load_config(args)
     import torch.distributed as dist
     from .dp import allreduce_mean, broadcast_buffers
-    from .data import ImageSet, VAEDataset
-    from .experiment import VAEXperiment
+    from .data import ImageSet, ImgDifficultySampler, VAEDataset
+    from .experiment import GraphedSteps, VAEXperiment, _fusable
     from .models import vae_models
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,8 +151,9 @@ def main(argv=None) -> Dict[str, float]:
     if world > 1 and not dist.is_initialized():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     seed = config['exp_params'].get('manual_seed', 1265)
-    torch.manual_seed(seed)                                       # seed_everything (run.py:66)
-    random.seed(seed)
+    torch.manual_seed(seed)                                       # seed_everything (run.py:66):
+    random.seed(seed)                                             # torch, Python and numpy
+    np.random.seed(seed)                                          # (the difficulty sampler's draws)
     mp = dict(config['model_params'])
     name = mp.pop('name')
     dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
@@ -167,6 +172,8 @@ def main(argv=None) -> Dict[str, float]:
                         train_dataset=None, test_dataset=None, device=dev, rank=rank, world=world)
         dm.train_set = ImageSet(imgs[:cut].to(dev), names[:cut])
         dm.val_set = dm.test_set = ImageSet(imgs[cut:].to(dev), names[cut:])
+        if dpar.get('use_difficulty_sampling'):
+            dm.difficulty_sampler = ImgDifficultySampler(names[:cut], dm.train_batch_size)
     else:
         # dataset.py VAEDataset(**data_params) with the -r / -t folders (run.py:71-76), resident on
         # the device; split_images uses Python's `random`, seeded above like seed_everything
@@ -190,10 +197,19 @@ def main(argv=None) -> Dict[str, float]:
             optims, scheds = opt_cfg, []
         best, step = float("inf"), 0
         epochs = config['trainer_params'].get('max_epochs', 1)
+        graphed = None
+        if args.engine == 'graph' and hasattr(model, 'fused_train_step') and len(optims) == 1 and _fusable(model):
+            # the fused step replayed from HIP graphs (DDP gradient mean and rank-0 buffers inside
+            # the TrainStep); no host synchronisation inside the epoch
+            graphed = GraphedSteps(experiment, optims[0])
         for epoch in range(epochs):
             model.train()
             sums: Dict[str, float] = {}
             for i, batch in enumerate(dm.train_dataloader()):
+                if graphed is not None:
+                    graphed(batch, i)
+                    step += 1
+                    continue
                 optims[0].zero_grad(set_to_none=True)
                 loss = experiment.training_step(batch, i)
                 loss.backward()
@@ -202,6 +218,8 @@ def main(argv=None) -> Dict[str, float]:
                     broadcast_buffers(model.net.running)
                 optims[0].step()
                 step += 1
+            if graphed is not None:
+                graphed.flush()                                 # per-image losses, extreme images
             dm.on_epoch_end()                                   # difficulty sampler update
             for k, v in experiment.logged.items():
                 sums[k] = float(v)

@@ -1,0 +1,72 @@
+# One parameterised driver for every GPU-box job of this repo (run through gpurun):
+#
+#   gpurun -- bash scripts/gpu.sh TAG STEP [STEP ...]
+#
+# Steps run in order, each under its own time limit; the first failing step ends the job (no
+# GPU step runs after a fault, abort or timeout).  Output: gpurun_out/TAG_<step>.log (+ dirs).
+#
+#   tests            pytest -m gpu (all GPU tests)
+#   tests:EXPR       pytest -m gpu -k EXPR
+#   smoke            __graft_entry__.smoke()
+#   bench            default bench line (driver's command: N=1, CPU baseline included)
+#   quick            VanillaVAE bench, 200 steps, no CPU baseline, per-call breakdown
+#   arch:A:B         bench --arch A --batch B (betaH, iwae, vq, ae_big ...), no CPU baseline
+#   prof             rocprofv3 --kernel-trace --stats over a short VanillaVAE bench
+#   prof:A:B         the same for --arch A --batch B
+#   pmc              PMC passes (SQ / MFMA / FETCH / WRITE) of the VanillaVAE step, one run each
+#   pmc:A:B          the same for --arch A --batch B
+#   kprobe           per-block phase probe (needs `make probe`)
+#   kbench[:ARGS]    per-launch microbench under a kernel trace (tools/kbench.py, ARGS comma-separated)
+set -o pipefail
+TAG=${1:?tag}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+PT="python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread"
+
+run() {   # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "[$(date +%T)] $name" >&2
+  (cd $R && timeout -k 10 $secs "$@") > $O/${TAG}_${name}.log 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >&2
+  return $rc
+}
+
+prof() {  # name bench-args...
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+     -d $O/${TAG}_${name} -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-dropin "$@") \
+     > $O/${TAG}_${name}.log 2>&1
+}
+
+pmc() {   # name bench-args...   (one counter group per run: rocprofv3 does not split passes)
+  local name=$1; shift
+  local B="python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph --no-dropin $*"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $O/${TAG}_${name}_pa -o run -- $B > $O/${TAG}_${name}_pa.log 2>&1 || return $?
+  timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 FETCH_SIZE --output-format csv -d $O/${TAG}_${name}_pb -o run -- $B > $O/${TAG}_${name}_pb.log 2>&1 || return $?
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum --output-format csv -d $O/${TAG}_${name}_pc -o run -- $B > $O/${TAG}_${name}_pc.log 2>&1 || return $?
+  cd $R && python3 tools/pmc_summary.py --dirs $O/${TAG}_${name}_pa $O/${TAG}_${name}_pb $O/${TAG}_${name}_pc \
+     --out $O/${TAG}_${name}_pmc.json --config "$*" > $O/${TAG}_${name}_pmcsum.log 2>&1
+}
+
+for step in "$@"; do
+  IFS=: read -r kind a1 a2 <<< "$step"
+  case $kind in
+    tests) if [ -n "$a1" ]; then run tests 900 $PT -k "$a1"; else run tests 900 $PT; fi ;;
+    smoke) run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 400 python3 -u bench.py ;;
+    quick) run quick 300 python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --kernel-breakdown ;;
+    arch) run arch_${a1}_${a2} 300 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --no-cpu-baseline --kernel-breakdown ;;
+    prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;
+    pmc) if [ -n "$a1" ]; then pmc pmc_$a1 --arch $a1 --batch $a2; else pmc pmc; fi ;;
+    kprobe) run kprobe 200 env VAE_HIP_LIB=probe python3 -u tools/kprobe.py --out $O/${TAG}_kp.json ;;
+    kbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+               -d $O/${TAG}_kb -o kb -- python3 $R/tools/kbench.py --out $O/${TAG}_kb_groups.json ${a1//,/ }) \
+               > $O/${TAG}_kbench.log 2>&1 ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+  rc=$?
+  [ $rc -eq 0 ] || { echo "step $step failed rc=$rc" >&2; exit $rc; }
+done

@@ -87,3 +87,25 @@ def test_data_module_batches_and_loss_recording(tmp_path):
     assert dm.sampled_img_names == [] and float(np.min(dm.difficulty_sampler.img_weights)) > 0
     vb = list(dm.val_dataloader())
     assert [b[0].shape[0] for b in vb] == [2]
+
+
+@pytest.mark.parametrize("world,n,bs", [(2, 9, 4), (3, 10, 2), (4, 3, 8), (2, 8, 4)])
+def test_eval_loaders_cover_every_image_on_every_rank_count(world, n, bs):
+    """val / test loaders with several ranks evaluate every image (DistributedSampler
+    padding: wrap-around to a multiple of world, rank r takes r, r+world, ...) and every rank
+    runs the same number of batches, so their loss all-reduces stay matched."""
+    imgs = torch.arange(n, dtype=torch.float32).view(n, 1, 1, 1).expand(n, 3, 2, 2).contiguous()
+    names = [f"{i}.png" for i in range(n)]
+    seen, counts = [], []
+    for rank in range(world):
+        dm = V.VAEDataset("", val_batch_size=bs, test_batch_size=bs, train_dataset=None, patch_size=2,
+                          rank=rank, world=world)
+        dm.val_set = dm.test_set = V.ImageSet(imgs, names)
+        batches = list(dm.val_dataloader())
+        counts.append(len(batches))
+        for x, _, nm in batches:
+            seen += nm
+            assert x.shape[0] == len(nm) <= bs
+    assert len(set(counts)) == 1
+    assert set(seen) == set(names)
+    assert len(seen) == -(-n // world) * world

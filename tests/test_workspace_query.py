@@ -95,3 +95,31 @@ def test_bad_op_is_rejected():
     a = _conv(4, 8, 8, 8)
     out = ctypes.c_size_t(0)
     assert lib.vae_conv2d_workspace_size(ctypes.byref(a), 9, ctypes.byref(out)) == -1
+
+
+def _bn(kind, c):
+    x = L.Xform(kind=kind, channels=c, count=1.0, slope=0.01, eps=1e-5)
+    for f in ("sum", "sumsq", "gamma", "beta", "dgamma", "dbeta", "aux"):
+        setattr(x, f, FAKE)
+    return x
+
+
+def test_filter_batch_workspace_is_the_sum_of_its_items():
+    """vae_conv_bwd_filter_batch runs its layers concurrently, so every item gets its own
+    workspace: the batch's need is the sum of the items' (256-byte rounded) needs."""
+    fin = _conv(64, 32, 32, 32)                  # final_layer ConvT 32 -> 32, 32x32 -> 64x64
+    fin.p = fin.q = 64
+    fin.dy = fin.dw = FAKE
+    fin.x_xf, fin.dy_xf = _bn(L.X_BN_ACT, 32), _bn(L.X_BN_DY, 32)
+    enc = _conv(64, 16, 64, 128)                 # encoder.2 conv 64 -> 128
+    enc.dy = enc.dw = FAKE
+    enc.x_xf, enc.dy_xf = _bn(L.X_BN_ACT, 64), _bn(L.X_BN_DY, 128)
+    n1 = _need("vae_convT2d_bwd_filter", fin)
+    n2 = _need("vae_conv2d_bwd_filter", enc)
+    assert n1 > 0                                # 512 K slices x 9216 dW words: slab partials
+    b = L.FilterBatch([("vae_convT2d_bwd_filter", ctypes.byref(fin)), ("vae_conv2d_bwd_filter", ctypes.byref(enc))])
+    r = lambda v: (v + 255) // 256 * 256
+    assert b.workspace_size() == r(n1) + r(n2)
+    lib = L.load()
+    rc = lib.vae_conv_bwd_filter_batch(2, b.kinds, b.items, FAKE, r(n1) + r(n2) - 4, None)
+    assert rc == -1 and b"workspace" in lib.vae_last_error()
