@@ -243,11 +243,49 @@ def center_weight_mask(h, w, sigma):
     return (wgt * (h * w / wgt.sum())).unsqueeze(0).unsqueeze(0)
 
 
-def ae_loss(recons, x, center_focus_sigma=None):
-    """models/autoencoder.py:230-262 (no VGG / MSSIM): MSE or the centre-weighted MSE."""
+def mssim_window(window_size: int, channels: int, sigma: float = 1.5):
+    """models/mssim_vae.py:205-215: the separable window as the reference builds it — note the
+    reference's exponent is +(x - w//2)^2 / (2 sigma^2) (an inverted bell), kept as is."""
+    k = torch.tensor([math.exp((i - window_size // 2) ** 2 / (2 * sigma ** 2)) for i in range(window_size)])
+    k = (k / k.sum()).unsqueeze(1)
+    w2 = k.mm(k.t()).float().unsqueeze(0).unsqueeze(0)
+    return w2.expand(channels, 1, window_size, window_size).contiguous()
+
+
+def mssim_loss(img1, img2, window_size: int = 11, normalize: bool = True):
+    """models/mssim_vae.py:217-282: 1 - MS-SSIM over 5 levels (avg-pool 2x2 between levels),
+    size_average=True, dynamic range 1, normalised (s+1)/2."""
+    C = img1.shape[1]
+    win = mssim_window(window_size, C).to(img1)
+    pad = window_size // 2
+    weights = torch.tensor([0.0448, 0.2856, 0.3001, 0.2363, 0.1333], device=img1.device)
+    ms, mc = [], []
+    for _ in range(weights.numel()):
+        mu1 = F.conv2d(img1, win, padding=pad, groups=C)
+        mu2 = F.conv2d(img2, win, padding=pad, groups=C)
+        mu1_sq, mu2_sq, mu12 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+        s1 = F.conv2d(img1 * img1, win, padding=pad, groups=C) - mu1_sq
+        s2 = F.conv2d(img2 * img2, win, padding=pad, groups=C) - mu2_sq
+        s12 = F.conv2d(img1 * img2, win, padding=pad, groups=C) - mu12
+        c1, c2 = 0.01 ** 2, 0.03 ** 2
+        v1 = 2.0 * s12 + c2
+        v2 = s1 + s2 + c2
+        mc.append(torch.mean(v1 / v2))
+        ms.append((((2 * mu12 + c1) * v1) / ((mu1_sq + mu2_sq + c1) * v2)).mean())
+        img1, img2 = F.avg_pool2d(img1, (2, 2)), F.avg_pool2d(img2, (2, 2))
+    ms, mc = torch.stack(ms), torch.stack(mc)
+    if normalize:
+        ms, mc = (ms + 1) / 2, (mc + 1) / 2
+    return 1 - torch.prod((mc ** weights)[:-1] * (ms ** weights)[-1])
+
+
+def ae_loss(recons, x, center_focus_sigma=None, use_mssim=False):
+    """models/autoencoder.py:230-262 (no VGG): MSE, the centre-weighted MSE or the MSSIM loss."""
     if center_focus_sigma is not None:
         m = center_weight_mask(x.shape[2], x.shape[3], center_focus_sigma)
         rl = ((recons - x) ** 2 * m.expand(x.shape[0], x.shape[1], -1, -1)).mean()
+    elif use_mssim:
+        rl = mssim_loss(recons, x)
     else:
         rl = F.mse_loss(recons, x)
     zero = torch.tensor(0.0)
@@ -402,7 +440,7 @@ TRAINABLE_KINDS = ("conv_w", "convT_w", "lin_w", "bias", "bn_w", "bn_b", "codebo
 def train_step(arch: str, sd, x, eps=None, *, M_N: float, lr: float = 0.005, hidden_dims=None,
                beta=4.0, gamma=1000.0, loss_type="H", max_capacity=25.0, Capacity_max_iter=1e5,
                num_iter=1, vq_beta=0.25, do_adam=True, training=True, vq_indices=None,
-               center_focus_sigma=None):
+               center_focus_sigma=None, use_mssim_loss=False):
     """forward -> loss_function -> backward -> Adam on a copy of ``sd``.
 
     Returns a dict: outputs (recon, mu, log_var / vq_loss, indices), loss terms, per-image
@@ -439,7 +477,7 @@ def train_step(arch: str, sd, x, eps=None, *, M_N: float, lr: float = 0.005, hid
         hd = list(hidden_dims or DEFAULT_HIDDEN)
         z = ae_encode(P, x, hd, training, stats)
         recon = vanilla_decode(P, z, hd, training, stats)
-        ld = ae_loss(recon, x, center_focus_sigma)
+        ld = ae_loss(recon, x, center_focus_sigma, use_mssim_loss)
         per_img = F.mse_loss(recon.detach(), x, reduction="none").mean(dim=[1, 2, 3])
         out.update(recon=recon.detach(), z=z.detach())
     elif arch == "VQVAE":

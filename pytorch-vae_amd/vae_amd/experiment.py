@@ -324,9 +324,9 @@ class GraphedSteps:
 
 
 def _fusable(model) -> bool:
-    """Models whose whole step the fused engine computes (the centre-weighted Autoencoder loss
-    runs through loss_function instead)."""
-    return getattr(model, "center_focus_sigma", None) is None
+    """Models whose whole step the fused engine computes (the centre-weighted and MSSIM
+    Autoencoder losses run through loss_function instead)."""
+    return getattr(model, "center_focus_sigma", None) is None and getattr(model, "mssim", None) is None
 
 
 def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=None,

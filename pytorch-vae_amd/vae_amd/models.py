@@ -26,6 +26,7 @@ backward; model.eval(): eval-mode BatchNorm from the running statistics, forward
 """
 from __future__ import annotations
 
+import math
 from abc import abstractmethod
 from typing import Any, Dict, List, Optional, Union
 
@@ -422,6 +423,58 @@ class IWAE(_HipVAE):
         return {'loss': loss, 'Reconstruction_Loss': log_p_x_z.mean(), 'KLD': -kld_loss.mean()}
 
 
+class MSSIM(nn.Module):
+    """models/mssim_vae.py:182-282: the differentiable MS-SSIM loss 1 - Π cs_l^w_l · ssim_L^w_L over five
+    levels (11x11 window, avg-pool 2x2 between levels, size_average, dynamic range 1, normalised
+    (s+1)/2).  The window is built as the reference builds it — its Gaussian has a POSITIVE
+    exponent, exp(+(x - 5)^2 / 4.5) (mssim_vae.py:205-209), an inverted bell the reference's
+    trained models depend on, so it is kept."""
+
+    WEIGHTS = (0.0448, 0.2856, 0.3001, 0.2363, 0.1333)
+
+    def __init__(self, in_channels: int = 3, window_size: int = 11, normalize: bool = True,
+                 size_average: bool = True) -> None:
+        super().__init__()
+        self.in_channels, self.window_size = in_channels, window_size
+        self.normalize, self.size_average = normalize, size_average
+        k = torch.tensor([math.exp((i - window_size // 2) ** 2 / (2 * 1.5 ** 2)) for i in range(window_size)])
+        k = (k / k.sum()).unsqueeze(1)
+        self._window = k.mm(k.t()).float().unsqueeze(0).unsqueeze(0).expand(
+            in_channels, 1, window_size, window_size).contiguous()
+
+    def ssim(self, img1: Tensor, img2: Tensor):
+        """mssim_vae.py:217-250: (ssim, contrast sensitivity) at one level."""
+        C, pad = self.in_channels, self.window_size // 2
+        w = self._window.to(img1)
+        mu1 = F.conv2d(img1, w, padding=pad, groups=C)
+        mu2 = F.conv2d(img2, w, padding=pad, groups=C)
+        mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+        sigma1_sq = F.conv2d(img1 * img1, w, padding=pad, groups=C) - mu1_sq
+        sigma2_sq = F.conv2d(img2 * img2, w, padding=pad, groups=C) - mu2_sq
+        sigma12 = F.conv2d(img1 * img2, w, padding=pad, groups=C) - mu1_mu2
+        C1, C2 = 0.01 ** 2, 0.03 ** 2
+        v1 = 2.0 * sigma12 + C2
+        v2 = sigma1_sq + sigma2_sq + C2
+        cs = torch.mean(v1 / v2)
+        ssim_map = ((2 * mu1_mu2 + C1) * v1) / ((mu1_sq + mu2_sq + C1) * v2)
+        ret = ssim_map.mean() if self.size_average else ssim_map.mean(1).mean(1).mean(1)
+        return ret, cs
+
+    def forward(self, img1: Tensor, img2: Tensor) -> Tensor:
+        """mssim_vae.py:252-282."""
+        weights = torch.tensor(self.WEIGHTS, device=img1.device)
+        ms, mcs = [], []
+        for _ in range(len(self.WEIGHTS)):
+            sim, cs = self.ssim(img1, img2)
+            ms.append(sim)
+            mcs.append(cs)
+            img1, img2 = F.avg_pool2d(img1, (2, 2)), F.avg_pool2d(img2, (2, 2))
+        ms, mcs = torch.stack(ms), torch.stack(mcs)
+        if self.normalize:
+            ms, mcs = (ms + 1) / 2, (mcs + 1) / 2
+        return 1 - torch.prod((mcs ** weights)[:-1] * (ms ** weights)[-1])
+
+
 class Autoencoder(_HipVAE):
     """models/autoencoder.py:9-305 (the fork's main model) on libvaehip.
 
@@ -435,9 +488,13 @@ class Autoencoder(_HipVAE):
     autograd gradient seeds the fused HIP backward.  forward returns [recons, input, zeros, zeros]
     (the VGG-feature placeholders, :224-227); the dict adds KLD = 0 and feature_loss = 0.
 
+    The MSSIM loss (use_mssim_loss, :32, :266-267) is the reference's MSSIM module restated in torch
+    (class MSSIM below) on the HIP forward's reconstruction; its autograd gradient seeds the fused
+    HIP backward, as the centre-weighted MSE's does.
+
     Not on this path (raise): the VGG feature loss (needs pretrained vgg19_bn weights, a network
-    download), the MSSIM loss, hidden_dims other than five stride-2 layers (the stride-1 extra
-    layers, :39) and BatchNorm widths above the kernels' 512-channel transform tables."""
+    download), hidden_dims other than five stride-2 layers (the stride-1 extra layers, :39) and
+    BatchNorm widths above the kernels' 512-channel transform tables."""
 
     def __init__(self, in_channels: int, latent_dim: int, hidden_dims: List = None, use_vgg: bool = False,
                  center_focus_sigma: float = None, use_skip_connections: bool = False,
@@ -445,8 +502,6 @@ class Autoencoder(_HipVAE):
         if use_vgg:
             raise NotImplementedError("Autoencoder(use_vgg=True) needs pretrained vgg19_bn weights (network "
                                       "download) — not on the MI355X path")
-        if use_mssim_loss:
-            raise NotImplementedError("Autoencoder(use_mssim_loss=True) is not on the MI355X path")
         hd = list(hidden_dims) if hidden_dims is not None else [32, 64, 128, 256, 512]
         if len(hd) != 5:
             raise NotImplementedError(f"Autoencoder with {len(hd)} layers (stride-1 extra layers, "
@@ -457,6 +512,7 @@ class Autoencoder(_HipVAE):
         super().__init__(in_channels, latent_dim, hd, **kwargs)
         self.center_focus_sigma = center_focus_sigma
         self.center_weight_mask = None
+        self.mssim = MSSIM(in_channels) if use_mssim_loss else None
         # with five stride-2 layers no decoder output matches an encoder output's spatial size
         # (autoencoder.py:205-210 compares shapes), so the skip connections never fire
         self.use_skip_connections = use_skip_connections
@@ -503,9 +559,9 @@ class Autoencoder(_HipVAE):
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
                          betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
-        if self.center_focus_sigma is not None:
-            raise NotImplementedError("the fused step computes the plain MSE; the centre-weighted loss runs "
-                                      "through loss_function (torch loss, HIP backward)")
+        if self.center_focus_sigma is not None or self.mssim is not None:
+            raise NotImplementedError("the fused step computes the plain MSE; the centre-weighted and MSSIM "
+                                      "losses run through loss_function (torch loss, HIP backward)")
         step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group, opt)
         step.plan.eps.zero_()
         step.zero_eps = True
@@ -532,14 +588,16 @@ class Autoencoder(_HipVAE):
         recons, input = args[0], args[1]
         zero = torch.tensor(0.0, device=recons.device)
         last = self._last
-        if (self.center_focus_sigma is None and last is not None and self.training and torch.is_grad_enabled()
-                and recons is last[2] and input is last[1]):
+        if (self.center_focus_sigma is None and self.mssim is None and last is not None and self.training
+                and torch.is_grad_enabled() and recons is last[2] and input is last[1]):
             g = _HipELBO.apply(self.flat, last[2], last[3], last[4], last[0], dict(loss="vanilla", kld_weight=0.0))
             return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': zero, 'feature_loss': zero}
         if self.center_focus_sigma is not None:
             if self.center_weight_mask is None:
                 self.center_weight_mask = self.create_center_weight_mask(input.shape[2], input.shape[3], input.device)
             recons_loss = self.weighted_mse_loss(recons, input, self.center_weight_mask)
+        elif self.mssim is not None:
+            recons_loss = self.mssim(recons, input)               # autoencoder.py:266-267
         else:
             recons_loss = F.mse_loss(recons, input)
         return {'loss': recons_loss, 'Reconstruction_Loss': recons_loss, 'KLD': zero, 'feature_loss': zero}

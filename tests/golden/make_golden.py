@@ -19,6 +19,7 @@ these fixtures do.
 """
 from __future__ import annotations
 
+import copy
 import json
 import os
 import sys
@@ -43,6 +44,9 @@ CASES = {
     "iwae_b4": ("IWAE", 4, dict(in_channels=3, latent_dim=128, num_samples=5), 2.5e-4, 0.007, {"S": 5}),
     "ae_b16": ("Autoencoder", 16, dict(in_channels=3, latent_dim=128), 0.0, 0.005, {}),
     "ae_center_b8": ("Autoencoder", 8, dict(in_channels=3, latent_dim=128, center_focus_sigma=11), 0.0, 0.0005, {}),
+    "ae_mssim_b8": ("Autoencoder", 8, dict(in_channels=3, latent_dim=128, use_mssim_loss=True), 0.0, 0.005, {}),
+    "ae_big_b4": ("Autoencoder", 4, dict(in_channels=3, latent_dim=128, hidden_dims=[128, 256, 512, 1024, 2048]),
+                  0.0, 0.005, {}),
     "vq_b4": ("VQVAE", 4, dict(in_channels=3, embedding_dim=64, num_embeddings=512, img_size=64, beta=0.25),
               0.0, 0.005, {}),
 }
@@ -74,9 +78,10 @@ def summary(t):
 def run_case(models, name):
     arch, B, kw, M_N, lr, extra = CASES[name]
     torch.manual_seed(0)
-    model = models.vae_models[arch](**kw)
+    model = models.vae_models[arch](**copy.deepcopy(kw))     # (the reference reverses hidden_dims in place)
     spec = (O.vq_param_spec(embedding_dim=kw["embedding_dim"], num_embeddings=kw["num_embeddings"])
-            if arch == "VQVAE" else O.ae_param_spec(latent_dim=kw["latent_dim"]) if arch == "Autoencoder"
+            if arch == "VQVAE" else O.ae_param_spec(latent_dim=kw["latent_dim"], hidden_dims=kw.get("hidden_dims"))
+            if arch == "Autoencoder"
             else O.vanilla_param_spec(latent_dim=kw["latent_dim"]))
     sd = O.make_params(spec, SEED)
     model.load_state_dict(sd, strict=True)

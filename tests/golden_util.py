@@ -5,7 +5,8 @@ import os
 import numpy as np
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["vanilla_b16", "vanilla_b8_kl", "betaH_b16", "betaB_b8", "iwae_b4", "vq_b4", "ae_b16", "ae_center_b8"]
+CASES = ["vanilla_b16", "vanilla_b8_kl", "betaH_b16", "betaB_b8", "iwae_b4", "vq_b4", "ae_b16", "ae_center_b8",
+         "ae_mssim_b8", "ae_big_b4"]
 
 
 def load_case(name):
@@ -33,7 +34,7 @@ def case_inputs(meta):
     if meta["arch"] == "VQVAE":
         spec = O.vq_param_spec(embedding_dim=kw["embedding_dim"], num_embeddings=kw["num_embeddings"])
     elif meta["arch"] == "Autoencoder":
-        spec = O.ae_param_spec(latent_dim=kw["latent_dim"])
+        spec = O.ae_param_spec(latent_dim=kw["latent_dim"], hidden_dims=kw.get("hidden_dims"))
     else:
         spec = O.vanilla_param_spec(latent_dim=kw["latent_dim"])
     sd = O.make_params(spec, meta["seed"])
@@ -54,5 +55,6 @@ def oracle_kwargs(meta):
     if meta["arch"] == "VQVAE":
         d.update(vq_beta=kw.get("beta", 0.25))
     if meta["arch"] == "Autoencoder":
-        d.update(center_focus_sigma=kw.get("center_focus_sigma"))
+        d.update(center_focus_sigma=kw.get("center_focus_sigma"), use_mssim_loss=kw.get("use_mssim_loss", False),
+                 hidden_dims=kw.get("hidden_dims"))
     return d
