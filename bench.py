@@ -122,6 +122,8 @@ def conv_cost(fn, a, dsz):
         return 2 * macs, x_b + w_b + y_b
     if fn.endswith("_bwd_data"):
         return 2 * macs, y_b + w_b + x_b
+    if fn.endswith("_bwd"):                                  # both: dy + its pre-BN y, x, W -> dx, dW
+        return 4 * macs, 2 * y_b + 2 * x_b + w_b + k * c * R * R * 4
     return 2 * macs, x_b + y_b + k * c * R * R * 4          # bwd_filter writes fp32 dW
 
 
@@ -321,12 +323,15 @@ def selftest(args, distributed):
         dist.destroy_process_group()
 
 
-def dropin_leg(args, dtype, steps=None, warmup=3):
-    """The drop-in path a reference user runs (run.py -> VAEXperiment.training_step): the BaseVAE
-    model's forward, loss_function (vae_elbo_fwd on the GPU), loss.backward() (the fused HIP
-    backward behind autograd) and torch.optim.Adam on the flat parameter — eager, no graphs —
-    timed like the headline (same batch, synchronised region).  Returns its img/s."""
-    from vae_amd.experiment import VAEXperiment
+def dropin_leg(args, dtype, steps=None, warmup=3, engine="graph"):
+    """The drop-in path a reference user runs (vae_amd.run / experiment.fit, the counterpart of
+    run.py -> VAEXperiment.training_step), timed like the headline (same batch, synchronised
+    region).  engine="graph" (their default): experiment.GraphedSteps — the BaseVAE model's fused
+    step replayed from HIP graphs with the experiment's logging on the device and the torch
+    optimizer's state; engine="eager": the model's forward, loss_function (vae_elbo_fwd on the
+    GPU), loss.backward() (the fused HIP backward behind autograd) and torch.optim.Adam.  Returns
+    its img/s."""
+    from vae_amd.experiment import GraphedSteps, VAEXperiment
     from vae_amd.models import vae_models
     arch = {"vanilla": ("VanillaVAE", {}), "betaH": ("BetaVAE", {"loss_type": "H", "beta": 4}),
             "iwae": ("IWAE", {"num_samples": 5}), "vq": ("VQVAE", None)}[args.arch]
@@ -343,8 +348,12 @@ def dropin_leg(args, dtype, steps=None, warmup=3):
     x = torch.rand(args.batch, 3, 64, 64, generator=g, device="cuda")
     batch = (x, torch.zeros(args.batch, device="cuda"), [f"{i}.png" for i in range(args.batch)])
     steps = steps or max(10, min(args.steps, 50))
+    gs = GraphedSteps(exp, opt) if engine == "graph" else None
 
     def one(i):
+        if gs is not None:
+            gs(batch, i)
+            return
         opt.zero_grad(set_to_none=True)
         loss = exp.training_step(batch, i)
         loss.backward()
@@ -357,10 +366,13 @@ def dropin_leg(args, dtype, steps=None, warmup=3):
         one(i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if gs is not None:
+        gs.flush()
+    path = ("experiment.fit(engine='graph') step: GraphedSteps (fused HIP-graph step, torch Adam state shared, "
+            "logging on the device)" if gs is not None else
+            "VAEXperiment.training_step -> loss.backward -> torch.optim.Adam (eager; loss_function on the GPU ELBO kernel)")
     return {"value": round(args.batch * steps / el, 1), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 4),
-            "steps": steps, "path": "VAEXperiment.training_step -> loss.backward -> torch.optim.Adam (eager; "
-                                     "loss_function on the GPU ELBO kernel)",
-            "loss": float(exp.logged["loss"])}
+            "steps": steps, "path": path, "loss": float(exp.logged["loss"])}
 
 
 def main():
@@ -467,9 +479,10 @@ def main():
                  "frac": round(attain_us / (ms * 1e3), 4),
                  "mfma_frac": round(step_flops / (ms * 1e-3) / (peak_tf * 1e12), 4),
                  "step_gflop": round(step_flops / 1e9, 3)}
-    dropin = None
+    dropin = dropin_eager = None
     if world == 1 and not args.no_dropin:
-        dropin = dropin_leg(args, dtype)
+        dropin = dropin_leg(args, dtype, steps=max(20, min(args.steps, 100)))
+        dropin_eager = dropin_leg(args, dtype, engine="eager")
     line = {
         "metric": METRIC if args.arch == "vanilla" else f"train images/sec {args.arch} 64x64 bs={args.batch} (1 GPU config)",
         "value": round(value, 1),
@@ -496,6 +509,7 @@ def main():
         "roofline": roof,
         "step_roofline": step_roof,
         "dropin": dropin,
+        "dropin_eager": dropin_eager,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 10
+#define VAE_ABI_VERSION 11
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -305,6 +305,12 @@ int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream);
 int vae_convT2d_fwd(const vae_conv_args* a, void* stream);
 int vae_convT2d_bwd_data(const vae_conv_args* a, void* stream);
 int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream);
+/* both gradients of the layer in one call (the bwd_data and bwd_filter fields together): the
+ * decoder's full-resolution last ConvTranspose2d (final_layer.0, vanilla_vae.py:64-70; bf16,
+ * 32 -> 32 channels, 32x32 -> 64x64) in ONE pass over dy on a fused kernel whose filter partials
+ * take vae_convT2d_workspace_size(a, VAE_OP_BWD) bytes of workspace; any other layer runs
+ * vae_convT2d_bwd_data then vae_convT2d_bwd_filter. */
+int vae_convT2d_bwd(const vae_conv_args* a, void* stream);
 /* --- Linear (fc_mu/fc_var vanilla_vae.py:36-37,89-90; decoder_input :43,101) -------- */
 int vae_linear_fwd(const vae_linear_args* a, void* stream);
 int vae_linear_bwd_data(const vae_linear_args* a, void* stream);

@@ -4,6 +4,10 @@
 
 using namespace vae;
 
+namespace vae {
+int hires_convT_fwd_launch(const vae_conv_args* a, hipStream_t st);   // vae_hires.hip
+}
+
 // y[n,ho,wo,k] = Σ_{r,s,c: ho = h*S-P+r} xf(x)[n,h,w,c] · W[c][r][s][k] + b[k]   (phase GEMMs)
 extern "C" int vae_convT2d_fwd(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "convT2d_fwd") || !a->x || !a->wt || !a->y) return fail(VAE_E_BADARG, "convT2d_fwd: null tensor");
@@ -22,6 +26,11 @@ extern "C" int vae_convT2d_fwd(const vae_conv_args* a, void* stream) {
   p.sum_reps = a->sum_reps; p.sum_rstride = a->sum_rstride;
   p.residual = a->residual; p.res_xf = sanitize(a->residual_xf);
   if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "convT2d_fwd")) return rc;
+  if (a->dtype == VAE_BF16) {
+    // the decoder's full-resolution last ConvTranspose2d (32 -> 32, 32x32 -> 64x64)
+    const int rc = hires_convT_fwd_launch(a, (hipStream_t)stream);
+    if (rc != kHeadFallback) return rc;
+  }
   if (a->dtype == VAE_BF16) {
     // bf16 conv-GEMM: B = the swapped-axes weight copy WT[k][r][s][c] (k-contiguous rows), taken
     // from the caller (wt_t, refreshed with the weights) or built at the end of the workspace

@@ -765,6 +765,7 @@ extern "C" int vae_convT2d_workspace_size(const vae_conv_args* a, int32_t op, si
     case VAE_OP_FWD: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_fwd(c, nullptr); });
     case VAE_OP_BWD_DATA: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_bwd_data(c, nullptr); });
     case VAE_OP_BWD_FILTER: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_bwd_filter(c, nullptr); });
+    case VAE_OP_BWD: return ws_size(a, bytes, [](const vae_conv_args* c) { return vae_convT2d_bwd(c, nullptr); });
   }
   return fail(VAE_E_BADARG, "convT2d_workspace_size: op %d", op);
 }

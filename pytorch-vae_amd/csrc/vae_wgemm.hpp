@@ -40,6 +40,8 @@ struct WgParams {
   FastDiv fd_wu, fd_hu, fd_r;
   float* slab;                       // non-NULL: K slice s stores its partial dW at slab + s*slab_ld
   long slab_ld;                      //   (plain stores; wg_slab_reduce adds the slices into dw)
+  int own;                           // one K slice: each dW element has one writer, so it is
+                                     // accumulated with a plain load + store instead of an atomic
 };
 
 template <int BM> constexpr int wg_rs() { return BM == 32 ? 64 : (BM == 64 ? 160 : 288); }
@@ -266,6 +268,7 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, cha
         if (mm >= p.M) continue;
         const long o = mm * rowstride + (long)tap * p.J + jj;
         if (part) part[o] = acc[i][j][e];
+        else if (p.own) p.dw[o] += acc[i][j][e];
         else atomicAdd(p.dw + o, acc[i][j][e]);
       }
     }
@@ -513,6 +516,7 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
           if (mm >= p.M) continue;
           const long o = mm * rowstride + (long)t * p.J + jj;
           if (part) part[o] = acc[t][i][j][e];
+          else if (p.own) p.dw[o] += acc[t][i][j][e];
           else atomicAdd(p.dw + o, acc[t][i][j][e]);
         }
       }
@@ -619,7 +623,9 @@ struct WgPlan {
 };
 
 // Plan one layer (tile, K slices, partial slab in `ws` when it pays); launches nothing.
-inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out) {
+// slots_req > 0: the workgroups this layer should take (a share of a grouped launch) instead of
+// ~2 per CU of its own.
+inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots_req = 0) {
   p.fd_wu = make_fastdiv(p.wu);
   p.fd_hu = make_fastdiv(p.hu);
   p.fd_r = make_fastdiv(p.R);
@@ -642,7 +648,7 @@ inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out) {
   static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
   static const int mink_env = tune_env("VAE_WG_MINK", 0);
   const int mink = mink_env > 0 ? mink_env : (p.R == 1 ? 16 : 4);
-  const long slots = (long)wgpercu * kCUs;
+  const long slots = slots_req > 0 ? slots_req : (long)wgpercu * kCUs;
   long split = (slots + tiles - 1) / tiles;
   if (split > ksteps / mink) split = ksteps / mink;
   // one round of workgroups: ceil(slots / tiles) slices overfill the slots by up to tiles - 1
@@ -661,6 +667,7 @@ inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out) {
     if (!ws_fits(split * cols * 4, ws_bytes, "wgemm K-slice partials")) return VAE_E_BADARG;
     p.slab = static_cast<float*>(ws);
   }
+  p.own = (split == 1 && !p.slab) ? 1 : 0;
   out->p = p;
   out->T = T;
   out->taps = taps_in_block ? p.R : 0;

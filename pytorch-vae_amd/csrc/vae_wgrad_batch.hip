@@ -150,6 +150,28 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       if (rc) return rc;
     }
   }
+  // Grouped 64 x 64 / 128 x 128 layers (deep, few pixels, large dW): their K slices were sized
+  // for ~2 workgroups per CU each, and every slice adds its whole dW tile with fp32 atomics (the
+  // 3x3 128-channel layers: 8 slices x 1.2 MB).  In a group the layers fill the chip together, so
+  // each takes its share of one round of workgroups (one per CU), in proportion to its MACs:
+  // fewer slices, and a single slice accumulates with plain stores (WgParams.own).
+  static const int group_slots = tune_env("VAE_WG_GROUP_SLOTS", kCUs);
+  for (int c = 1; c < kClasses; ++c) {
+    double macs = 0.0;
+    for (int i = 0; i < n; ++i)
+      if (cls[i] == c) macs += (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
+    if (macs <= 0.0) continue;
+    for (int i = 0; i < n; ++i) {
+      if (cls[i] != c) continue;
+      const double m = (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
+      long slots = (long)(group_slots * m / macs + 0.5);
+      if (slots < 1) slots = 1;
+      WgParams w = plans[i].p;
+      w.slab = nullptr;
+      if (int rc = wg2_plan(w, querying() ? workspace : region(i), region_bytes(i), &plans[i], slots)) return rc;
+      if (wg_class(plans[i]) != c) return fail(VAE_E_UNSUPPORTED, "conv_bwd_filter_batch: replanned class");
+    }
+  }
   // one launch per tile class (chunks of kWgGroupMax layers)
   for (int c = 0; c < kClasses; ++c) {
     WgGroup g;

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -116,6 +116,7 @@ _SIGS = {
     "vae_convT2d_fwd": [POINTER(ConvArgs), c_void_p],
     "vae_convT2d_bwd_data": [POINTER(ConvArgs), c_void_p],
     "vae_convT2d_bwd_filter": [POINTER(ConvArgs), c_void_p],
+    "vae_convT2d_bwd": [POINTER(ConvArgs), c_void_p],
     "vae_linear_fwd": [POINTER(LinearArgs), c_void_p],
     "vae_linear_bwd_data": [POINTER(LinearArgs), c_void_p],
     "vae_linear_bwd_filter": [POINTER(LinearArgs), c_void_p],
@@ -188,6 +189,7 @@ WS_QUERY = {
     "vae_convT2d_fwd": ("vae_convT2d_workspace_size", OP_FWD),
     "vae_convT2d_bwd_data": ("vae_convT2d_workspace_size", OP_BWD_DATA),
     "vae_convT2d_bwd_filter": ("vae_convT2d_workspace_size", OP_BWD_FILTER),
+    "vae_convT2d_bwd": ("vae_convT2d_workspace_size", OP_BWD),
     "vae_linear_fwd": ("vae_linear_workspace_size", OP_FWD),
     "vae_linear_bwd_data": ("vae_linear_workspace_size", OP_BWD_DATA),
     "vae_linear_bwd_filter": ("vae_linear_workspace_size", OP_BWD_FILTER),

@@ -226,6 +226,10 @@ class GraphedSteps:
         self._per: List[Tensor] = []                 # per-image losses of the epoch (device)
         self._names: List[Any] = []
         self._ext = None                             # device extreme-image state
+        self._book: Dict[int, Any] = {}              # bookkeeping graph per batch size
+        self._per_img: Dict[int, Tensor] = {}
+        self._terms: Dict[str, Tensor] = {}
+        self._k = None
 
     def _shared_adam(self):
         from .engine import FusedAdam
@@ -257,47 +261,79 @@ class GraphedSteps:
         self.fused.set_lr(self.opt.param_groups[0]['lr'])
         exp.curr_device = imgs.device
         plan = step.plan
-        eps = None
-        if hasattr(plan, "eps"):
-            eps = (torch.zeros(plan.eps.shape, device=imgs.device) if getattr(step, "zero_eps", False)
-                   else torch.randn(plan.eps.shape, device=imgs.device))
-        step(imgs, eps)
+        if hasattr(plan, "eps") and not getattr(step, "zero_eps", False):
+            plan.eps.normal_()                        # torch.randn_like(std), vanilla_vae.py:116
+        step(imgs)
         self.nstep += 1
         self.opt.state[model.flat]['step'] = torch.tensor(float(self.nstep))
         if hasattr(model, "num_iter"):
             model.num_iter += 1                       # BetaVAE: the loss_function's counter
-        # loss terms: the rank mean when distributed (TrainStep reduces them with the last gradient
-        # bucket, experiment.py:55 sync_dist) — no collective of their own here
-        out = plan.metrics if step.world > 1 else plan.out
-        third = "VQ_Loss" if not hasattr(plan, "eps") else "KLD"
-        terms = {'loss': out[0].clone(), 'Reconstruction_Loss': out[1].clone(), third: out[2].clone()}
-        if getattr(step, "zero_eps", False):                  # Autoencoder: no KL, no feature loss
-            terms.update(KLD=torch.zeros_like(out[2]), feature_loss=torch.zeros_like(out[2]))
-        exp.logged.update(terms)
-        per = plan.per_img.view(B, -1).mean(dim=1)
-        recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:, 0]
-        self._per.append(per)
+        book = self._book.get(B)
+        if book is None:
+            book = self._book[B] = self._make_book(step, imgs.device)
+        book.replay()
+        exp.logged.update(self._terms)
+        self._per.append(self._per_img[B].clone())
         self._names.append(names)
-        self._extremes(per, imgs, recon, len(self._names) - 1)
         return exp.logged['loss']
 
-    def _extremes(self, per: Tensor, imgs: Tensor, recon: Tensor, k: int):
-        """experiment.py:65-84 on the device: the running highest / lowest per-image loss with its
-        image, reconstruction and (step, index) — first index wins ties, as the strict comparisons."""
-        dev = per.device
+    def _make_book(self, step, dev):
+        """One HIP graph per batch size for the per-step bookkeeping of training_step on the
+        device (experiment.py:45-86): the logged loss terms, the per-image losses and the running
+        extreme images (:65-84) — a dozen small ops replayed as one launch."""
+        plan = step.plan
+        B = plan.x.shape[0]
         if self._ext is None:
-            self._ext = {key: {'loss': torch.full((), init, device=dev), 'img': torch.zeros_like(imgs[:1]),
-                               'recon': torch.zeros_like(recon[:1]), 'at': torch.full((2,), -1, dtype=torch.int64, device=dev)}
+            img = plan.x[:1]
+            recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:1, 0]
+            self._ext = {key: {'loss': torch.full((), init, device=dev), 'img': torch.zeros_like(img),
+                               'recon': torch.zeros_like(recon),
+                               'at': torch.full((2,), -1, dtype=torch.int64, device=dev)}
                          for key, init in (('highest', float('-inf')), ('lowest', float('inf')))}
-        for key, i in (('highest', torch.argmax(per)), ('lowest', torch.argmin(per))):
+            self._k = torch.zeros((), dtype=torch.int64, device=dev)           # step of the epoch
+            third = "VQ_Loss" if not hasattr(plan, "eps") else "KLD"
+            self._terms = {'loss': torch.zeros((), device=dev), 'Reconstruction_Loss': torch.zeros((), device=dev),
+                           third: torch.zeros((), device=dev)}
+            if getattr(step, "zero_eps", False):                                # Autoencoder
+                self._terms.update(KLD=torch.zeros((), device=dev), feature_loss=torch.zeros((), device=dev))
+        self._per_img[B] = torch.zeros(B, device=dev)
+        saved = {k: {kk: vv.clone() for kk, vv in e.items()} for k, e in self._ext.items()}
+        k0 = self._k.clone()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self._book_ops(plan, step.world, B)           # warm-up (lazy init), then the capture
+            with torch.cuda.graph(g, stream=s):
+                self._book_ops(plan, step.world, B)
+        torch.cuda.current_stream().wait_stream(s)
+        # this step's record: the state before the warm-up, then one replay
+        for k, e in saved.items():
+            for kk, vv in e.items():
+                self._ext[k][kk].copy_(vv)
+        self._k.copy_(k0)
+        return g
+
+    def _book_ops(self, plan, world: int, B: int):
+        # loss terms: the rank mean when distributed (TrainStep reduces them with the last gradient
+        # bucket, experiment.py:55 sync_dist) — no collective of their own here
+        out = plan.metrics if world > 1 else plan.out
+        for i, k in enumerate(list(self._terms)[:3]):
+            self._terms[k].copy_(out[i])
+        per = plan.per_img.view(B, -1).mean(dim=1)
+        self._per_img[B].copy_(per)
+        recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:, 0]
+        for key in ('highest', 'lowest'):
             e = self._ext[key]
-            v = per[i]
+            # index_select with a device index: no host synchronisation (capturable)
+            i = (torch.argmax(per) if key == 'highest' else torch.argmin(per)).reshape(1)
+            v = per.index_select(0, i).reshape(())
             better = v > e['loss'] if key == 'highest' else v < e['loss']
-            e['loss'] = torch.where(better, v, e['loss'])
-            e['img'] = torch.where(better, imgs[i].unsqueeze(0), e['img'])
-            e['recon'] = torch.where(better, recon[i].unsqueeze(0).detach(), e['recon'])
-            at = torch.stack([torch.tensor(k, device=dev), i.to(torch.int64)])
-            e['at'] = torch.where(better, at, e['at'])
+            e['loss'].copy_(torch.where(better, v, e['loss']))
+            e['img'].copy_(torch.where(better, plan.x.index_select(0, i), e['img']))
+            e['recon'].copy_(torch.where(better, recon.index_select(0, i), e['recon']))
+            e['at'].copy_(torch.where(better, torch.cat([self._k.reshape(1), i.to(torch.int64)]), e['at']))
+        self._k.add_(1)
 
     def flush(self):
         """Hand the epoch's device-side records to the host (one synchronisation): per-image
@@ -313,14 +349,18 @@ class GraphedSteps:
         if self._ext is not None:
             for key, e in self._ext.items():
                 k, i = e['at'].tolist()
-                if k < 0:
-                    continue
-                v = float(e['loss'])
-                better = v > exp.extreme_images[key]['loss'] if key == 'highest' else v < exp.extreme_images[key]['loss']
-                if better:
-                    exp.extreme_images[key] = {'loss': v, 'img': e['img'].cpu(), 'recon': e['recon'].cpu(),
-                                               'name': self._names[k][i]}
-        self._per, self._names, self._ext = [], [], None
+                if k >= 0:
+                    v = float(e['loss'])
+                    better = (v > exp.extreme_images[key]['loss'] if key == 'highest'
+                              else v < exp.extreme_images[key]['loss'])
+                    if better:
+                        exp.extreme_images[key] = {'loss': v, 'img': e['img'].cpu(), 'recon': e['recon'].cpu(),
+                                                   'name': self._names[k][i]}
+                # reset in place: the bookkeeping graphs hold these tensors
+                e['loss'].fill_(float('-inf') if key == 'highest' else float('inf'))
+                e['at'].fill_(-1)
+            self._k.zero_()
+        self._per, self._names = [], []
 
 
 def _fusable(model) -> bool:

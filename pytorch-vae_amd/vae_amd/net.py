@@ -508,8 +508,8 @@ class StepPlan:
             if i > 0:
                 a.dx_epi = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t), aux=x_t)
                 self.bwd_sums(a, dec_pre[i - 1])
-            self._add(Bw, "vae_convT2d_bwd_data", a)
-            f = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
+            f = a if i == len(r) - 1 else L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp,
+                                                      r=3, stride=2, pad=1)
             f.x = x_t.data_ptr()
             if i > 0:
                 f.x_xf = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t))
@@ -517,7 +517,13 @@ class StepPlan:
             f.dy_xf = dy_xf
             f.dw = self.g(dec_w[i] + ".weight")      # bias gradient: closed form (bn_finalize / bwd_extras)
             self.bwd_extras(f, dec_pre[i])
-            self._add(Bw, "vae_convT2d_bwd_filter", f)
+            if i == len(r) - 1:
+                # the full-resolution last ConvTranspose2d: both gradients in one pass over dy
+                # (vaehip.h vae_convT2d_bwd; other shapes run the two calls inside it)
+                self._add(Bw, "vae_convT2d_bwd", a)
+            else:
+                self._add(Bw, "vae_convT2d_bwd_data", a)
+                self._add(Bw, "vae_convT2d_bwd_filter", f)
         # decoder_input: dz -> d[mu|logvar] (reparameterization + KL), and its weight grads
         a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
         a.dy = self.g_h0.data_ptr()
