@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 11
+#define VAE_ABI_VERSION 12
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -394,6 +394,23 @@ int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const vae_conv_ar
                               void* workspace, int64_t workspace_bytes, void* stream);
 int vae_conv_bwd_filter_batch_workspace_size(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
                                              size_t* bytes);
+/* --- the bookkeeping of one training step (experiment.py:45-86 training_step after the loss):
+ * one launch instead of a dozen small tensor ops.
+ *   terms[0..nterms) = src_terms[0..nterms)                 (the logged loss terms)
+ *   per[b] = mean_s per_img[b*samples + s]                  (per-image MSE, experiment.py:58-62)
+ *   the running extremes (experiment.py:65-84): if max_b per[b] > best[0] (strictly; the first
+ *   index wins ties) then best[0] = that loss, at[0..1] = {step, b}, hi_img = img[b],
+ *   hi_recon = recon[b*samples] (first sample); the same with min / best[1] / at[2..3] / lo_*.
+ * img: [batch][img_elems] fp32, recon: [batch*samples][img_elems] fp32; one workgroup. */
+typedef struct vae_record_args {
+  int32_t batch, samples, img_elems, nterms, step;
+  const float* src_terms; float* terms;
+  const float* per_img; float* per;
+  const float* img; const float* recon;
+  float* best; int32_t* at;            /* best[2] = {highest, lowest}, at[4] */
+  float* hi_img; float* hi_recon; float* lo_img; float* lo_recon;
+} vae_record_args;
+int vae_step_record(const vae_record_args* a, void* stream);
 /* --- start of a training step: zero `bytes` at `zero` and ++*step ------------------ */
 int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream);
 

@@ -4,6 +4,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <math.h>
+
 #include "vae_common.hpp"
 
 namespace vae {
@@ -659,6 +661,74 @@ extern "C" int vae_cast_bf16(int64_t n, const float* src, void* dst, void* strea
   if (!src || !dst) return fail(VAE_E_BADARG, "cast_bf16: null");
   VAE_LAUNCH(cast_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (long)n, src, (__bf16*)dst);
   return check_launch("cast_bf16");
+}
+
+// ------------------------------------------------------------------ training-step record
+namespace {
+__global__ void __launch_bounds__(256) step_record_kernel(const vae_record_args a) {
+  __shared__ float pv[1024];
+  __shared__ float rv[2][256];
+  __shared__ int ri[2][256];
+  __shared__ int win[2];
+  const int tid = threadIdx.x;
+  if (tid < a.nterms) a.terms[tid] = a.src_terms[tid];
+  const float inv_s = 1.0f / (float)a.samples;
+  for (int b = tid; b < a.batch; b += 256) {
+    float v = 0.f;
+    for (int s = 0; s < a.samples; ++s) v += a.per_img[b * a.samples + s];
+    v *= inv_s;
+    pv[b] = v;
+    a.per[b] = v;
+  }
+  __syncthreads();
+  // first index of the maximum / minimum (ties -> lowest index, as the reference's strict '>'/'<')
+  float mx = -INFINITY, mn = INFINITY;
+  int imx = 0x7fffffff, imn = 0x7fffffff;
+  for (int b = tid; b < a.batch; b += 256) {
+    const float v = pv[b];
+    if (v > mx) { mx = v; imx = b; }
+    if (v < mn) { mn = v; imn = b; }
+  }
+  rv[0][tid] = mx; ri[0][tid] = imx; rv[1][tid] = mn; ri[1][tid] = imn;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+      const float v1 = rv[0][tid + off], v0 = rv[0][tid];
+      const int i1 = ri[0][tid + off], i0 = ri[0][tid];
+      if (v1 > v0 || (v1 == v0 && i1 < i0)) { rv[0][tid] = v1; ri[0][tid] = i1; }
+      const float w1 = rv[1][tid + off], w0 = rv[1][tid];
+      const int j1 = ri[1][tid + off], j0 = ri[1][tid];
+      if (w1 < w0 || (w1 == w0 && j1 < j0)) { rv[1][tid] = w1; ri[1][tid] = j1; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    win[0] = rv[0][0] > a.best[0] ? ri[0][0] : -1;
+    win[1] = rv[1][0] < a.best[1] ? ri[1][0] : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int b = win[k];
+    if (b < 0) continue;
+    float* di = k == 0 ? a.hi_img : a.lo_img;
+    float* dr = k == 0 ? a.hi_recon : a.lo_recon;
+    for (int e = tid; e < a.img_elems; e += 256) {
+      di[e] = a.img[(long)b * a.img_elems + e];
+      dr[e] = a.recon[(long)b * a.samples * a.img_elems + e];
+    }
+    if (tid == 0) { a.best[k] = rv[k][0]; a.at[2 * k] = a.step; a.at[2 * k + 1] = b; }
+  }
+}
+}  // namespace
+
+extern "C" int vae_step_record(const vae_record_args* a, void* stream) {
+  if (!a || a->batch <= 0 || a->batch > 1024 || a->samples <= 0 || a->img_elems <= 0 || a->nterms < 0 || a->nterms > 8 ||
+      (a->nterms && (!a->src_terms || !a->terms)) || !a->per_img || !a->per || !a->img || !a->recon || !a->best || !a->at ||
+      !a->hi_img || !a->hi_recon || !a->lo_img || !a->lo_recon)
+    return fail(VAE_E_BADARG, "step_record: args");
+  VAE_LAUNCH(step_record_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, *a);
+  return check_launch("step_record");
 }
 
 extern "C" int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream) {

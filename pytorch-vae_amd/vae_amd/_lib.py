@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -100,6 +100,13 @@ class ReconArgs(ctypes.Structure):
                 ("grad_scale", c_float), ("grad_recon", c_void_p), ("ld", c_int32)]
 
 
+class RecordArgs(ctypes.Structure):
+    _fields_ = [("batch", c_int32), ("samples", c_int32), ("img_elems", c_int32), ("nterms", c_int32),
+                ("step", c_int32), ("src_terms", c_void_p), ("terms", c_void_p), ("per_img", c_void_p),
+                ("per", c_void_p), ("img", c_void_p), ("recon", c_void_p), ("best", c_void_p), ("at", c_void_p),
+                ("hi_img", c_void_p), ("hi_recon", c_void_p), ("lo_img", c_void_p), ("lo_recon", c_void_p)]
+
+
 class SwapDesc(ctypes.Structure):
     _fields_ = [("src", c_void_p), ("dst", c_void_p), ("a", c_int32), ("rs", c_int32), ("b", c_int32)]
 
@@ -135,6 +142,7 @@ _SIGS = {
                       ctypes.c_double, c_float, c_float, c_void_p, c_void_p],
     "vae_cast_bf16": [c_int64, c_void_p, c_void_p, c_void_p],
     "vae_step_begin": [c_void_p, c_int64, c_void_p, c_void_p],
+    "vae_step_record": [POINTER(RecordArgs), c_void_p],
     "vae_swap_axes": [c_int32, c_void_p, c_void_p],
     "vae_nchw_to_nhwc_pad": [c_int32, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
     "vae_pad_channels": [c_int32, c_int64, c_int32, c_int32, c_void_p, c_void_p, c_void_p],
@@ -241,6 +249,7 @@ class FilterBatch:
         self.kinds = (c_int32 * n)(*[self.FNS[fn] for fn, _ in self.calls])
         self.items = (c_void_p * n)(*[ctypes.addressof(ref._obj) for _, ref in self.calls])
         self.workspace, self.workspace_bytes = None, 0
+        self.side = False            # run on the plan's side stream (net.run_calls)
 
     @property
     def args(self):

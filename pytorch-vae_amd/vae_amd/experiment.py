@@ -15,6 +15,7 @@ or `fit()` below — calls.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from typing import Any, Dict, List, Optional
 
@@ -223,13 +224,12 @@ class GraphedSteps:
                        betas=g['betas'])
         self.fused = None
         self.nstep = 0
-        self._per: List[Tensor] = []                 # per-image losses of the epoch (device)
+        self._per: List[Any] = []                    # (offset, batch) of each step in _per_buf
         self._names: List[Any] = []
         self._ext = None                             # device extreme-image state
-        self._book: Dict[int, Any] = {}              # bookkeeping graph per batch size
-        self._per_img: Dict[int, Tensor] = {}
         self._terms: Dict[str, Tensor] = {}
-        self._k = None
+        self._img_shape = None
+        self._lr = None
 
     def _shared_adam(self):
         from .engine import FusedAdam
@@ -258,7 +258,11 @@ class GraphedSteps:
             if self.fused is None:
                 self.fused = self._shared_adam()
             step = self.steps[B] = model.fused_train_step(B, opt=self.fused, **self.kw)
-        self.fused.set_lr(self.opt.param_groups[0]['lr'])
+        lr = self.opt.param_groups[0]['lr']
+        if lr != self._lr:                            # (a device scalar: written only on change)
+            self.fused.set_lr(lr)
+            self._lr = lr
+        self._img_shape = tuple(imgs.shape[1:])
         exp.curr_device = imgs.device
         plan = step.plan
         if hasattr(plan, "eps") and not getattr(step, "zero_eps", False):
@@ -268,99 +272,75 @@ class GraphedSteps:
         self.opt.state[model.flat]['step'] = torch.tensor(float(self.nstep))
         if hasattr(model, "num_iter"):
             model.num_iter += 1                       # BetaVAE: the loss_function's counter
-        book = self._book.get(B)
-        if book is None:
-            book = self._book[B] = self._make_book(step, imgs.device)
-        book.replay()
+        self._record(step, imgs)
         exp.logged.update(self._terms)
-        self._per.append(self._per_img[B].clone())
         self._names.append(names)
         return exp.logged['loss']
 
-    def _make_book(self, step, dev):
-        """One HIP graph per batch size for the per-step bookkeeping of training_step on the
-        device (experiment.py:45-86): the logged loss terms, the per-image losses and the running
-        extreme images (:65-84) — a dozen small ops replayed as one launch."""
+    def _record(self, step, imgs):
+        """The per-step bookkeeping of training_step on the device in ONE launch
+        (vaehip.h vae_step_record): the logged loss terms, the per-image losses (experiment.py:58-62,
+        kept for the data module until flush()) and the running extreme images (:65-84)."""
+        from . import _lib as L
         plan = step.plan
         B = plan.x.shape[0]
+        S = plan.recon.shape[0] // B
+        dev = imgs.device
         if self._ext is None:
-            img = plan.x[:1]
-            recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:1, 0]
-            self._ext = {key: {'loss': torch.full((), init, device=dev), 'img': torch.zeros_like(img),
-                               'recon': torch.zeros_like(recon),
-                               'at': torch.full((2,), -1, dtype=torch.int64, device=dev)}
-                         for key, init in (('highest', float('-inf')), ('lowest', float('inf')))}
-            self._k = torch.zeros((), dtype=torch.int64, device=dev)           # step of the epoch
+            ie = plan.x[0].numel()
             third = "VQ_Loss" if not hasattr(plan, "eps") else "KLD"
-            self._terms = {'loss': torch.zeros((), device=dev), 'Reconstruction_Loss': torch.zeros((), device=dev),
-                           third: torch.zeros((), device=dev)}
+            self._terms_buf = torch.zeros(3, device=dev)
+            self._terms = {'loss': self._terms_buf[0], 'Reconstruction_Loss': self._terms_buf[1],
+                           third: self._terms_buf[2]}
             if getattr(step, "zero_eps", False):                                # Autoencoder
-                self._terms.update(KLD=torch.zeros((), device=dev), feature_loss=torch.zeros((), device=dev))
-        self._per_img[B] = torch.zeros(B, device=dev)
-        saved = {k: {kk: vv.clone() for kk, vv in e.items()} for k, e in self._ext.items()}
-        k0 = self._k.clone()
-        g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            self._book_ops(plan, step.world, B)           # warm-up (lazy init), then the capture
-            with torch.cuda.graph(g, stream=s):
-                self._book_ops(plan, step.world, B)
-        torch.cuda.current_stream().wait_stream(s)
-        # this step's record: the state before the warm-up, then one replay
-        for k, e in saved.items():
-            for kk, vv in e.items():
-                self._ext[k][kk].copy_(vv)
-        self._k.copy_(k0)
-        return g
-
-    def _book_ops(self, plan, world: int, B: int):
-        # loss terms: the rank mean when distributed (TrainStep reduces them with the last gradient
-        # bucket, experiment.py:55 sync_dist) — no collective of their own here
-        out = plan.metrics if world > 1 else plan.out
-        for i, k in enumerate(list(self._terms)[:3]):
-            self._terms[k].copy_(out[i])
-        per = plan.per_img.view(B, -1).mean(dim=1)
-        self._per_img[B].copy_(per)
-        recon = plan.recon.view(B, -1, *plan.recon.shape[1:])[:, 0]
-        for key in ('highest', 'lowest'):
-            e = self._ext[key]
-            # index_select with a device index: no host synchronisation (capturable)
-            i = (torch.argmax(per) if key == 'highest' else torch.argmin(per)).reshape(1)
-            v = per.index_select(0, i).reshape(())
-            better = v > e['loss'] if key == 'highest' else v < e['loss']
-            e['loss'].copy_(torch.where(better, v, e['loss']))
-            e['img'].copy_(torch.where(better, plan.x.index_select(0, i), e['img']))
-            e['recon'].copy_(torch.where(better, recon.index_select(0, i), e['recon']))
-            e['at'].copy_(torch.where(better, torch.cat([self._k.reshape(1), i.to(torch.int64)]), e['at']))
-        self._k.add_(1)
+                z = torch.zeros((), device=dev)
+                self._terms.update(KLD=z, feature_loss=z)
+            self._ext = {'best': torch.tensor([float('-inf'), float('inf')], device=dev),
+                         'at': torch.full((4,), -1, dtype=torch.int32, device=dev),
+                         'img': torch.zeros(2, ie, device=dev), 'recon': torch.zeros(2, ie, device=dev)}
+            self._per_buf = torch.zeros(1024 * 64, device=dev)              # grows in flush-sized chunks
+            self._per_off = 0
+        if self._per_off + B > self._per_buf.numel():                       # keep the epoch's records
+            self._per_buf = torch.cat([self._per_buf, torch.zeros_like(self._per_buf)])
+        e = self._ext
+        out = plan.metrics if step.world > 1 else plan.out
+        a = L.RecordArgs(batch=B, samples=S, img_elems=plan.x[0].numel(), nterms=3, step=len(self._names))
+        a.src_terms, a.terms = out.data_ptr(), self._terms_buf.data_ptr()
+        a.per_img, a.per = plan.per_img.data_ptr(), self._per_buf.data_ptr() + 4 * self._per_off
+        a.img, a.recon = plan.x.data_ptr(), plan.recon.data_ptr()
+        a.best, a.at = e['best'].data_ptr(), e['at'].data_ptr()
+        a.hi_img, a.lo_img = e['img'][0].data_ptr(), e['img'][1].data_ptr()
+        a.hi_recon, a.lo_recon = e['recon'][0].data_ptr(), e['recon'][1].data_ptr()
+        L.call("vae_step_record", ctypes.byref(a), L.stream_ptr())
+        self._per.append((self._per_off, B))
+        self._per_off += B
 
     def flush(self):
         """Hand the epoch's device-side records to the host (one synchronisation): per-image
         losses to the data module (dataset.py:130-136), extreme images to the experiment."""
         exp = self.exp
         if self._per:
-            per = torch.cat(self._per).cpu().tolist()
+            per = self._per_buf[:self._per_off].cpu().tolist()
             if exp.datamodule is not None and hasattr(exp.datamodule, "record_img_losses"):
-                o = 0
-                for names in self._names:
-                    exp.datamodule.record_img_losses(names, per[o:o + len(names)])
-                    o += len(names)
+                for (o, b), names in zip(self._per, self._names):
+                    exp.datamodule.record_img_losses(names, per[o:o + b])
         if self._ext is not None:
-            for key, e in self._ext.items():
-                k, i = e['at'].tolist()
-                if k >= 0:
-                    v = float(e['loss'])
-                    better = (v > exp.extreme_images[key]['loss'] if key == 'highest'
-                              else v < exp.extreme_images[key]['loss'])
-                    if better:
-                        exp.extreme_images[key] = {'loss': v, 'img': e['img'].cpu(), 'recon': e['recon'].cpu(),
-                                                   'name': self._names[k][i]}
-                # reset in place: the bookkeeping graphs hold these tensors
-                e['loss'].fill_(float('-inf') if key == 'highest' else float('inf'))
-                e['at'].fill_(-1)
-            self._k.zero_()
-        self._per, self._names = [], []
+            e = self._ext
+            best, at = e['best'].tolist(), e['at'].tolist()
+            shape = self._img_shape
+            for k, key in enumerate(('highest', 'lowest')):
+                step_i, i = at[2 * k], at[2 * k + 1]
+                if step_i < 0:
+                    continue
+                v = best[k]
+                better = v > exp.extreme_images[key]['loss'] if key == 'highest' else v < exp.extreme_images[key]['loss']
+                if better:
+                    exp.extreme_images[key] = {'loss': v, 'img': e['img'][k].view(1, *shape).cpu(),
+                                               'recon': e['recon'][k].view(1, *shape).cpu(),
+                                               'name': self._names[step_i][i]}
+            e['best'].copy_(torch.tensor([float('-inf'), float('inf')]))
+            e['at'].fill_(-1)
+        self._per, self._names, self._per_off = [], [], 0
 
 
 def _fusable(model) -> bool:

@@ -130,7 +130,8 @@ class StepPlan:
     def __init__(self, net: VAENet, batch: int, *, loss: str = "vanilla", kld_weight: float = 1e-8,
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
                  capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
-                 concurrent: bool = False, fuse_bn: bool = False, bn_in_consumer: bool = True):
+                 concurrent: bool = False, fuse_bn: bool = False, bn_in_consumer: bool = True,
+                 wg_overlap: bool = False):
         self.net = net
         self.B = batch
         # training=False: eval-mode BatchNorm (running statistics, nothing updated; the
@@ -225,6 +226,14 @@ class StepPlan:
         self.bwd_calls: List = []
         # side stream for the weight gradients (run_calls); None: one stream
         self.side = torch.cuda.Stream(device=dev) if (concurrent and training) else None
+        # wg_overlap: the decoder's weight gradients (one batch) on a side stream, beside the
+        # encoder's data-gradient chain (batch_wgrads); one fork and one join per step.  Off by
+        # default: measured 0.670 vs 0.648 ms/step (B=64, graph-replayed) — the graph's cross-stream
+        # edges cost more than the overlap gains, as the per-call side stream of round 1 did
+        self.wg_overlap = wg_overlap and training and not concurrent and not os.environ.get("VAE_NO_WG_OVERLAP")
+        self.side_all = self.side is not None            # concurrent: every weight-gradient call
+        if self.wg_overlap:
+            self.side = torch.cuda.Stream(device=dev)
         self._build()
         # the backward as built, one call per op; bwd_calls batches its weight gradients
         # (batch_wgrads: one vae_conv_bwd_filter_batch per backward segment)
@@ -243,8 +252,18 @@ class StepPlan:
         """Rebuild bwd_calls from bwd_calls_raw with the conv / convT weight gradients of each
         backward segment (calls [ends[k-1], ends[k]) of the raw list) moved into one
         vae_conv_bwd_filter_batch call at the segment's end, and size the workspaces.  Returns the
-        segment ends as indices into the new list.  VAE_NO_WG_BATCH=1 keeps one call per layer."""
-        self.bwd_calls, new_ends = batch_filter_calls(self.bwd_calls_raw, ends)
+        segment ends as indices into the new list.  VAE_NO_WG_BATCH=1 keeps one call per layer.
+
+        With one segment (one rank) and wg_overlap, the decoder's weight gradients form a batch of
+        their own, issued on the side stream where the decoder's data-gradient chain ends: it runs
+        beside the encoder's data gradients (the critical path) instead of after them."""
+        splits = []
+        if self.wg_overlap and len(ends) == 1:
+            raw = self.bwd_calls_raw
+            first_lin = next((i for i, (fn, _) in enumerate(raw) if fn == "vae_linear_bwd_data"), None)
+            if first_lin is not None:
+                splits = [first_lin]
+        self.bwd_calls, new_ends = batch_filter_calls(self.bwd_calls_raw, ends, splits)
         size_workspaces(self, [self.fwd_calls, self.bwd_calls])
         return new_ends
 
@@ -671,29 +690,40 @@ BATCH_FN = "vae_conv_bwd_filter_batch"
 DEFERRED_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_unpad_accumulate"))
 
 
-def batch_filter_calls(calls, ends):
+def batch_filter_calls(calls, ends, splits=()):
     """Weight gradients are read only by the optimizer, so within a backward segment they can
     run after the segment's data-gradient chain and together: the conv / convT bwd_filter calls
     of each segment become one vae_conv_bwd_filter_batch call (grouped launches) at its end,
     followed by the calls that must follow them (vae_unpad_accumulate reads the padded first-layer
-    weight gradient).  Returns (new call list, new segment ends)."""
+    weight gradient).  `splits`: raw call indices inside a segment where the weight gradients so
+    far are emitted as a batch of their own that runs on the plan's side stream (run_calls).
+    Returns (new call list, new segment ends)."""
     if os.environ.get("VAE_NO_WG_BATCH"):
         return list(calls), list(ends)
     out, new_ends, lo = [], [], 0
-    for end in ends:
-        deferred, wg = [], []
-        for fn, ref in calls[lo:end]:
-            if fn in DEFERRED_FNS:
-                deferred.append((fn, ref))
-                if fn != "vae_unpad_accumulate":
-                    wg.append((fn, ref))
-            else:
-                out.append((fn, ref))
-        if len(wg) > 1:
-            out.append((BATCH_FN, L.FilterBatch(wg)))
+
+    def emit(deferred, side):
+        wg = [(fn, ref) for fn, ref in deferred if fn != "vae_unpad_accumulate"]
+        if len(wg) > 1 or (side and wg):
+            b = L.FilterBatch(wg)
+            b.side = side
+            out.append((BATCH_FN, b))
             out.extend((fn, ref) for fn, ref in deferred if fn == "vae_unpad_accumulate")
         else:
             out.extend(deferred)
+
+    for end in ends:
+        deferred = []
+        for i in range(lo, end):
+            if i in splits and deferred:
+                emit(deferred, True)
+                deferred = []
+            fn, ref = calls[i]
+            if fn in DEFERRED_FNS:
+                deferred.append((fn, ref))
+            else:
+                out.append((fn, ref))
+        emit(deferred, False)
         new_ends.append(len(out))
         lo = end
     return out, new_ends
@@ -722,7 +752,8 @@ def size_workspaces(plan, call_lists):
             else:
                 arg = ref._obj
                 b = L.workspace_size(fn, arg)
-            chain = "side" if side_on and fn in SIDE_FNS else "main"
+            on_side = (fn == BATCH_FN and getattr(ref, "side", False)) or (getattr(plan, "side_all", True) and fn in SIDE_FNS)
+            chain = "side" if side_on and on_side else "main"
             need[chain] = max(need[chain], b)
             sized.append((arg, b, chain))
     bufs = {c: torch.empty(max(1, (n + 3) // 4), dtype=torch.float32, device=dev) for c, n in need.items()}
@@ -751,7 +782,8 @@ def run_calls(plan, calls, stream):
         side = None                          # an explicit foreign stream: keep everything on it
     forked = False
     for fn, arg in calls:
-        if side is not None and fn in SIDE_FNS:
+        on_side = (fn == BATCH_FN and getattr(arg, "side", False)) or (getattr(plan, "side_all", True) and fn in SIDE_FNS)
+        if side is not None and on_side:
             side.wait_stream(main)
             call_one(fn, arg, side.cuda_stream)
             forked = True

@@ -276,3 +276,52 @@ def test_head_fwd_bwd(dtype, fused):
     # LeakyReLU branch (a factor 1/slope on an element that is ~0 anyway)
     d = dx.float().permute(0, 3, 1, 2).cpu()
     assert float((d - z.grad).norm() / z.grad.norm()) < t
+
+
+def test_step_record_tracks_terms_per_image_and_extremes():
+    """vae_step_record (the device bookkeeping of experiment.py:45-86 training_step) against the
+    reference's loop: per-image mean over samples, strict '>' / '<' running extremes with the
+    first index winning ties, the image and the first sample's reconstruction copied."""
+    L = _L()
+    dev = "cuda"
+    B, S, ie = 6, 2, 3 * 4 * 4
+    best = torch.tensor([float("-inf"), float("inf")], device=dev)
+    at = torch.full((4,), -1, dtype=torch.int32, device=dev)
+    hi_img, lo_img = torch.zeros(ie, device=dev), torch.zeros(ie, device=dev)
+    hi_rec, lo_rec = torch.zeros(ie, device=dev), torch.zeros(ie, device=dev)
+    ref_best, ref_at = [float("-inf"), float("inf")], [(-1, -1), (-1, -1)]
+    g = torch.Generator().manual_seed(3)
+    for step in range(3):
+        src = torch.randn(3, generator=g).to(dev)
+        per_img = torch.rand(B * S, generator=g)
+        if step == 1:
+            per_img[2 * S:3 * S] = per_img.view(B, S).mean(1).max() + 1.0   # a tie for the max:
+            per_img[4 * S:5 * S] = per_img[2 * S:3 * S]                       # index 2 must win
+        img = torch.randn(B, ie, generator=g)
+        rec = torch.randn(B * S, ie, generator=g)
+        terms, per = torch.zeros(3, device=dev), torch.zeros(B, device=dev)
+        a = L.RecordArgs(batch=B, samples=S, img_elems=ie, nterms=3, step=step)
+        keep = [src, per_img.to(dev), img.to(dev), rec.to(dev)]
+        a.src_terms, a.terms = keep[0].data_ptr(), terms.data_ptr()
+        a.per_img, a.per = keep[1].data_ptr(), per.data_ptr()
+        a.img, a.recon = keep[2].data_ptr(), keep[3].data_ptr()
+        a.best, a.at = best.data_ptr(), at.data_ptr()
+        a.hi_img, a.hi_recon, a.lo_img, a.lo_recon = hi_img.data_ptr(), hi_rec.data_ptr(), lo_img.data_ptr(), lo_rec.data_ptr()
+        L.call("vae_step_record", ctypes.byref(a), _stream())
+        torch.cuda.synchronize()
+        pm = per_img.view(B, S).mean(1)
+        torch.testing.assert_close(terms.cpu(), src.cpu())
+        torch.testing.assert_close(per.cpu(), pm)
+        for k, better in ((0, lambda v, b: v > b), (1, lambda v, b: v < b)):
+            for i in range(B):                          # experiment.py:65-84, in order
+                if better(float(pm[i]), ref_best[k]):
+                    ref_best[k], ref_at[k] = float(pm[i]), (step, i)
+                    want_img, want_rec = img[i], rec[i * S]
+                    if k == 0:
+                        hi_want = (want_img, want_rec)
+                    else:
+                        lo_want = (want_img, want_rec)
+        assert abs(float(best[0]) - ref_best[0]) < 1e-6 and abs(float(best[1]) - ref_best[1]) < 1e-6
+        assert tuple(at.tolist()) == (*ref_at[0], *ref_at[1])
+        torch.testing.assert_close(hi_img.cpu(), hi_want[0]); torch.testing.assert_close(hi_rec.cpu(), hi_want[1])
+        torch.testing.assert_close(lo_img.cpu(), lo_want[0]); torch.testing.assert_close(lo_rec.cpu(), lo_want[1])
