@@ -203,28 +203,69 @@ def time_kernels(plan, reps=20):
     return res
 
 
-# device symbols of the ABI calls with a kernel of their own (profiles/*pmc*.json is keyed by symbol)
-KERNEL_SYMBOL = {"vae_head_bwd": "head_bwd_mfma", "vae_head_fwd": "head_fwd_mfma", "vae_elbo_fwd": "elbo_kernel"}
+# device kernels each ABI call of the VanillaVAE step launches (profiles/*pmc*.json and the
+# rocprofv3 kernel_stats CSVs are keyed by kernel symbol; a call is timed as a whole)
+KERNEL_SYMBOLS = {"vae_head_bwd": ["head_bwd_mfma", "reduce_rows_kernel"], "vae_head_fwd": ["head_fwd_mfma"],
+                  "vae_elbo_fwd": ["elbo_kernel"],
+                  "vae_convT2d_bwd": ["hires_convT_bwd_kernel", "hires_slab_reduce"],
+                  "vae_conv_bwd_filter_batch": ["wg_group_kernel", "wg_slab_reduce"],
+                  "vae_convT2d_fwd": ["hires_convT_fwd_kernel", "cgemm_kernel"],
+                  "vae_conv2d_fwd": ["cgemm_kernel"], "vae_conv2d_bwd_data": ["cgemm_kernel"],
+                  "vae_convT2d_bwd_data": ["cgemm_kernel"]}
 
 
-def pmc_traffic(kernel_symbol_hint: str):
-    """HBM bytes per launch of the dominant kernel from profiles/*pmc*.json (tools/pmc_traffic.py),
-    corrected per MI355X_MICROARCH.md §HBM (FETCH_SIZE x2).  None when not collected."""
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")), reverse=True):
+def _profiles(pattern, arch):
+    """profiles/ files of this arch (VQ-VAE / wide-AE runs carry "vq" / "ae_big" in the name),
+    newest round/version first (natural order of the r<round>_v<version> prefix)."""
+    import re
+    tag = {"vq": "vq", "ae_big": "ae_big"}.get(arch)
+    paths = [p for p in glob.glob(os.path.join(REPO, "profiles", pattern))
+             if (tag in os.path.basename(p) if tag else not re.search(r"vq|ae_big", os.path.basename(p)))]
+    key = lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))]
+    return sorted(paths, key=key, reverse=True)
+
+
+def pmc_traffic(symbols, arch="vanilla"):
+    """HBM bytes per launch of a call's kernels from the newest profiles/*pmc*.json holding them
+    (tools/pmc_summary.py; FETCH_SIZE x2 per MI355X_MICROARCH.md §HBM), with the file and the git
+    HEAD it was measured at.  None when not collected for these kernels."""
+    for path in _profiles("*pmc*.json", arch):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        for k, v in d.get("kernels", {}).items():
-            if kernel_symbol_hint in k:
-                return v.get("hbm_bytes_per_launch")
+        got = {k: v.get("hbm_bytes_per_launch") for k, v in d.get("kernels", {}).items()
+               if any(sym in k for sym in symbols)}
+        if got:
+            return {"bytes_per_launch": got, "file": os.path.relpath(path, REPO), "head": d.get("head")}
+    return None
+
+
+def rocprof_times(symbols, arch="vanilla"):
+    """Average duration (us) of a call's kernels in the newest committed rocprofv3 kernel_stats CSV
+    that holds them (file named in the result): the kernels' own time next to the call's."""
+    import csv
+    for path in _profiles("*kernel_stats.csv", arch):
+        try:
+            rows = list(csv.DictReader(open(path)))
+        except Exception:
+            continue
+        got = {r["Name"][:120]: round(float(r["AverageNs"]) / 1e3, 2) for r in rows
+               if any(sym in r["Name"] for sym in symbols)}
+        if got:
+            return {"avg_us": got, "file": os.path.relpath(path, REPO)}
     return None
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def cpu_baseline(batch, seconds, arch="vanilla"):
-    """The oracle's fp32 step (fwd + loss + bwd + Adam) on the host cores, bounded sample."""
+def cpu_baseline(batch, seconds, arch="vanilla", threads=None):
+    """The oracle's fp32 step (fwd + loss + bwd + Adam) on the host cores, bounded sample.
+    threads: torch intra-op threads (default: torch's own, i.e. OMP_NUM_THREADS — the box's CPU
+    share for one GPU, 16; os.cpu_count() reports the whole machine there)."""
     from oracle import vae_oracle as O
+    prev = torch.get_num_threads()
+    if threads:
+        torch.set_num_threads(threads)
     threads = torch.get_num_threads()
     vq = arch == "vq"
     sd = O.make_params(O.vq_param_spec() if vq else O.vanilla_param_spec(), 1265)
@@ -264,6 +305,7 @@ def cpu_baseline(batch, seconds, arch="vanilla"):
         if el >= seconds or n >= 200:
             break
     name = "VQVAE" if vq else "VanillaVAE"
+    torch.set_num_threads(prev)
     return {"value": round(n * batch / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle {name} fp32 train step (fwd+loss+bwd+Adam), B={batch}, {n} steps / {el:.1f}s "
                       f"on {threads} threads ({os.cpu_count()} visible CPUs)"}
@@ -458,9 +500,13 @@ def main():
     else:
         roof = {"bound": "hbm", "achieved": round(by / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    roof["traffic"] = pmc_traffic(KERNEL_SYMBOL[fn]) if fn in KERNEL_SYMBOL else None
-    roof["kernel"] = f"{fn} (launch #{idx} of the step)"
+    syms = KERNEL_SYMBOLS.get(fn, [])
+    tr = pmc_traffic(syms, args.arch) if syms else None
+    roof["traffic"] = (sum(v for v in tr["bytes_per_launch"].values() if v) if tr else None)
+    roof["traffic_source"] = tr
+    roof["kernel"] = f"{fn} (call #{idx} of the step; its kernels: {', '.join(syms) or 'n/a'})"
     roof["us_per_launch"] = round(us, 2)
+    roof["rocprof"] = rocprof_times(syms, args.arch) if syms else None
     roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}
     step_kernel_us = sum(r[0] for r in rows)
     # the step-level attainable time — every kernel at its own roofline bound,
@@ -469,9 +515,10 @@ def main():
     attain_us = sum(max(fl_ / (peak_tf * 1e6), by_ / (HBM_PEAK_GBS * 1e3)) for _, _, fl_, by_ in rows)
     step_flops = sum(r[2] for r in rows)
 
-    cpu = None
+    cpu = cpu1 = None
     if not args.no_cpu_baseline and world == 1:     # the CPU baseline is an N=1 figure (rank 0)
         cpu = cpu_baseline(args.batch, args.cpu_seconds, args.arch)
+        cpu1 = cpu_baseline(args.batch, args.cpu_seconds * 0.6, args.arch, threads=1)
 
     ms = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
@@ -511,6 +558,7 @@ def main():
         "dropin": dropin,
         "dropin_eager": dropin_eager,
         "cpu_baseline": cpu,
+        "cpu_baseline_1thread": cpu1,
     }
     print(json.dumps(line), flush=True)
     if distributed:

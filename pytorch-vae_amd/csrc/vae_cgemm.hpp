@@ -274,6 +274,45 @@ cgemm_kernel(const GemmParams p) {
     // were requested together); ring mode: every slot, so vmcnt stays exact across the loop
     if (!OR || kt0 + u < kt1) issue(kt0 + u, ring[u]);
   }
+  // The epilogue's own loads (the stored pre-activation / residual of the output rows, the bias)
+  // go out now, behind the ring: the output tile is known from the start, and issued after the
+  // K loop they were one more memory round trip on every workgroup's critical path.
+  constexpr int EC = BN / 8, ERS = 256 / EC;
+  constexpr int EPT = (BM + ERS - 1) / ERS;
+  const int ec = tid % EC, er0 = tid / EC;
+  const int col = n0 + ec * 8;
+  const bool col_ok = col < p.N;                     // host: N % 8 == 0
+  uint32_t aux[EPT][4], res[EPT][4];
+  int obase[EPT];
+  bool rok[EPT];
+  float bias[8];
+  const bool has_res = p.residual != nullptr;
+  // (the 128-row tiles keep them after the loop: 8 rows x 2 operands per thread would stay live
+  // across it, 64 VGPRs under their two-workgroups-per-CU cap; so do the tiles capped at three
+  // workgroups per CU, which would spill)
+  constexpr bool EARLY = EPT <= 2 && cg_waves_per_eu<BM, BN, XA>() < 3;
+  auto epi_loads = [&]() {
+    const rsrc_t raux = epi_aux_rsrc<EM>(p);
+    const rsrc_t rres = epi_res_rsrc<EM>(p);
+    const bool loads = p.slab == nullptr;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int rl = er0 + i * ERS, row = m0 + rl;
+      rok[i] = rl < BM && row < p.M && col_ok;
+      obase[i] = out_row_base(p, phase, rok[i] ? row : 0) + col;
+      const uint32_t off = (rok[i] && loads) ? (uint32_t)obase[i] * 2u : kOOB;
+      bload<16>(raux, off, aux[i]);
+      if (EM == E_BNBWD && has_res) bload<16>(rres, off, res[i]);
+      else res[i][0] = res[i][1] = res[i][2] = res[i][3] = 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bias[e] = 0.f;
+    if (EM == E_STORE && p.bias && col_ok && loads) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bias[e] = p.bias[col + e];     // (parameter slices are 4-B aligned only)
+    }
+  };
+  if constexpr (EARLY) epi_loads();
   if (a_tab) {
     const int C = p.a_xf.channels;
 #pragma unroll
@@ -416,12 +455,7 @@ cgemm_kernel(const GemmParams p) {
         for (int e = 0; e < 4; ++e) Cs[(rq + i * 16 + e) * LDC + cq + j * 16] = acc[i][j][e];
   }
   __syncthreads();
-  // thread -> 8 consecutive columns of rows er0, er0 + ERS, ...
-  constexpr int EC = BN / 8, ERS = 256 / EC;
-  constexpr int EPT = (BM + ERS - 1) / ERS;
-  const int ec = tid % EC, er0 = tid / EC;
-  const int col = n0 + ec * 8;
-  const bool col_ok = col < p.N;                     // host: N % 8 == 0
+  // thread -> 8 consecutive columns of rows er0, er0 + ERS, ... (loads issued in the prologue)
   if (p.slab) {
     float* sl = p.slab + ((long)(phase * p.ksplit + ks) * p.M) * p.N;
 #pragma unroll
@@ -436,31 +470,8 @@ cgemm_kernel(const GemmParams p) {
     }
     return;
   }
-  // pass 1: every load (aux / residual / bias) before any store
-  const rsrc_t raux = epi_aux_rsrc<EM>(p);
-  const rsrc_t rres = epi_res_rsrc<EM>(p);
-  const bool has_res = p.residual != nullptr;
-  uint32_t aux[EPT][4], res[EPT][4];
-  int obase[EPT];
-  bool rok[EPT];
-#pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int rl = er0 + i * ERS, row = m0 + rl;
-    rok[i] = rl < BM && row < p.M && col_ok;
-    obase[i] = out_row_base(p, phase, rok[i] ? row : 0) + col;
-    const uint32_t off = rok[i] ? (uint32_t)obase[i] * 2u : kOOB;
-    bload<16>(raux, off, aux[i]);
-    if (EM == E_BNBWD && has_res) bload<16>(rres, off, res[i]);
-    else res[i][0] = res[i][1] = res[i][2] = res[i][3] = 0u;
-  }
-  float bias[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bias[e] = 0.f;
-  if (EM == E_STORE && p.bias && col_ok) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bias[e] = p.bias[col + e];     // (parameter slices are 4-B aligned only)
-  }
-  // pass 2: apply (outputs stay in registers), per-column sums -> this block's flush, then the
+  if constexpr (!EARLY) epi_loads();
+  // apply (outputs stay in registers), per-column sums -> this block's flush, then the
   // stores: nothing waits on the stores (a barrier behind them would drain them: vmcnt(0))
   float s1[8], s2[8];
 #pragma unroll

@@ -156,7 +156,13 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   // each takes its share of one round of workgroups (one per CU), in proportion to its MACs:
   // fewer slices, and a single slice accumulates with plain stores (WgParams.own).
   static const int group_slots = tune_env("VAE_WG_GROUP_SLOTS", kCUs);
-  for (int c = 1; c < kClasses; ++c) {
+  // the 32 x 32 all-taps class (wide, few-channel layers: thousands of pixels per dW element)
+  // gets its own round (measured, VanillaVAE B=64: 0 = each layer's standalone split 127 us for
+  // the batch, 256 -> 103 us, 512 -> 107, 768 -> 126); VAE_WG_GROUP_SLOTS0=0 keeps the
+  // standalone plans
+  static const int group_slots0 = tune_env("VAE_WG_GROUP_SLOTS0", kCUs);
+  for (int c = group_slots0 > 0 ? 0 : 1; c < kClasses; ++c) {
+    const int gs = c == 0 ? group_slots0 : group_slots;
     double macs = 0.0;
     for (int i = 0; i < n; ++i)
       if (cls[i] == c) macs += (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
@@ -164,7 +170,7 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
     for (int i = 0; i < n; ++i) {
       if (cls[i] != c) continue;
       const double m = (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
-      long slots = (long)(group_slots * m / macs + 0.5);
+      long slots = (long)(gs * m / macs + 0.5);
       if (slots < 1) slots = 1;
       WgParams w = plans[i].p;
       w.slab = nullptr;

@@ -114,10 +114,12 @@ def allreduce_mean(t: torch.Tensor, group=None, async_op: bool = False):
     return None
 
 
-def broadcast_buffers(running: torch.Tensor, group=None):
-    """DDP broadcast_buffers=True: every rank takes rank 0's BatchNorm running statistics."""
+def broadcast_buffers(running: torch.Tensor, group=None, async_op: bool = False):
+    """DDP broadcast_buffers=True: every rank takes rank 0's BatchNorm running statistics.
+    async_op: returns the work handle (the caller waits before the next forward reads them —
+    on RCCL a stream-ordered wait, so the optimizer step runs meanwhile)."""
     src = dist.get_global_rank(group, 0) if group is not None else 0
-    dist.broadcast(running, src=src, group=group)
+    return dist.broadcast(running, src=src, group=group, async_op=async_op)
 
 
 class BucketedAllReduce:

@@ -144,13 +144,18 @@ class TrainStep:
                 self._segment(k)
             if self.comm is not None:
                 self.comm.launch(k)
+        bcast = None
         if self.comm is not None:
             self.comm.wait()
-            broadcast_buffers(self.net.running, self.pg)
+            # rank 0's BatchNorm running statistics, off the critical path: the broadcast runs on
+            # the communication stream while the optimizer step (which does not read them) runs
+            bcast = broadcast_buffers(self.net.running, self.pg, async_op=True)
         if self.use_graph:
             self.g_opt.replay()
         else:
             self._opt()
+        if bcast is not None:
+            bcast.wait()                 # before the next step's forward updates them
         self.net.num_batches_tracked += 1
 
     def loss_terms(self):

@@ -74,6 +74,18 @@ def _worker(rank, world, port, q):
         err = float((mine - want).abs().max() / want.abs().max())
         assert err < 1e-6, err
         assert torch.equal(run, run0)
+        # the step's asynchronous form (engine.TrainStep): each rank's forward moved its own
+        # statistics, the broadcast runs beside other work, and after the wait every rank holds
+        # rank 0's — two steps in a row
+        for step in range(2):
+            run.add_(float(rank + 1) * (step + 1))
+            ref = run.clone()
+            dist.broadcast(ref, src=0)                 # what rank 0 holds now
+            work = broadcast_buffers(run, async_op=True)
+            other = torch.ones(1000).cumsum(0)         # the optimizer step's stand-in
+            work.wait()
+            assert torch.equal(run, ref), step
+            assert float(other[-1]) == 1000.0
         q.put((rank, "ok"))
     except Exception as e:  # report to the parent
         import traceback

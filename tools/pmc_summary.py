@@ -75,7 +75,13 @@ def main():
         for name in ("GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"):
             if name in c:
                 tot[name] += sum(c[name])
-    summary = {"config": args.config, "sources": args.dirs,
+    import subprocess
+    try:
+        head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                              cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
+    except Exception:
+        head = None
+    summary = {"config": args.config, "sources": args.dirs, "head": head,
                "all_vae_dispatches_mfma_busy": (round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] /
                                                      (tot["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
                                                if tot["GRBM_GUI_ACTIVE"] else None),
