@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 12
+#define VAE_ABI_VERSION 13
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -413,6 +413,81 @@ typedef struct vae_record_args {
 int vae_step_record(const vae_record_args* a, void* stream);
 /* --- start of a training step: zero `bytes` at `zero` and ++*step ------------------ */
 int vae_step_begin(void* zero, int64_t bytes, int32_t* step, void* stream);
+
+/* --- start of a training step in ONE launch: what vae_step_begin, vae_nchw_to_nhwc_pad and up to
+ *     VAE_PAD_MAX vae_pad_channels calls do (the zero region and ++*step, the RGB image as 8
+ *     zero-padded NHWC channels, the padded first-layer weight copies), as block ranges of one grid.
+ *     Replaces the three dependent launches at the head of every step (experiment.py:45-49 → the
+ *     inputs of models/vanilla_vae.py:84; 16.5 us of launches in profiles/r3a). ---------------- */
+#define VAE_PAD_MAX 4
+typedef struct vae_pad_desc {
+  int64_t rows;
+  int32_t c, cp;                     /* dst[r][j] = j < c ? src[r][j] : 0, j < cp */
+  const void* src;                   /* dtype (the step's weight copies) */
+  void* dst;
+} vae_pad_desc;
+typedef struct vae_step_begin_args {
+  void* zero;                        /* 16-B aligned; bytes may be 0 */
+  int64_t bytes;
+  int32_t* step;                     /* ++ once, or NULL */
+  int32_t dtype;                     /* of the padded image and the pad descriptors */
+  int32_t n, c, h, w, cp;            /* image: fp32 NCHW x -> NHWC y with cp channels (x NULL: none) */
+  const float* x;
+  void* y;
+  int32_t npad;
+  vae_pad_desc pad[VAE_PAD_MAX];
+} vae_step_begin_args;
+int vae_step_begin_ex(const vae_step_begin_args* a, void* stream);
+
+/* --- the VAE bottleneck, bf16, as two launches each way (VanillaVAE / BetaVAE / IWAE training):
+ *   vae_latent_fc_fwd   mulv += act(x)·W1^T (+ b1)      fc_mu|fc_var (vanilla_vae.py:36-37, :89-90).
+ *                       x: the last encoder map, stored pre-BatchNorm, NHWC [batch][in_features];
+ *                       x_xf its BatchNorm+LeakyReLU (running statistics updated when set).  K is
+ *                       split over workgroups that add with fp32 atomics: mulv must be ZERO on entry
+ *                       (the step's zero region).  Replaces vae_linear_fwd + its split-K finalize.
+ *   vae_latent_dec_fwd  z = mu + eps*exp(logvar/2)       reparameterize (vanilla_vae.py:107-117; row
+ *                       r of z uses mu row r/samples), z written bf16 [batch*samples][latent], and
+ *                       h = z·W2^T + b2                  decoder_input (vanilla_vae.py:43, :101), bf16
+ *                       [batch*samples][out_features] — one launch for vae_reparam_fwd +
+ *                       vae_linear_fwd.  eps NULL: z is an input (decode of a given z).
+ *   vae_latent_dec_bwd  d[mu|logvar] += the reparameterization backward of dz = dh·W2 plus the KL
+ *                       seed kl_coef (as vae_linear_bwd_data with mulv set; dmulv accumulated, zero on
+ *                       entry), dW2 += dh^T·z, db2 += sum_r dh — one launch for the decoder_input
+ *                       bwd_data (+ finalize) and bwd_filter.
+ *   vae_latent_fc_bwd   dx = dx_epi-backward(dmulv·W1) of x (BatchNorm+LeakyReLU backward; sums
+ *                       Sg -> dx_dbeta, Sg*xhat -> dx_dgamma replicas, as vae_linear_bwd_data),
+ *                       dW1 += dmulv^T·act(x), db1 += sum_r dmulv — one launch for fc bwd_data and
+ *                       bwd_filter.
+ * Shapes: latent % 32 == 0, latent <= 256; x_xf.channels % 128 == 0 and in_features a multiple of
+ * it; out_features % 64 == 0; weights native ([2*latent][in_features], [out_features][latent]). */
+typedef struct vae_latent_args {
+  int32_t dtype;                     /* VAE_BF16 */
+  int32_t batch, samples, latent;
+  int32_t in_features, out_features;
+  const void* x;                     /* [batch][in_features] bf16, stored pre-activation */
+  vae_xform x_xf;                    /* BN_ACT (the encoder's last BatchNorm+LeakyReLU) */
+  const void* w1;                    /* fc_mu|fc_var [2*latent][in_features] bf16 */
+  const float* b1;
+  float* mulv;                       /* [batch][2*latent] fp32, accumulated */
+  const float* eps;                  /* [batch*samples][latent] or NULL */
+  void* z;                           /* [batch*samples][latent] bf16 (out, or in when eps NULL) */
+  const void* w2;                    /* decoder_input [out_features][latent] bf16 */
+  const float* b2;
+  void* h;                           /* [batch*samples][out_features] bf16 */
+  const void* dh;                    /* backward: dL/dh [batch*samples][out_features] bf16 */
+  const float* kl_coef;              /* [batch*samples] or NULL */
+  float* dmulv;                      /* [batch][2*latent], accumulated */
+  float* dw2; float* db2;            /* fp32, accumulated */
+  void* dx;                          /* [batch][in_features] bf16: gradient w.r.t. x's BN output */
+  vae_xform dx_epi;                  /* BN_ACT of x, aux = x */
+  float* dx_dgamma; float* dx_dbeta;
+  int32_t sum_reps, sum_rstride;
+  float* dw1; float* db1;            /* fp32, accumulated */
+} vae_latent_args;
+int vae_latent_fc_fwd(const vae_latent_args* a, void* stream);
+int vae_latent_dec_fwd(const vae_latent_args* a, void* stream);
+int vae_latent_dec_bwd(const vae_latent_args* a, void* stream);
+int vae_latent_fc_bwd(const vae_latent_args* a, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,104 @@
+// vae_step_begin_ex: the head of a training step as ONE launch (vaehip.h).  Three kinds of work that
+// do not depend on each other share the grid as block ranges:
+//   [0, nz)            zero the step's zero region (gradients, BatchNorm sums, SSE, d[mu|logvar]) and
+//                      ++*step — vae_step_begin
+//   [nz, nz + nx)      the fp32 NCHW image -> NHWC with cp channels (zeros above c), one pixel per
+//                      thread, one 16-byte store per pixel for bf16 / cp = 8 — vae_nchw_to_nhwc_pad
+//   [nz + nx, ...)     up to VAE_PAD_MAX padded weight copies — vae_pad_channels
+// The reference's step (experiment.py:45-49) feeds the image straight into the first Conv2d
+// (models/vanilla_vae.py:84); the padding exists only so that the first layer runs on the packed
+// 16-byte GEMM operand path.  profiles/r3a: the three separate launches took 6.5 + 5.2 + 4.8 us.
+#include "vae_common.hpp"
+
+namespace vae {
+namespace {
+
+struct StepBegin {
+  vae_step_begin_args a;
+  long n16;              // 16-byte words to zero
+  int ntail;             // bytes after them
+  int nz, nx;            // blocks of the zeroing and of the image ranges
+  int pad0[VAE_PAD_MAX + 1];   // first block of each pad descriptor (relative to nz + nx)
+};
+
+template <class T>
+__device__ __forceinline__ void image_pixel(const vae_step_begin_args& a, long pix) {
+  const long hw = (long)a.h * a.w;
+  const long img = pix / hw, sp = pix - img * hw;
+  const float* src = a.x + img * a.c * hw + sp;
+  T* dst = static_cast<T*>(a.y) + pix * a.cp;
+  if constexpr (sizeof(T) == 2) {
+    if (a.cp == 8) {                       // the packed RGB case: one 16-byte store
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (__bf16)(j < a.c ? src[j * hw] : 0.f);
+      *reinterpret_cast<bf16x8*>(dst) = o;
+      return;
+    }
+  }
+  for (int j = 0; j < a.cp; ++j) dst[j] = cvt<T>(j < a.c ? src[j * hw] : 0.f);
+}
+
+template <class T>
+__global__ void __launch_bounds__(256) step_begin_ex_kernel(const StepBegin s) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (b < s.nz) {
+    f32x4* z = static_cast<f32x4*>(s.a.zero);
+    for (long i = (long)b * 256 + tid; i < s.n16; i += (long)s.nz * 256) z[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (b == 0 && tid < s.ntail) reinterpret_cast<unsigned char*>(z + s.n16)[tid] = 0;
+    if (b == 0 && tid == 0 && s.a.step) *s.a.step += 1;
+    return;
+  }
+  if (b < s.nz + s.nx) {
+    const long pix = (long)(b - s.nz) * 256 + tid;
+    if (pix < (long)s.a.n * s.a.h * s.a.w) image_pixel<T>(s.a, pix);
+    return;
+  }
+  const int pb = b - s.nz - s.nx;
+  int k = 0;
+  while (k + 1 < s.a.npad && pb >= s.pad0[k + 1]) ++k;
+  const vae_pad_desc& d = s.a.pad[k];
+  const long i = (long)(pb - s.pad0[k]) * 256 + tid;
+  if (i >= d.rows * d.cp) return;
+  const long r = i / d.cp;
+  const int j = (int)(i - r * d.cp);
+  static_cast<T*>(d.dst)[i] = j < d.c ? static_cast<const T*>(d.src)[r * d.c + j] : cvt<T>(0.f);
+}
+
+}  // namespace
+}  // namespace vae
+
+using namespace vae;
+
+extern "C" int vae_step_begin_ex(const vae_step_begin_args* a, void* stream) {
+  if (!a || a->bytes < 0 || (a->bytes > 0 && !a->zero)) return fail(VAE_E_BADARG, "step_begin_ex: zero region");
+  if (((uintptr_t)a->zero & 15) != 0) return fail(VAE_E_BADARG, "step_begin_ex: zero region must be 16-B aligned");
+  if (a->dtype != VAE_F32 && a->dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "step_begin_ex: dtype");
+  if (a->npad < 0 || a->npad > VAE_PAD_MAX) return fail(VAE_E_BADARG, "step_begin_ex: %d pads", a->npad);
+  StepBegin s;
+  s.a = *a;
+  s.n16 = a->bytes / 16;
+  s.ntail = (int)(a->bytes - s.n16 * 16);
+  long zb = (s.n16 + 255) / 256;
+  s.nz = (int)(zb < 1 ? 1 : (zb > 2048 ? 2048 : zb));
+  s.nx = 0;
+  if (a->x) {
+    if (!a->y || a->n <= 0 || a->c <= 0 || a->h <= 0 || a->w <= 0 || a->cp < a->c)
+      return fail(VAE_E_BADARG, "step_begin_ex: image args");
+    if (a->dtype == VAE_BF16 && a->cp == 8 && ((uintptr_t)a->y & 15) != 0)
+      return fail(VAE_E_BADARG, "step_begin_ex: padded image must be 16-B aligned");
+    s.nx = (int)(((long)a->n * a->h * a->w + 255) / 256);
+  }
+  int nb = 0;
+  for (int k = 0; k < a->npad; ++k) {
+    const vae_pad_desc& d = a->pad[k];
+    if (!d.src || !d.dst || d.rows <= 0 || d.c <= 0 || d.cp < d.c) return fail(VAE_E_BADARG, "step_begin_ex: pad %d", k);
+    s.pad0[k] = nb;
+    nb += (int)((d.rows * d.cp + 255) / 256);
+  }
+  s.pad0[a->npad] = nb;
+  const dim3 grid((unsigned)(s.nz + s.nx + nb));
+  if (a->dtype == VAE_BF16) VAE_LAUNCH(step_begin_ex_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, s);
+  else VAE_LAUNCH(step_begin_ex_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, s);
+  return check_launch("step_begin_ex");
+}

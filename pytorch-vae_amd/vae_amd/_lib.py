@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -112,6 +112,27 @@ class SwapDesc(ctypes.Structure):
 
 
 SWAP_MAX = 16
+PAD_MAX = 4
+
+
+class PadDesc(ctypes.Structure):
+    _fields_ = [("rows", c_int64), ("c", c_int32), ("cp", c_int32), ("src", c_void_p), ("dst", c_void_p)]
+
+
+class StepBeginArgs(ctypes.Structure):
+    _fields_ = [("zero", c_void_p), ("bytes", c_int64), ("step", c_void_p), ("dtype", c_int32),
+                ("n", c_int32), ("c", c_int32), ("h", c_int32), ("w", c_int32), ("cp", c_int32),
+                ("x", c_void_p), ("y", c_void_p), ("npad", c_int32), ("pad", PadDesc * PAD_MAX)]
+
+
+class LatentArgs(ctypes.Structure):
+    _fields_ = [("dtype", c_int32), ("batch", c_int32), ("samples", c_int32), ("latent", c_int32),
+                ("in_features", c_int32), ("out_features", c_int32),
+                ("x", c_void_p), ("x_xf", Xform), ("w1", c_void_p), ("b1", c_void_p), ("mulv", c_void_p),
+                ("eps", c_void_p), ("z", c_void_p), ("w2", c_void_p), ("b2", c_void_p), ("h", c_void_p),
+                ("dh", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p), ("dw2", c_void_p), ("db2", c_void_p),
+                ("dx", c_void_p), ("dx_epi", Xform), ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p),
+                ("sum_reps", c_int32), ("sum_rstride", c_int32), ("dw1", c_void_p), ("db1", c_void_p)]
 
 # name -> (argtypes)
 _SIGS = {
@@ -153,6 +174,11 @@ _SIGS = {
     "vae_head_workspace_size": [POINTER(HeadArgs), c_int32, POINTER(ctypes.c_size_t)],
     "vae_conv_bwd_filter_batch": [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "vae_conv_bwd_filter_batch_workspace_size": [c_int32, c_void_p, c_void_p, POINTER(ctypes.c_size_t)],
+    "vae_step_begin_ex": [POINTER(StepBeginArgs), c_void_p],
+    "vae_latent_fc_fwd": [POINTER(LatentArgs), c_void_p],
+    "vae_latent_dec_fwd": [POINTER(LatentArgs), c_void_p],
+    "vae_latent_dec_bwd": [POINTER(LatentArgs), c_void_p],
+    "vae_latent_fc_bwd": [POINTER(LatentArgs), c_void_p],
 }
 EXPORTED = tuple(_SIGS)
 

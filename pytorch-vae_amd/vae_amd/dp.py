@@ -21,7 +21,7 @@ import torch
 import torch.distributed as dist
 
 # fields of the argument structs that point into the gradient buffer
-_GRAD_FIELDS = ("dw", "db", "dcodebook")
+_GRAD_FIELDS = ("dw", "db", "dcodebook", "dw1", "db1", "dw2", "db2")
 _XF_GRAD_FIELDS = ("dgamma_out", "dbeta_out")
 
 

@@ -9,6 +9,7 @@ buffer with RCCL between the backward graph and the optimizer graph.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -45,6 +46,30 @@ class FusedAdam:
                stream if stream is not None else L.stream_ptr())
         if getattr(net, "swap_descs", None) is not None:
             net.refresh_swaps(stream)
+
+
+PAD_FNS = ("vae_nchw_to_nhwc_pad", "vae_pad_channels")
+
+
+def begin_args(plan, step: torch.Tensor):
+    """vae_step_begin_ex arguments for a plan: its zero region and the step counter, plus the image
+    and weight padding calls that head its forward list (they run inside the same launch).
+    Returns (args, number of leading forward calls it replaces)."""
+    a = L.StepBeginArgs(zero=plan.zero.data_ptr(), bytes=plan.zero.numel() * 4, step=step.data_ptr(),
+                        dtype=plan.net.dcode)
+    k = npad = 0
+    for fn, arg in plan.fwd_calls:
+        if fn == "vae_nchw_to_nhwc_pad" and not a.x:
+            a.dtype, a.n, a.c, a.h, a.w, a.cp, a.x, a.y = arg
+        elif fn == "vae_pad_channels" and npad < L.PAD_MAX and arg[0] == a.dtype:
+            _, rows, c, cp, src, dst = arg
+            a.pad[npad] = L.PadDesc(rows=rows, c=c, cp=cp, src=src, dst=dst)
+            npad += 1
+        else:
+            break
+        k += 1
+    a.npad = npad
+    return a, k
 
 
 class TrainStep:
@@ -84,6 +109,9 @@ class TrainStep:
         self.graphs = []
         self.g_opt: Optional[torch.cuda.CUDAGraph] = None
         self.stream = torch.cuda.Stream(device=net.device)
+        # the step's head (zeroing, step count, image and weight padding) as one launch;
+        # VAE_NO_BEGIN_EX=1 keeps vae_step_begin + the padding calls (A/B timing)
+        self._begin = None if os.environ.get("VAE_NO_BEGIN_EX") else begin_args(plan, opt.step)
 
     # -------------------------------------------------------------- eager pieces
     def _segment(self, k: int):
@@ -91,10 +119,15 @@ class TrainStep:
         p = self.plan
         st = L.stream_ptr()
         if k == 0:
-            L.call("vae_step_begin", p.zero.data_ptr(), p.zero.numel() * 4, self.opt.step.data_ptr(), st)
+            skip = 0
+            if self._begin is not None:
+                args, skip = self._begin
+                L.call("vae_step_begin_ex", args, st)
+            else:
+                L.call("vae_step_begin", p.zero.data_ptr(), p.zero.numel() * 4, self.opt.step.data_ptr(), st)
             if p.loss_kind == L.LOSS_BETA_B:
                 p.num_iter.add_(1.0)
-            p.forward(st)
+            p._run(p.fwd_calls[skip:], st)
             if self.world > 1:
                 p.metrics.copy_(p.out)
         lo = 0 if k == 0 else self.buckets[k - 1][0]
@@ -120,6 +153,18 @@ class TrainStep:
         self.opt.v.copy_(state[3]); self.opt.step.copy_(state[4]); self.plan.num_iter.copy_(state[5])
         self.net.sync_lowp()
         self.graphs = []
+        if self.comm is None:
+            # one rank: the whole step (forward, backward and the optimizer) is one graph, one
+            # launch from the host — two graphs per step left an ~8.7 us gap between them
+            # (profiles/r3a: the replay of the optimizer graph behind the backward graph)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self._segment(0)
+                self._opt()
+            self.graphs.append(g)
+            self.g_opt = None
+            torch.cuda.synchronize()
+            return
         for k in range(len(self.buckets)):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
@@ -151,7 +196,8 @@ class TrainStep:
             # the communication stream while the optimizer step (which does not read them) runs
             bcast = broadcast_buffers(self.net.running, self.pg, async_op=True)
         if self.use_graph:
-            self.g_opt.replay()
+            if self.g_opt is not None:
+                self.g_opt.replay()
         else:
             self._opt()
         if bcast is not None:

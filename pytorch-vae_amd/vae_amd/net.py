@@ -156,6 +156,14 @@ class StepPlan:
         dev, T = net.device, net.dtype
         D, h, img = net.latent_dim, net.hidden_dims, net.img_size
         B, BS = self.B, self.B * self.S
+        # latent: the bottleneck (fc_mu|fc_var, reparameterize, decoder_input and their backward) on
+        # the vae_latent_* kernels — two launches each way instead of nine (vaehip.h).  bf16 training
+        # plans with the fused loss (the TrainStep engine) and the shapes those kernels take;
+        # VAE_NO_LATENT=1 keeps the per-op calls (A/B timing).
+        C5, r0 = net.hidden_dims[-1], net.hidden_dims[::-1][0]
+        self.latent_fused = (T == torch.bfloat16 and training and fused_loss and net.latent_dim in (64, 128)
+                             and C5 % 128 == 0 and (4 * r0) % 128 == 0 and net.img_size == 64
+                             and not os.environ.get("VAE_NO_LATENT"))
         self._keep = []            # ctypes structs referenced by the call lists
 
         # -------- buffers
@@ -200,7 +208,7 @@ class StepPlan:
         # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
         nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
         nz = (_pad4(net.layout.total) + 4 + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns)) +
-              _pad4(h[0] * 9 * 8))
+              _pad4(h[0] * 9 * 8) + (_pad4(B * 2 * D) if self.latent_fused else 0))
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += _pad4(net.layout.total)
@@ -217,6 +225,8 @@ class StepPlan:
         self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
         self.counters = self.zero[o:o + 2 * len(net.layout.bns)].view(torch.int32); o += _pad4(2 * len(net.layout.bns))
         self.dw8 = self.zero[o:o + h[0] * 9 * 8]; o += _pad4(h[0] * 9 * 8)       # padded first-conv dW
+        if self.latent_fused:       # vae_latent_fc_fwd accumulates mu|log_var: zero at every step
+            self.mulv = self.zero[o:o + B * 2 * D].view(B, 2 * D); o += _pad4(B * 2 * D)
         # per-BatchNorm coefficient tables, rewritten every step by vae_bn_finalize:
         # forward [4][C] (BN_ACT) then backward [3][C] (BN_DY)
         self.bntab: Dict[str, torch.Tensor] = {
@@ -421,6 +431,19 @@ class StepPlan:
             self.bn_finalize(F, enc_pre[i], fmode, cnt(self.enc[i]))
             sp //= 2
         # ---------------------------------------------------------------- fc_mu | fc_var
+        if self.latent_fused:
+            la = self._latent = L.LatentArgs(dtype=T, batch=B, samples=self.S, latent=D, in_features=4 * h[-1],
+                                              out_features=4 * r[0])
+            la.x = self.enc[-1].data_ptr()
+            la.x_xf = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), running=True)
+            la.w1, la.b1 = net.w("fc_mu.weight"), net.p("fc_mu.bias")
+            la.mulv, la.eps, la.z = self.mulv.data_ptr(), self.eps.data_ptr(), self.z.data_ptr()
+            la.w2, la.b2 = net.w("decoder_input.weight"), net.p("decoder_input.bias")
+            la.h = self.h0.data_ptr()
+            self._add(F, "vae_latent_fc_fwd", la)
+            self.n_encode = len(F)
+            self.n_decode0 = len(F)            # (decode() of a fused plan starts at the reparameterization)
+            F.append(("vae_latent_dec_fwd", F[-1][1]))
         a = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
         a.x = self.enc[-1].data_ptr()
         a.x_xf = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), running=True)
@@ -428,18 +451,19 @@ class StepPlan:
         a.bias = net.p("fc_mu.bias")
         a.y = self.mulv.data_ptr()
         a.y_f32 = 1
-        self._add(F, "vae_linear_fwd", a)
-        self.n_encode = len(F)                 # calls of encode(): encoder + fc_mu|fc_var
         self._reparam = (T, BS, self.S, D, self.mulv.data_ptr(), self.eps.data_ptr(), self.z.data_ptr())
-        F.append(("vae_reparam_fwd", self._reparam))
-        self.n_decode0 = len(F)                # decode(): decoder_input .. head
-        # ---------------------------------------------------------------- decoder_input
-        a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
-        a.x = self.z.data_ptr()
-        a.wt = net.w("decoder_input.weight")
-        a.bias = net.p("decoder_input.bias")
-        a.y = self.h0.data_ptr()
-        self._add(F, "vae_linear_fwd", a)
+        if not self.latent_fused:
+            self._add(F, "vae_linear_fwd", a)
+            self.n_encode = len(F)             # calls of encode(): encoder + fc_mu|fc_var
+            F.append(("vae_reparam_fwd", self._reparam))
+            self.n_decode0 = len(F)            # decode(): decoder_input .. head
+            # ------------------------------------------------------------ decoder_input
+            a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
+            a.x = self.z.data_ptr()
+            a.wt = net.w("decoder_input.weight")
+            a.bias = net.p("decoder_input.bias")
+            a.y = self.h0.data_ptr()
+            self._add(F, "vae_linear_fwd", a)
         # ---------------------------------------------------------------- decoder (ConvT)
         sp = 2
         prev, prev_pre = self.h0, None
@@ -543,6 +567,19 @@ class StepPlan:
             else:
                 self._add(Bw, "vae_convT2d_bwd_data", a)
                 self._add(Bw, "vae_convT2d_bwd_filter", f)
+        if self.latent_fused:
+            la = self._latent
+            la.dh, la.kl_coef, la.dmulv = self.g_h0.data_ptr(), self.kl_coef.data_ptr(), self.dmulv.data_ptr()
+            la.dw2, la.db2 = self.g("decoder_input.weight"), self.g("decoder_input.bias")
+            la.dx = self.g_enc[-1].data_ptr()
+            la.dx_epi = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), aux=self.enc[-1])
+            s = self.bnbwd[enc_pre[-1]]
+            la.dx_dgamma, la.dx_dbeta = s[0].data_ptr(), s[1].data_ptr()
+            la.sum_reps, la.sum_rstride = s.shape[1], s.shape[2]
+            la.dw1, la.db1 = self.g("fc_mu.weight"), self.g("fc_mu.bias")
+            Bw.append(("vae_latent_dec_bwd", F[self.n_encode - 1][1]))
+            Bw.append(("vae_latent_fc_bwd", F[self.n_encode - 1][1]))
+            self._reparam_bwd = None
         # decoder_input: dz -> d[mu|logvar] (reparameterization + KL), and its weight grads
         a = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
         a.dy = self.g_h0.data_ptr()
@@ -552,14 +589,16 @@ class StepPlan:
         a.kl_coef = self.kl_coef.data_ptr() if self.fused_loss else None
         a.dmulv = self.dmulv.data_ptr()
         a.samples = self.S
-        self._add(Bw, "vae_linear_bwd_data", a)
-        self._reparam_bwd = a
+        if not self.latent_fused:
+            self._add(Bw, "vae_linear_bwd_data", a)
+            self._reparam_bwd = a
         f = L.LinearArgs(dtype=T, m=BS, n=4 * r[0], k=D)
         f.dy = self.g_h0.data_ptr()
         f.x = self.z.data_ptr()
         f.dw = self.g("decoder_input.weight")
         f.db = self.g("decoder_input.bias")
-        self._add(Bw, "vae_linear_bwd_filter", f)
+        if not self.latent_fused:
+            self._add(Bw, "vae_linear_bwd_filter", f)
         # fc_mu | fc_var
         a = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
         a.dy = self.dmulv.data_ptr()
@@ -568,7 +607,8 @@ class StepPlan:
         a.dx = self.g_enc[-1].data_ptr()
         a.dx_epi = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]), aux=self.enc[-1])
         self.bwd_sums(a, enc_pre[-1])
-        self._add(Bw, "vae_linear_bwd_data", a)
+        if not self.latent_fused:
+            self._add(Bw, "vae_linear_bwd_data", a)
         f = L.LinearArgs(dtype=T, m=B, n=2 * D, k=4 * h[-1])
         f.dy = self.dmulv.data_ptr()
         f.dy_f32 = 1
@@ -576,7 +616,8 @@ class StepPlan:
         f.x_xf = self.bn_xf(enc_pre[-1], L.X_BN_ACT, cnt(self.enc[-1]))
         f.dw = self.g("fc_mu.weight")
         f.db = self.g("fc_mu.bias")
-        self._add(Bw, "vae_linear_bwd_filter", f)
+        if not self.latent_fused:
+            self._add(Bw, "vae_linear_bwd_filter", f)
         # encoder, last block first
         sps = [img // 2 ** i for i in range(nenc)]
         for i in reversed(range(nenc)):

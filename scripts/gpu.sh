@@ -10,6 +10,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench line (driver's command: N=1, CPU baseline included)
 #   quick            VanillaVAE bench, 200 steps, no CPU baseline, per-call breakdown
+#   qenv:V=x,W=y     the quick bench with environment overrides (tunable sweeps)
 #   arch:A:B         bench --arch A --batch B (betaH, iwae, vq, ae_big ...), no CPU baseline
 #   prof             rocprofv3 --kernel-trace --stats over a short VanillaVAE bench
 #   prof:A:B         the same for --arch A --batch B
@@ -58,6 +59,7 @@ for step in "$@"; do
     smoke) run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python3 -u bench.py ;;
     quick) run quick 300 python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --kernel-breakdown ;;
+    qenv) run qenv_${a1//[=,]/_} 300 env ${a1//,/ } python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-dropin ;;
     arch) run arch_${a1}_${a2} 300 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --no-cpu-baseline --kernel-breakdown ;;
     prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;
     pmc) if [ -n "$a1" ]; then pmc pmc_$a1 --arch $a1 --batch $a2; else pmc pmc; fi ;;
