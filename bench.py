@@ -46,6 +46,9 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "train images/sec (node) VanillaVAE 64×64 bs=64 at 1/2/4/8 GPU; ELBO match"
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # dense, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+# the fork's Autoencoder configs (models/autoencoder.py; hidden_dims of configs/*ae*.yaml)
+AE_WIDTHS = {"ae_big": [128, 256, 512, 1024, 2048], "ae_vbig": [256, 512, 1024, 2048, 4096],
+             "ae_vvbig": [512, 1024, 2048, 4096, 4096]}
 
 
 def parse():
@@ -57,8 +60,10 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in path leg (model.forward + "
                     "loss_function + backward + torch.optim.Adam through VAEXperiment.training_step)")
-    ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae", "vq"],
-                    help="vq: BASELINE.json configs[4], VQ-VAE B=128 (pass --batch 128)")
+    ap.add_argument("--arch", default="vanilla", choices=["vanilla", "betaH", "iwae", "vq"] + sorted(AE_WIDTHS),
+                    help="vq: BASELINE.json configs[4], VQ-VAE B=128 (pass --batch 128); ae_big / ae_vbig / "
+                         "ae_vvbig: the Autoencoder of configs/big_ae.yaml / patient_vbig_ae.yaml / "
+                         "patient_vvbig_ae.yaml (MSE, no KL)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--concurrent", choices=["auto", "on", "off"], default="auto",
                     help="weight gradients on a side stream beside the data-gradient chain; auto = on for "
@@ -218,9 +223,10 @@ def _profiles(pattern, arch):
     """profiles/ files of this arch (VQ-VAE / wide-AE runs carry "vq" / "ae_big" in the name),
     newest round/version first (natural order of the r<round>_v<version> prefix)."""
     import re
-    tag = {"vq": "vq", "ae_big": "ae_big"}.get(arch)
+    tag = arch if arch == "vq" or arch in AE_WIDTHS else None
     paths = [p for p in glob.glob(os.path.join(REPO, "profiles", pattern))
-             if (tag in os.path.basename(p) if tag else not re.search(r"vq|ae_big", os.path.basename(p)))]
+             if (re.search(tag + r"(_|\.|$)", os.path.basename(p)) if tag else
+                 not re.search(r"vq|ae_", os.path.basename(p)))]
     key = lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))]
     return sorted(paths, key=key, reverse=True)
 
@@ -268,7 +274,9 @@ def cpu_baseline(batch, seconds, arch="vanilla", threads=None):
         torch.set_num_threads(threads)
     threads = torch.get_num_threads()
     vq = arch == "vq"
-    sd = O.make_params(O.vq_param_spec() if vq else O.vanilla_param_spec(), 1265)
+    ae = AE_WIDTHS.get(arch)
+    sd = O.make_params(O.vq_param_spec() if vq else (O.ae_param_spec(hidden_dims=ae) if ae else O.vanilla_param_spec()),
+                       1265)
     P = {k: (v.clone().requires_grad_(True) if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))
              else v.clone()) for k, v in sd.items()}
     leaves = [v for v in P.values() if v.requires_grad]
@@ -283,6 +291,9 @@ def cpu_baseline(batch, seconds, arch="vanilla", threads=None):
             q, vq_loss, _, _ = O.vq_quantize(O.vq_encode(P, x, hd), P["vq_layer.embedding.weight"], 0.25)
             rec = O.vq_decode(P, q, hd)
             loss = torch.nn.functional.mse_loss(rec, x) + vq_loss
+        elif ae:
+            rec = O.vanilla_decode(P, O.ae_encode(P, x, ae, True, stats), ae, True, stats)
+            loss = O.ae_loss(rec, x)["loss"]
         else:
             hd = O.DEFAULT_HIDDEN
             mu, lv = O.vanilla_encode(P, x, hd, True, stats)
@@ -304,7 +315,7 @@ def cpu_baseline(batch, seconds, arch="vanilla", threads=None):
         el = time.perf_counter() - t0
         if el >= seconds or n >= 200:
             break
-    name = "VQVAE" if vq else "VanillaVAE"
+    name = "VQVAE" if vq else (f"Autoencoder {ae}" if ae else "VanillaVAE")
     torch.set_num_threads(prev)
     return {"value": round(n * batch / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"oracle {name} fp32 train step (fwd+loss+bwd+Adam), B={batch}, {n} steps / {el:.1f}s "
@@ -455,6 +466,16 @@ def main():
         net = VQNet(dtype=dtype, device="cuda", generator=gen)
         plan = VQStepPlan(net, args.batch, concurrent=args.concurrent != "off")
         opt = FusedAdam(net, lr=0.005)                             # configs/vae/vq_vae.yaml LR
+    elif args.arch in AE_WIDTHS:
+        # models.Autoencoder's fused step: the VanillaVAE plan with the fc_var half pinned at zero and
+        # eps = 0 (z = fc(h)), MSE only (M_N = 0); configs/big_ae.yaml LR
+        net = VAENet(latent_dim=128, hidden_dims=AE_WIDTHS[args.arch], dtype=dtype, device="cuda", generator=gen)
+        for nm in ("fc_var.weight", "fc_var.bias"):
+            sp = net.layout.by_name[nm]
+            net.params[sp.offset:sp.offset + sp.numel].zero_()
+        net.sync_lowp()
+        plan = StepPlan(net, args.batch, loss="vanilla", kld_weight=0.0, concurrent=args.concurrent == "on")
+        opt = FusedAdam(net, lr=0.005)
     else:
         net = VAENet(latent_dim=128, dtype=dtype, device="cuda", generator=gen)
         loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
@@ -465,7 +486,7 @@ def main():
     # synthetic data resident in HBM (per-rank seed 1265+rank): U[0,1) images, N(0,1) eps
     g = torch.Generator(device="cuda").manual_seed(1265 + rank)
     plan.x.copy_(torch.rand(plan.x.shape, generator=g, device="cuda"))
-    if hasattr(plan, "eps"):
+    if hasattr(plan, "eps") and args.arch not in AE_WIDTHS:
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
     step = TrainStep(net, plan, opt, graph=not args.no_graph)
 
@@ -527,7 +548,7 @@ def main():
                  "mfma_frac": round(step_flops / (ms * 1e-3) / (peak_tf * 1e12), 4),
                  "step_gflop": round(step_flops / 1e9, 3)}
     dropin = dropin_eager = None
-    if world == 1 and not args.no_dropin:
+    if world == 1 and not args.no_dropin and args.arch not in AE_WIDTHS:
         dropin = dropin_leg(args, dtype, steps=max(20, min(args.steps, 100)))
         dropin_eager = dropin_leg(args, dtype, engine="eager")
     line = {
@@ -545,13 +566,17 @@ def main():
         "data": "synthetic: U[0,1) 64x64x3 images + N(0,1) eps resident in HBM, random-init weights",
         "config": {"workload": ("VQVAE embedding_dim=64 num_embeddings=512 64x64 train step (fwd+loss+bwd+Adam)"
                                 if args.arch == "vq" else
+                                f"Autoencoder hidden_dims={AE_WIDTHS[args.arch]} latent_dim=128 64x64 train step "
+                                "(fwd+MSE+bwd+Adam)" if args.arch in AE_WIDTHS else
                                 f"{'VanillaVAE' if args.arch == 'vanilla' else args.arch} latent_dim=128 "
                                 f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}"),
                    "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                    "parallelism": f"dp{world}", "graph": not args.no_graph, "comm": comm,
                    "devices_used": min(world, ndev)},
-        "elbo": {"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1],
-                 ("VQ_Loss" if args.arch == "vq" else "KLD"): loss_terms[2], "finite": finite},
+        "elbo": ({"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1], "finite": finite}
+                 if args.arch in AE_WIDTHS else      # (the Autoencoder's loss is the MSE alone)
+                 {"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1],
+                  ("VQ_Loss" if args.arch == "vq" else "KLD"): loss_terms[2], "finite": finite}),
         "sum_kernel_us_isolated": round(step_kernel_us, 1),
         "roofline": roof,
         "step_roofline": step_roof,

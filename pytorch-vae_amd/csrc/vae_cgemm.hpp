@@ -237,10 +237,13 @@ cgemm_kernel(const GemmParams p) {
 
   // Prologue.  Table loads go out first and the ring's loads after them: vmcnt counts in issue
   // order, so writing the tables to LDS then waits for the table loads only, not the ring.
-  constexpr int TCH = 2;                             // channels per thread (<= 512 = MAXC)
+  // precomputed tables of up to 512 channels are copied with their loads hoisted (2 channels per
+  // thread); wider ones (the Autoencoder's 1024-4096-channel layers) take tab_fill's loop below
+  constexpr int TCH = 2;
   float tva[3][TCH], tve[4][TCH];
-  const bool a_tab = ABN && p.a_xf.table != nullptr;
-  const bool e_tab = EM == E_BNBWD && p.epi_xf.kind == VAE_X_BN_ACT && p.epi_xf.table != nullptr;
+  const bool a_tab = ABN && p.a_xf.table != nullptr && p.a_xf.channels <= 256 * TCH;
+  const bool e_tab = EM == E_BNBWD && p.epi_xf.kind == VAE_X_BN_ACT && p.epi_xf.table != nullptr &&
+                     p.epi_xf.channels <= 256 * TCH;
   if (a_tab) {
     const int C = p.a_xf.channels;
 #pragma unroll

@@ -287,7 +287,7 @@ __host__ __device__ inline int tab_stride(int c) { return tab_pad(c) + 8; }
 // every workgroup of every consumer derives bit-identical coefficients.
 __host__ __device__ inline bool bn_fast_ok(const vae_xform& x) {
   const int C = x.channels, R = x.reps > 1 ? x.reps : 1;
-  if (C <= 0 || R * C > 1024 || (x.reps > 1 && x.rstride < C)) return false;
+  if (C <= 0 || C > 512 || R * C > 1024 || (x.reps > 1 && x.rstride < C)) return false;   // (finish: <= 2 channels a thread)
   return C <= 256 ? (256 % C == 0) : (C % 256 == 0);
 }
 

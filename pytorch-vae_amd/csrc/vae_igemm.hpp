@@ -36,7 +36,10 @@ enum AMode { A_CONV = 0, A_CONVT = 1, A_DENSE = 2, A_KM = 3 };
 enum BMode { B_NK = 0, B_KN = 1, B_GATHER = 2 };
 enum EMode { E_STORE = 0, E_BNBWD = 1, E_ACC = 2, E_REPARAM = 3 };
 
-constexpr int MAXC = 512;   // max channels of a per-channel transform table
+// max channels of a per-channel transform table (the Autoencoder's widest BatchNorm: 4096,
+// configs/patient_vvbig_ae.yaml); the tables live in dynamic LDS sized by the real channel count,
+// and a launch whose tables would not fit the LDS budget falls back or fails (lds_fits)
+constexpr int MAXC = 4096;
 constexpr int NTHREADS = 256;
 
 template <class T> constexpr int bk_of() { return sizeof(T) == 2 ? 64 : 32; }

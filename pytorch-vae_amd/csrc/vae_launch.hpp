@@ -14,6 +14,22 @@ namespace {
 
 constexpr int kCUs = 256;
 constexpr int kTargetBlocks = 512;   // 2 resident workgroups per CU
+constexpr long kLdsBytes = 160 * 1024;   // LDS one workgroup may use (MI355X_MICROARCH.md)
+
+// dynamic LDS of the per-channel tables a cgemm launch carries (cg_launch_tile)
+inline long cg_table_bytes(const GemmParams& p, int em) {
+  const int k = p.a_xf.kind;
+  return 4l * (((k == VAE_X_BN_ACT || k == VAE_X_BN_DY) ? 3 * tab_stride(p.a_xf.channels) : 0) +
+               (em == E_BNBWD ? 4 * tab_stride(p.epi_xf.channels) : 0));
+}
+// static LDS of a cgemm tile (operand ring buffers or the epilogue tile, plus the statistic
+// partials), with both ring buffers counted
+inline long cg_static_bytes(int bm, int bn) {
+  const int bk = bm >= 128 ? 64 : 128;
+  const long loop = 2l * (bm + bn) * (bk + 8) * 2, epi = (long)bm * (bn + 4) * 4;
+  const int wn = bn >= 2 * bm ? 4 : (bm >= 2 * bn ? 1 : 2);
+  return (loop > epi ? loop : epi) + (4 / wn) * 2l * bn * 4 + 256;
+}
 
 inline vae_xform sanitize(vae_xform x) {
   if (x.channels <= 0) x.channels = 1;
@@ -203,9 +219,24 @@ inline int launch_finalize(const GemmParams& p, hipStream_t st) {
   return check_launch("igemm_finalize");
 }
 
+// A launch whose dynamic tables are large (> 64 KB: BatchNorm widths of 2048-4096 channels) is
+// checked against the LDS budget with the kernel's own static LDS; the launch is skipped and
+// check_launch's caller sees VAE_E_UNSUPPORTED through lds_error.
+inline thread_local bool lds_error = false;
+template <class K>
+inline bool lds_fits(K kernel, size_t dyn) {
+  if (dyn <= 64 * 1024 || querying()) return true;
+  hipFuncAttributes at;
+  if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(kernel)) != hipSuccess) return true;
+  if ((long)(at.sharedSizeBytes + dyn) <= kLdsBytes) return true;
+  lds_error = true;
+  return false;
+}
+
 #define VAE_TILE_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
-    VAE_LAUNCH((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VA, VB, DYA, DYB>), grid, block, lds, st, p); \
+    if (lds_fits(igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VA, VB, DYA, DYB>, lds)) \
+      VAE_LAUNCH((igemm_kernel<T, TA, TB, BM_, BN_, AM, BMD, EM, VA, VB, DYA, DYB>), grid, block, lds, st, p); \
     return; \
   }
 
@@ -255,6 +286,11 @@ inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
   else if (va) launch_shape<T, TA, TB, AM, BMD, EM, true, false, DYA, DYB>(p, t, st);
   else if (vb) launch_shape<T, TA, TB, AM, BMD, EM, false, true, DYA, DYB>(p, t, st);
   else launch_shape<T, TA, TB, AM, BMD, EM, false, false, DYA, DYB>(p, t, st);
+  if (lds_error) {
+    lds_error = false;
+    return fail(VAE_E_UNSUPPORTED, "igemm: per-channel tables of %d / %d channels exceed the LDS", p.a_xf.channels,
+                p.epi_xf.channels);
+  }
   int rc = check_launch("igemm");
   if (rc) return rc;
   if (EM != E_ACC && p.slab) return launch_finalize<T, EM>(p, st);
@@ -471,6 +507,8 @@ inline bool cg_ok(const GemmParams& p, int em) {
   if ((k == VAE_X_BN_ACT || k == VAE_X_BN_DY) && (p.a_xf.channels != p.gc || p.a_xf.channels > MAXC)) return false;
   if (k == VAE_X_BN_DY && !aligned(p.a_xf.aux, 16)) return false;
   if (p.residual && !aligned(p.residual, 16)) return false;
+  // the widest BatchNorm tables (4096 channels on both sides) leave no room for an operand tile
+  if (cg_table_bytes(p, em) + cg_static_bytes(32, 32) > kLdsBytes) return false;
   if (em == E_BNBWD && p.epi_xf.kind != VAE_X_NONE) {
     // (a plain LeakyReLU epilogue has no per-channel table: its channel count is not read)
     if (!aligned(p.epi_xf.aux, 16) || (p.epi_xf.kind == VAE_X_BN_ACT && p.epi_xf.channels % 8)) return false;
@@ -493,9 +531,10 @@ inline int cg_splitwg() { static const int v = tune_env("VAE_CG_SPLITWG", 1); re
 
 // Largest tile that still gives every CU ~2 workgroups; split-K (slabs + igemm_finalize) when
 // even the smallest leaves the chip half empty and K is deep.
-inline CgTile cg_pick(long M, long N, int nphase) {
+inline CgTile cg_pick(long M, long N, int nphase, long table_bytes = 0) {
   const CgTile c[] = {{128, 128}, {128, 32}, {64, 64}, {64, 32}, {32, 64}, {32, 32}};
   for (const CgTile& t : c) {
+    if (table_bytes + cg_static_bytes(t.bm, t.bn) > kLdsBytes) continue;   // (wide BatchNorm tables)
     if (t.bm > 32 && M < t.bm) continue;
     if (t.bn > 32 && N < t.bn) continue;
     // 128 x 32 only for the long thin maps (>= 8 workgroups per CU at 64 x 32)
@@ -542,7 +581,7 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
 #ifdef VAE_PROBE
   p.probe = vae_probe_buffer();
 #endif
-  const CgTile t = cg_pick(p.M, p.N, p.nphase);
+  const CgTile t = cg_pick(p.M, p.N, p.nphase, cg_table_bytes(p, EM));
   const int bk = t.bm >= 128 ? 64 : 128;
   int kmax = p.K;
   if (AM == A_CONVT) {

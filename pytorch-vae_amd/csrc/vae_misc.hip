@@ -36,7 +36,9 @@ int check_launch(const char* what) {
 
 namespace {
 
-constexpr int HEAD_MAXC = 64;      // channels entering the head
+constexpr int HEAD_MAXC = 512;     // channels entering the head (the Autoencoder's widest final layer:
+                                   // configs/patient_vvbig_ae.yaml, hidden_dims[0] = 512)
+constexpr int HEAD_CW = 32;        // channels staged per pass when the input has more than 64
 constexpr int HEAD_T = 256;        // threads = pixels per tile
 constexpr int CO = 3;              // RGB
 constexpr int HEAD_GS = 774;       // max (rows+2)*(w+2) with rows*w == 256
@@ -86,11 +88,17 @@ __device__ void head_coefs(const vae_xform& xf, float* ta, float* tb, float* tp,
   }
 }
 
-// Stage act(x) rows [h0-1, h0+rows] x cols [-1, w] into LDS as [(rows+2)][(w+2)][c+4] floats
+// Channels staged per pass: all of them up to 32 (one tile of (rows+2) x (w+2) x (c+4) floats),
+// HEAD_CW at a time above (a 64-channel tile of a 64-wide image is already 105 KB)
+__host__ __device__ inline int head_cw(int c) { return c > 32 ? HEAD_CW : c; }
+
+// Stage act(x) rows [h0-1, h0+rows] x cols [-1, w], channels [c0, c0+cw) into LDS as
+// [(rows+2)][(w+2)][cw+4] floats
 template <class T>
-__device__ void stage_input(const HeadP& p, int n, int h0, float* xs, const float* ta, const float* tb) {
-  const int CP = p.c + 4, WP = p.w + 2;
-  const int oct_per_pix = p.c / 8;
+__device__ void stage_input(const HeadP& p, int n, int h0, float* xs, const float* ta, const float* tb, int c0,
+                            int cw) {
+  const int CP = cw + 4, WP = p.w + 2;
+  const int oct_per_pix = cw / 8;
   const int total = (p.rows + 2) * WP * oct_per_pix;
   const T* X = static_cast<const T*>(p.x);
   for (int e = threadIdx.x; e < total; e += blockDim.x) {
@@ -100,9 +108,9 @@ __device__ void stage_input(const HeadP& p, int n, int h0, float* xs, const floa
     const int hi = h0 + rr - 1, wi = cc - 1;
     float v[8];
     if (hi >= 0 && hi < p.h && wi >= 0 && wi < p.w) {
-      ld8(X + (((long)n * p.h + hi) * p.w + wi) * p.c + o * 8, v);
+      ld8(X + (((long)n * p.h + hi) * p.w + wi) * p.c + c0 + o * 8, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = act_of(p.xf, ta, tb, v[j], o * 8 + j);
+      for (int j = 0; j < 8; ++j) v[j] = act_of(p.xf, ta, tb, v[j], c0 + o * 8 + j);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = 0.f;
@@ -117,30 +125,36 @@ __device__ void stage_input(const HeadP& p, int n, int h0, float* xs, const floa
 template <class T>
 __global__ void __launch_bounds__(HEAD_T) head_fwd_kernel(HeadP p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  __shared__ float ta[HEAD_MAXC], tb[HEAD_MAXC], ws[CO * 9 * HEAD_MAXC], red[HEAD_T / 64];
+  __shared__ float ta[HEAD_MAXC], tb[HEAD_MAXC], ws[CO * 9 * 64], red[HEAD_T / 64];
   const int tiles_per_img = p.h / p.rows;
   const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x % tiles_per_img) * p.rows;
   head_coefs(p.xf, ta, tb, nullptr, nullptr, blockIdx.x == 0);
-  for (int i = threadIdx.x; i < CO * 9 * p.c; i += blockDim.x) ws[i] = p.wt[i];
-  __syncthreads();
-  stage_input<T>(p, n, h0, smem, ta, tb);
-  __syncthreads();
-  const int CP = p.c + 4, WP = p.w + 2;
+  const int cw = head_cw(p.c);
+  const int CP = cw + 4, WP = p.w + 2;
   const int tr = threadIdx.x / p.w, tc = threadIdx.x % p.w;
   float o[CO] = {p.bias[0], p.bias[1], p.bias[2]};
-  for (int r = 0; r < 3; ++r)
-    for (int s = 0; s < 3; ++s) {
-      const float* xp = smem + ((tr + r) * WP + tc + s) * CP;
-      const float* wp = ws + (r * 3 + s) * p.c;
-      for (int c = 0; c < p.c; c += 4) {
-        const f32x4 xv = *reinterpret_cast<const f32x4*>(xp + c);
+  for (int c0 = 0; c0 < p.c; c0 += cw) {
+    __syncthreads();                                 // tables / the previous pass's reads
+    for (int i = threadIdx.x; i < CO * 9 * cw; i += blockDim.x) {   // weights [co][tap][c0 .. c0+cw)
+      const int ct = i / cw, c = i - ct * cw;
+      ws[i] = p.wt[ct * p.c + c0 + c];
+    }
+    stage_input<T>(p, n, h0, smem, ta, tb, c0, cw);
+    __syncthreads();
+    for (int r = 0; r < 3; ++r)
+      for (int s = 0; s < 3; ++s) {
+        const float* xp = smem + ((tr + r) * WP + tc + s) * CP;
+        const float* wp = ws + (r * 3 + s) * cw;
+        for (int c = 0; c < cw; c += 4) {
+          const f32x4 xv = *reinterpret_cast<const f32x4*>(xp + c);
 #pragma unroll
-        for (int co = 0; co < CO; ++co) {
-          const float* wq = wp + co * 9 * p.c + c;
-          o[co] = fmaf(xv[0], wq[0], fmaf(xv[1], wq[1], fmaf(xv[2], wq[2], fmaf(xv[3], wq[3], o[co]))));
+          for (int co = 0; co < CO; ++co) {
+            const float* wq = wp + co * 9 * cw + c;
+            o[co] = fmaf(xv[0], wq[0], fmaf(xv[1], wq[1], fmaf(xv[2], wq[2], fmaf(xv[3], wq[3], o[co]))));
+          }
         }
       }
-    }
+  }
   const int hh = h0 + tr;
   const int img_t = n / p.samples;
   float sq = 0.f;
@@ -250,13 +264,103 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_data_kernel(HeadP p) {
   }
 }
 
+// head_bwd_data_kernel for inputs wider than 64 channels (the Autoencoder's 128-512-channel final
+// layers): the same sums, HEAD_CW channels at a time (a register accumulator per channel of the
+// pass, the pass's weights in LDS)
+template <class T>
+__global__ void __launch_bounds__(HEAD_T) head_bwd_data_wide_kernel(HeadP p) {
+  constexpr int CW = HEAD_CW;
+  __shared__ float ta[HEAD_MAXC], tb[HEAD_MAXC], tp[HEAD_MAXC], tq[HEAD_MAXC];
+  __shared__ float ws[CO * 9 * CW];
+  __shared__ float gs[HEAD_GS * CO];
+  __shared__ float r1[4][CW], r2[4][CW];
+  const int C = p.c;
+  const int tiles_per_img = p.h / p.rows;
+  const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x % tiles_per_img) * p.rows;
+  head_coefs(p.epi, ta, tb, tp, tq);
+  const int WP = p.w + 2;
+  for (int e = threadIdx.x; e < (p.rows + 2) * WP; e += blockDim.x) {
+    const int cc = e % WP, rr = e / WP;
+    const int hi = h0 + rr - 1, wi = cc - 1;
+    const bool in = hi >= 0 && hi < p.h && wi >= 0 && wi < p.w;
+#pragma unroll
+    for (int co = 0; co < CO; ++co) gs[e * CO + co] = in ? gseed_at(p, n, co, hi, wi) : 0.f;
+  }
+  const int tr = threadIdx.x / p.w, tc = threadIdx.x % p.w;
+  const long base = (((long)n * p.h + h0 + tr) * p.w + tc) * C;
+  const T* Y = static_cast<const T*>(p.epi.aux);
+  T* DX = static_cast<T*>(p.dx);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long roff = p.sum_reps > 1 ? (long)(blockIdx.x % p.sum_reps) * p.sum_rstride : 0;
+  for (int c0 = 0; c0 < C; c0 += CW) {
+    __syncthreads();                                 // gs / tables, and the previous pass's ws, r1, r2
+    for (int i = threadIdx.x; i < CO * 9 * CW; i += blockDim.x) {
+      const int ct = i / CW, c = i - ct * CW;
+      ws[i] = p.wt[ct * C + c0 + c];
+    }
+    __syncthreads();
+    float da[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) da[c] = 0.f;
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r)
+#pragma unroll 1
+      for (int s = 0; s < 3; ++s) {
+        const float* g = gs + ((tr + 2 - r) * WP + (tc + 2 - s)) * CO;
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+          const float gv = g[co];
+          const float* wq = ws + co * 9 * CW + (r * 3 + s) * CW;
+#pragma unroll
+          for (int c = 0; c < CW; ++c) da[c] = fmaf(gv, wq[c], da[c]);
+        }
+      }
+#pragma unroll
+    for (int k0 = 0; k0 < CW; k0 += 8) {
+      float y[8];
+      if (p.epi.kind != VAE_X_NONE) ld8(Y + base + c0 + k0, y);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + k0 + j;
+        float gv = da[k0 + j], s1 = 0.f, s2 = 0.f;
+        if (p.epi.kind == VAE_X_BN_ACT) {
+          const float z = fmaf(y[j], ta[c], tb[c]);
+          gv = z > 0.f ? gv : gv * p.epi.slope;
+          s1 = gv;
+          s2 = gv * fmaf(y[j], tp[c], tq[c]);
+        } else if (p.epi.kind == VAE_X_ACT) {
+          gv = y[j] > 0.f ? gv : gv * p.epi.slope;
+        }
+        DX[base + c] = cvt<T>(gv);
+        if (p.epi.kind == VAE_X_BN_ACT) {
+          for (int off = 32; off > 0; off >>= 1) { s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off); }
+          if (lane == 0) { r1[wv][k0 + j] = s1; r2[wv][k0 + j] = s2; }
+        }
+      }
+    }
+    if (p.epi.kind == VAE_X_BN_ACT) {
+      __syncthreads();
+      if (threadIdx.x < CW) {
+        const int c = threadIdx.x;
+        atomicAdd(p.dbeta + roff + c0 + c, r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c]);
+        atomicAdd(p.dgamma + roff + c0 + c, r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c]);
+      }
+    }
+  }
+}
+
 // dW[co][r][s][c] += Σ_pix gseed[pix][co] · act(x)[pix + (r-1, s-1)][c];  db[co] += Σ gseed
 template <class T>
 __global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float ta[HEAD_MAXC], tb[HEAD_MAXC], gs[HEAD_T * CO], red[CO][HEAD_T / 64];
-  constexpr int NI = 3;                              // (9*C)/256 rounded up, C <= 85
+  constexpr int NI = (9 * HEAD_MAXC + HEAD_T - 1) / HEAD_T;    // dW elements per thread
   const int nidx = 9 * p.c;
+  const int cw = head_cw(p.c);
   float acc[NI][CO];
   float dbacc[CO] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -265,11 +369,10 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
     for (int co = 0; co < CO; ++co) acc[i][co] = 0.f;
   head_coefs(p.xf, ta, tb, nullptr, nullptr);
   const int tiles_per_img = p.h / p.rows;
-  const int CP = p.c + 4, WP = p.w + 2;
+  const int CP = cw + 4, WP = p.w + 2;
   for (int tile = blockIdx.x; tile < p.tiles; tile += gridDim.x) {
     const int n = tile / tiles_per_img, h0 = (tile % tiles_per_img) * p.rows;
     __syncthreads();
-    stage_input<T>(p, n, h0, smem, ta, tb);
     {
       const int tr = threadIdx.x / p.w, tc = threadIdx.x % p.w;
 #pragma unroll
@@ -279,18 +382,23 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
         dbacc[co] += g;
       }
     }
-    __syncthreads();
+    for (int c0 = 0; c0 < p.c; c0 += cw) {
+      if (c0) __syncthreads();                       // the previous pass's reads of the tile
+      stage_input<T>(p, n, h0, smem, ta, tb, c0, cw);
+      __syncthreads();
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int idx = threadIdx.x + i * HEAD_T;
-      if (idx >= nidx) break;
-      const int tap = idx / p.c, c = idx - tap * p.c;
-      const int r = tap / 3, s = tap - r * 3;
-      for (int pix = 0; pix < HEAD_T; ++pix) {
-        const int tr = pix / p.w, tc = pix - tr * p.w;
-        const float xv = smem[((tr + r) * WP + tc + s) * CP + c];
+      for (int i = 0; i < NI; ++i) {
+        const int idx = threadIdx.x + i * HEAD_T;
+        if (idx >= nidx) break;
+        const int tap = idx / p.c, c = idx - tap * p.c;
+        if (c < c0 || c >= c0 + cw) continue;        // (this pass stages channels [c0, c0+cw))
+        const int r = tap / 3, s = tap - r * 3;
+        for (int pix = 0; pix < HEAD_T; ++pix) {
+          const int tr = pix / p.w, tc = pix - tr * p.w;
+          const float xv = smem[((tr + r) * WP + tc + s) * CP + c - c0];
 #pragma unroll
-        for (int co = 0; co < CO; ++co) acc[i][co] = fmaf(gs[pix * CO + co], xv, acc[i][co]);
+          for (int co = 0; co < CO; ++co) acc[i][co] = fmaf(gs[pix * CO + co], xv, acc[i][co]);
+        }
       }
     }
   }
@@ -320,7 +428,8 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
 
 int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
   if (!a || !a->x || !a->wt || !a->bias || !a->target || !a->recon) return fail(VAE_E_BADARG, "%s: null tensor", what);
-  if (a->c % 8 || a->c > HEAD_MAXC || a->c <= 0) return fail(VAE_E_UNSUPPORTED, "%s: channels %d", what, a->c);
+  if (a->c % 8 || a->c > HEAD_MAXC || a->c <= 0 || (a->c > 32 && a->c % HEAD_CW))
+    return fail(VAE_E_UNSUPPORTED, "%s: channels %d", what, a->c);
   if (a->w <= 0 || a->w > 256 || HEAD_T % a->w || a->h % (HEAD_T / a->w))
     return fail(VAE_E_UNSUPPORTED, "%s: spatial %dx%d (need w | 256 and (256/w) | h)", what, a->h, a->w);
   if (a->dtype != VAE_F32 && a->dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "%s: dtype", what);
@@ -536,7 +645,7 @@ extern "C" int vae_head_fwd(const vae_head_args* a, void* stream) {
   if (!a->sse) return fail(VAE_E_BADARG, "head_fwd: sse");
   rc = head_fwd_mfma_launch(a, (hipStream_t)stream);   // bf16, 64-wide, 32 channels
   if (rc != kHeadFallback) return rc;
-  const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
+  const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (head_cw(p.c) + 4) * sizeof(float);
   if (lds > 64 * 1024) return fail(VAE_E_UNSUPPORTED, "head_fwd: tile too large");
   if (a->dtype == VAE_F32) VAE_LAUNCH(head_fwd_kernel<float>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   else VAE_LAUNCH(head_fwd_kernel<__bf16>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
@@ -563,8 +672,11 @@ extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
       if (f) VAE_LAUNCH((head_bwd_data_kernel<float, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
       else VAE_LAUNCH((head_bwd_data_kernel<__bf16, 64>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
       break;
-    default:
-      return fail(VAE_E_UNSUPPORTED, "head_bwd_data: channels %d (32 or 64)", a->c);
+    default:      // (head_setup: 64 < c <= HEAD_MAXC, c % HEAD_CW == 0)
+      if (a->c <= 64) return fail(VAE_E_UNSUPPORTED, "head_bwd_data: channels %d (32, 64 or a multiple of %d)", a->c, HEAD_CW);
+      if (f) VAE_LAUNCH((head_bwd_data_wide_kernel<float>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      else VAE_LAUNCH((head_bwd_data_wide_kernel<__bf16>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
+      break;
   }
   return check_launch("head_bwd_data");
 }
@@ -574,10 +686,10 @@ extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
   int rc = head_setup(a, p, "head_bwd_filter");
   if (rc) return rc;
   if ((!a->coef && !a->grad_recon) || !a->dw) return fail(VAE_E_BADARG, "head_bwd_filter: coef/grad_recon/dw");
-  if (9 * a->c > 3 * HEAD_T) return fail(VAE_E_UNSUPPORTED, "head_bwd_filter: channels");
+  if (9 * a->c > 9 * HEAD_MAXC) return fail(VAE_E_UNSUPPORTED, "head_bwd_filter: channels");
   rc = head_bwd_mfma_launch(a, false, true, (hipStream_t)stream);
   if (rc != kHeadFallback) return rc;
-  const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (p.c + 4) * sizeof(float);
+  const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (head_cw(p.c) + 4) * sizeof(float);
   const int grid = p.tiles < 256 ? p.tiles : 256;
   if (a->dtype == VAE_F32) VAE_LAUNCH(head_bwd_filter_kernel<float>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   else VAE_LAUNCH(head_bwd_filter_kernel<__bf16>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);

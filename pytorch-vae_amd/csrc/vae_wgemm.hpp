@@ -60,6 +60,53 @@ template <int BM> constexpr int wg_kp() { return BM >= 128 ? 64 : 32; }
 // operand tiles of one workgroup (bytes of LDS): 2 buffers x (U + V) rows of KP pixels
 template <int BM, int BJ> constexpr int wgemm_lds_bytes() { return 2 * wg_kp<BM>() * (wg_rs<BM>() + wg_rs<BJ>()); }
 
+// Accumulator tile -> dW (or this K slice's partial slab): lane element (i, j, e) is row
+// mrow + 16i + e, column jcol + 16j, at offset row * rowstride + coff + column.  A single K slice
+// (p.own) adds into dW with plain loads and stores: every old value is loaded first, then every
+// sum is stored — interleaved, each load would wait behind the previous store (the compiler cannot
+// prove the addresses distinct), one memory round trip per element.
+template <int TM, int TJ>
+__device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, const f32x4 (&acc)[TM][TJ], int mrow,
+                                            int jcol, long rowstride, long coff) {
+  if (!part && p.own) {
+    float old[TM][TJ][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int mm = mrow + i * 16 + e, jj = jcol + j * 16;
+          old[i][j][e] = (mm < p.M && jj < p.J) ? p.dw[mm * rowstride + coff + jj] : 0.f;
+        }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int mm = mrow + i * 16 + e, jj = jcol + j * 16;
+          if (mm < p.M && jj < p.J) p.dw[mm * rowstride + coff + jj] = old[i][j][e] + acc[i][j][e];
+        }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int jj = jcol + j * 16;
+      if (jj >= p.J) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int mm = mrow + i * 16 + e;
+        if (mm >= p.M) continue;
+        const long o = mm * rowstride + coff + jj;
+        if (part) part[o] = acc[i][j][e];
+        else atomicAdd(p.dw + o, acc[i][j][e]);
+      }
+    }
+}
+
 // The per-tap weight-gradient GEMM of workgroup `bid` of its problem, operand tiles at `lds`
 // (wgemm_lds_bytes) — called by wgemm_kernel (one problem per launch) and by wg_group_kernel
 // (several layers' weight gradients in one launch, vae_wgrad_batch.hip).
@@ -256,22 +303,7 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, cha
   // D[m][j]: lane holds rows 4g + e of fragment i, column li of fragment j
   const long rowstride = (long)p.R * p.R * p.J;
   float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int jj = j0 + wn * WTJ + j * 16 + li;
-      if (jj >= p.J) continue;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int mm = m0 + wm * WTM + i * 16 + 4 * g + e;
-        if (mm >= p.M) continue;
-        const long o = mm * rowstride + (long)tap * p.J + jj;
-        if (part) part[o] = acc[i][j][e];
-        else if (p.own) p.dw[o] += acc[i][j][e];
-        else atomicAdd(p.dw + o, acc[i][j][e]);
-      }
-    }
+  wg_epilogue<TM, TJ>(p, part, acc, m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)tap * p.J);
 }
 
 template <int BM, int BJ, int XU, int XV>
@@ -504,22 +536,7 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
   float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
 #pragma unroll
   for (int t = 0; t < TAPS; ++t)
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int jj = j0 + wn * WTJ + j * 16 + li;
-        if (jj >= p.J) continue;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int mm = m0 + wm * WTM + i * 16 + 4 * g + e;
-          if (mm >= p.M) continue;
-          const long o = mm * rowstride + (long)t * p.J + jj;
-          if (part) part[o] = acc[t][i][j][e];
-          else if (p.own) p.dw[o] += acc[t][i][j][e];
-          else atomicAdd(p.dw + o, acc[t][i][j][e]);
-        }
-      }
+    wg_epilogue<TM, TJ>(p, part, acc[t], m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)t * p.J);
 }
 
 template <int BM, int BJ, int XU, int XV, int RR>
@@ -637,6 +654,15 @@ inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots
   int T = mn >= 128 ? 128 : (mn >= 64 ? 64 : 32);
   static const int t1 = tune_env("VAE_WG_T1X1", 0);            // tile override for 1x1 kernels (sweeps)
   if (p.R == 1 && (t1 == 64 || t1 == 32) && t1 < T) T = t1;
+  // wide BatchNorm tables (the Autoencoder's 2048-4096 channels) and the operand tiles share the LDS
+  {
+    const bool bu = p.u_xf.kind == VAE_X_BN_ACT || p.u_xf.kind == VAE_X_BN_DY;
+    const bool bv = p.v_xf.kind == VAE_X_BN_ACT || p.v_xf.kind == VAE_X_BN_DY;
+    const long tab = 4l * ((bu ? 3 * tab_stride(p.u_xf.channels) : 0) + (bv ? 3 * tab_stride(p.v_xf.channels) : 0));
+    auto tile_lds = [](int t) -> long { return 2l * (t >= 128 ? 64 : 32) * 2 * (t == 32 ? 64 : (t == 64 ? 160 : 288)); };
+    while (T > 32 && tab + tile_lds(T) > kLdsBytes) T /= 2;
+    if (tab + tile_lds(T) + 8192 > kLdsBytes) return fail(VAE_E_UNSUPPORTED, "wgemm: per-channel tables exceed the LDS");
+  }
   const bool taps_in_block = T == 32 && (p.R == 3 || (p.R == 4 && p.u_xf.kind <= VAE_X_ACT && p.v_xf.kind <= VAE_X_ACT));
   const long tiles = (long)((p.M + T - 1) / T) * ((p.J + T - 1) / T) * (taps_in_block ? 1 : p.R * p.R);
   const long ksteps = (npix + 31) / 32;

@@ -493,8 +493,10 @@ class Autoencoder(_HipVAE):
     HIP backward, as the centre-weighted MSE's does.
 
     Not on this path (raise): the VGG feature loss (needs pretrained vgg19_bn weights, a network
-    download), hidden_dims other than five stride-2 layers (the stride-1 extra layers, :39) and
-    BatchNorm widths above the kernels' 512-channel transform tables."""
+    download) and hidden_dims other than five stride-2 layers (the stride-1 extra layers, :39; no
+    reference config uses them).  Every width of the reference's configs runs, up to
+    patient_vvbig_ae.yaml's [512, 1024, 2048, 4096, 4096]: the per-channel BatchNorm tables are sized
+    by the real channel count in LDS (vae_launch.hpp lds budget)."""
 
     def __init__(self, in_channels: int, latent_dim: int, hidden_dims: List = None, use_vgg: bool = False,
                  center_focus_sigma: float = None, use_skip_connections: bool = False,
@@ -506,9 +508,9 @@ class Autoencoder(_HipVAE):
         if len(hd) != 5:
             raise NotImplementedError(f"Autoencoder with {len(hd)} layers (stride-1 extra layers, "
                                       "autoencoder.py:39) is not on the MI355X path; five stride-2 layers are")
-        if max(hd) > 512:
-            raise NotImplementedError(f"Autoencoder hidden width {max(hd)} > 512 channels (BatchNorm transform "
-                                      "tables of the GEMM kernels)")
+        if max(hd) > 4096 or hd[0] > 512:
+            raise NotImplementedError(f"Autoencoder hidden widths {hd}: the kernels take BatchNorm widths up to "
+                                      "4096 and a final layer of up to 512 channels (every reference config)")
         super().__init__(in_channels, latent_dim, hd, **kwargs)
         self.center_focus_sigma = center_focus_sigma
         self.center_weight_mask = None

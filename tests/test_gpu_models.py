@@ -276,7 +276,7 @@ def test_experiment_graph_engine_matches_eager(arch):
     assert float((dg - de).abs().max()) <= 2 * lr * 1.001
 
 
-@pytest.mark.parametrize("case", ["ae_b16", "ae_center_b8", "ae_mssim_b8"])
+@pytest.mark.parametrize("case", ["ae_b16", "ae_center_b8", "ae_mssim_b8", "ae_big_b4"])
 def test_autoencoder_against_reference(case):
     """Autoencoder (models/autoencoder.py) through the drop-in: reference-keyed state dict (`fc`),
     forward, loss dict (KLD and feature_loss zero), gradients through loss.backward() — the GPU
