@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
 
     if (q.data) {
       // ---- dact for this wave's 4 groups of 16 pixels, N = 32 channels (2 n-frags)
-#pragma unroll
+#pragma unroll 1
       for (int gi = 0; gi < 4; ++gi) {
         const int grp = wave * 4 + gi;
         const int row = grp >> 2, c0 = (grp & 3) * 16;

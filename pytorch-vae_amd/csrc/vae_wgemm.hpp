@@ -69,25 +69,30 @@ template <int TM, int TJ>
 __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, const f32x4 (&acc)[TM][TJ], int mrow,
                                             int jcol, long rowstride, long coff) {
   if (!part && p.own) {
-    float old[TM][TJ][4];
+    // in groups of fragment rows holding <= 32 values (registers: the 128 x 128 tiles run at 256)
+    constexpr int GI = TJ * 4 * TM <= 32 ? TM : (32 / (TJ * 4) > 0 ? 32 / (TJ * 4) : 1);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i0 = 0; i0 < TM; i0 += GI) {
+      float old[GI][TJ][4];
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
+      for (int i = 0; i < GI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int mm = mrow + i * 16 + e, jj = jcol + j * 16;
-          old[i][j][e] = (mm < p.M && jj < p.J) ? p.dw[mm * rowstride + coff + jj] : 0.f;
-        }
+        for (int j = 0; j < TJ; ++j)
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+          for (int e = 0; e < 4; ++e) {
+            const int mm = mrow + (i0 + i) * 16 + e, jj = jcol + j * 16;
+            old[i][j][e] = (mm < p.M && jj < p.J) ? p.dw[mm * rowstride + coff + jj] : 0.f;
+          }
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
+      for (int i = 0; i < GI; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int mm = mrow + i * 16 + e, jj = jcol + j * 16;
-          if (mm < p.M && jj < p.J) p.dw[mm * rowstride + coff + jj] = old[i][j][e] + acc[i][j][e];
-        }
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int mm = mrow + (i0 + i) * 16 + e, jj = jcol + j * 16;
+            if (mm < p.M && jj < p.J) p.dw[mm * rowstride + coff + jj] = old[i][j][e] + acc[i0 + i][j][e];
+          }
+    }
     return;
   }
 #pragma unroll
