@@ -165,6 +165,12 @@ class StepPlan:
                              and C5 % 128 == 0 and (4 * r0) % 128 == 0 and net.img_size == 64
                              and not os.environ.get("VAE_NO_LATENT"))
         self._keep = []            # ctypes structs referenced by the call lists
+        # wide_head: a final layer wider than the MFMA head kernels' 32 channels (the Autoencoder's
+        # 128-512, configs/big_ae.yaml) runs the head Conv2d(C->3) on the conv-GEMM paths with its 3
+        # outputs zero-padded to 8, then vae_recon_fwd (tanh, NCHW reconstruction, SSE, backward
+        # seed) — the VQ-VAE output layer's route.  The reconstruction seed is the mean-MSE one, so
+        # not for IWAE's per-sample weights (S > 1 keeps the head kernels).
+        self.wide_head = h[0] > 32 and self.S == 1
 
         # -------- buffers
         f32 = dict(dtype=torch.float32, device=dev)
@@ -191,6 +197,12 @@ class StepPlan:
             sp *= 2
             self.dec.append(torch.empty(BS, sp, sp, r[i + 1], dtype=T, device=dev))
         self.fin = torch.empty(BS, img, img, r[-1], dtype=T, device=dev)
+        if self.wide_head:
+            # the head's output (pre-tanh) and its gradient, 8 channels (3 real); the head weights
+            # zero-padded to 8 output rows (vae_pad_channels at the step's head: rows 3..7 stay 0)
+            self.y8 = torch.zeros(BS, img, img, 8, dtype=T, device=dev)
+            self.g8 = torch.zeros(BS, img, img, 8, dtype=T, device=dev)
+            self.w8h = torch.zeros(8 * 9 * r[-1], dtype=T, device=dev)
         self.recon = torch.empty(BS, 3, img, img, **f32)
         self.grad_recon = None if fused_loss else torch.zeros(BS, 3, img, img, **f32)
         self.out = torch.zeros(4, **f32)                                  # loss, recon, KLD(report), kld
@@ -208,7 +220,8 @@ class StepPlan:
         # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
         nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
         nz = (_pad4(net.layout.total) + 4 + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns)) +
-              _pad4(h[0] * 9 * 8) + (_pad4(B * 2 * D) if self.latent_fused else 0))
+              _pad4(h[0] * 9 * 8) + (_pad4(B * 2 * D) if self.latent_fused else 0) +
+              (_pad4(8 * 9 * r[-1]) + 8 if self.wide_head else 0))
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += _pad4(net.layout.total)
@@ -227,6 +240,9 @@ class StepPlan:
         self.dw8 = self.zero[o:o + h[0] * 9 * 8]; o += _pad4(h[0] * 9 * 8)       # padded first-conv dW
         if self.latent_fused:       # vae_latent_fc_fwd accumulates mu|log_var: zero at every step
             self.mulv = self.zero[o:o + B * 2 * D].view(B, 2 * D); o += _pad4(B * 2 * D)
+        if self.wide_head:          # the padded head's weight / bias gradients (vae_unpad_accumulate)
+            self.dw8h = self.zero[o:o + 8 * 9 * r[-1]]; o += _pad4(8 * 9 * r[-1])
+            self.db8h = self.zero[o:o + 8]; o += 8
         # per-BatchNorm coefficient tables, rewritten every step by vae_bn_finalize:
         # forward [4][C] (BN_ACT) then backward [3][C] (BN_DY)
         self.bntab: Dict[str, torch.Tensor] = {
@@ -240,6 +256,7 @@ class StepPlan:
         # encoder's data-gradient chain (batch_wgrads); one fork and one join per step.  Off by
         # default: measured 0.670 vs 0.648 ms/step (B=64, graph-replayed) — the graph's cross-stream
         # edges cost more than the overlap gains, as the per-call side stream of round 1 did
+        wg_overlap = wg_overlap or bool(os.environ.get("VAE_WG_OVERLAP"))        # (A/B timing)
         self.wg_overlap = wg_overlap and training and not concurrent and not os.environ.get("VAE_NO_WG_OVERLAP")
         self.side_all = self.side is not None            # concurrent: every weight-gradient call
         if self.wg_overlap:
@@ -409,6 +426,9 @@ class StepPlan:
         if self.pad_rgb:
             F.append(("vae_nchw_to_nhwc_pad", (T, B, 3, img, img, 8, self.x.data_ptr(), self.x8.data_ptr())))
             F.append(("vae_pad_channels", (T, h[0] * 9, 3, 8, net.w("encoder.0.0.weight"), self.w8.data_ptr())))
+        if self.wide_head:          # head weights [3][3][3][C] -> [8][3][3][C] (one row of 27C -> 72C)
+            F.append(("vae_pad_channels", (T, 1, 27 * r[-1], 72 * r[-1], net.w("final_layer.3.weight"),
+                                           self.w8h.data_ptr())))
         # ---------------------------------------------------------------- encoder
         sp = img
         for i in range(nenc):
@@ -485,6 +505,8 @@ class StepPlan:
             prev, prev_pre = dec_out[i], dec_pre[i]
             sp *= 2
         # ---------------------------------------------------------------- head + SSE
+        if self.wide_head:
+            self._wide_head_fwd(F, cnt)
         hd = L.HeadArgs(dtype=T, n=BS, h=img, w=img, c=r[-1], samples=self.S)
         hd.x = self.fin.data_ptr()
         hd.x_xf = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin), running=True)
@@ -493,7 +515,8 @@ class StepPlan:
         hd.target = self.x.data_ptr()
         hd.recon = self.recon.data_ptr()
         hd.sse = self.sse.data_ptr()
-        self._add(F, "vae_head_fwd", hd)
+        if not self.wide_head:
+            self._add(F, "vae_head_fwd", hd)
         # ---------------------------------------------------------------- ELBO
         e = L.ElboArgs(kind=self.loss_kind, batch=B, samples=self.S, latent=D, img_elems=3 * img * img,
                        kld_weight=self.kld_weight, beta=self.beta, gamma=self.gamma, c_max=self.c_max,
@@ -531,8 +554,12 @@ class StepPlan:
         self.bwd_sums(hb, "final_layer.1")
         hb.dw = self.g("final_layer.3.weight")
         hb.db = self.g("final_layer.3.bias")
-        self._add(Bw, "vae_head_bwd", hb)
-        self._head_bwd = hb
+        if self.wide_head:
+            self._wide_head_bwd(Bw, cnt)
+            self._head_bwd = None
+        else:
+            self._add(Bw, "vae_head_bwd", hb)
+            self._head_bwd = hb
         # decoder, last block first
         sps = [2 * 2 ** i for i in range(len(r))]          # input spatial of each ConvT
         for i in reversed(range(len(r))):
@@ -653,6 +680,53 @@ class StepPlan:
                 self.bwd_sums(a, enc_pre[i - 1])
                 self._add(Bw, "vae_conv2d_bwd_data", a)
 
+    def _wide_head_fwd(self, F, cnt):
+        """Head of a final layer wider than 32 channels: Conv2d(C -> 3 padded to 8, k3 s1 p1) on the
+        conv-GEMM path with BatchNorm+LeakyReLU applied to its input on load, then vae_recon_fwd:
+        tanh -> NCHW reconstruction, per-image SSE, and with the fused loss the backward seed
+        dL/dy = 2(recon - x)(1 - recon^2) / (B*3*H*W) (the mean-MSE term of the ELBO)."""
+        net, T, img, BS = self.net, self.net.dcode, self.net.img_size, self.B * self.S
+        C = self.fin.shape[-1]
+        a = L.ConvArgs(dtype=T, n=BS, h=img, w=img, c=C, k=8, p=img, q=img, r=3, stride=1, pad=1)
+        a.x = self.fin.data_ptr()
+        a.x_xf = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin), running=True)
+        a.wt = self.w8h.data_ptr()
+        a.bias = net.p("final_layer.3.bias")     # (channels 3..7 of y8 are never read)
+        a.y = self.y8.data_ptr()
+        self._add(F, "vae_conv2d_fwd", a)
+        rc = L.ReconArgs(dtype=T, n=BS, h=img, w=img, c=3, ld=8)
+        rc.y, rc.target, rc.recon, rc.sse = self.y8.data_ptr(), self.x.data_ptr(), self.recon.data_ptr(), self.sse.data_ptr()
+        if self.fused_loss and self.training:
+            rc.dy, rc.grad_scale = self.g8.data_ptr(), 1.0 / (self.B * 3 * img * img)
+        self._add(F, "vae_recon_fwd", rc)
+
+    def _wide_head_bwd(self, Bw, cnt):
+        """Backward of _wide_head_fwd: [the seed from dL/drecon (drop-in)], data gradient into the final
+        BatchNorm+LeakyReLU backward epilogue (its Σg, Σg·x̂), weight / bias gradient of the padded
+        head, and the padded gradients' first 3 rows added into the parameter gradients."""
+        net, T, img, BS = self.net, self.net.dcode, self.net.img_size, self.B * self.S
+        C = self.fin.shape[-1]
+        if not self.fused_loss:
+            rb = L.ReconArgs(dtype=T, n=BS, h=img, w=img, c=3, ld=8)
+            rb.target, rb.recon = self.x.data_ptr(), self.recon.data_ptr()
+            rb.dy, rb.grad_recon = self.g8.data_ptr(), self.grad_recon.data_ptr()
+            self._add(Bw, "vae_recon_bwd", rb)
+        a = L.ConvArgs(dtype=T, n=BS, h=img, w=img, c=C, k=8, p=img, q=img, r=3, stride=1, pad=1)
+        a.dy = self.g8.data_ptr()
+        a.wt = self.w8h.data_ptr()
+        a.dx = self.g_fin.data_ptr()
+        a.dx_epi = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin), aux=self.fin)
+        self.bwd_sums(a, "final_layer.1")
+        self._add(Bw, "vae_conv2d_bwd_data", a)
+        f = L.ConvArgs(dtype=T, n=BS, h=img, w=img, c=C, k=8, p=img, q=img, r=3, stride=1, pad=1)
+        f.dy = self.g8.data_ptr()
+        f.x = self.fin.data_ptr()
+        f.x_xf = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin))
+        f.dw, f.db = self.dw8h.data_ptr(), self.db8h.data_ptr()
+        self._add(Bw, "vae_conv2d_bwd_filter", f)
+        Bw.append(("vae_unpad_accumulate", (1, 72 * C, 27 * C, self.dw8h.data_ptr(), self.g("final_layer.3.weight"))))
+        Bw.append(("vae_unpad_accumulate", (1, 8, 3, self.db8h.data_ptr(), self.g("final_layer.3.bias"))))
+
     # ------------------------------------------------------------------ execution
     def _run(self, calls, stream):
         run_calls(self, calls, stream)
@@ -710,6 +784,16 @@ class StepPlan:
         if self.fused_loss or not self.training:
             return
         hb, rb = self._head_bwd, self._reparam_bwd
+        if hb is None:               # wide head: its seed is vae_recon_bwd's, from grad_recon
+            if on:                   # dL/drecon of the GPU ELBO: head_coef[n] * (recon - x)
+                S = self.S
+                torch.mul(self.head_coef.view(-1, 1, 1, 1),
+                          self.recon - self.x.repeat_interleave(S, 0) if S > 1 else self.recon - self.x,
+                          out=self.grad_recon)
+                rb.kl_coef = self.kl_coef.data_ptr()
+            else:
+                rb.kl_coef = None
+            return
         if on:
             hb.coef, hb.grad_recon = self.head_coef.data_ptr(), None
             rb.kl_coef = self.kl_coef.data_ptr()
@@ -725,6 +809,9 @@ class StepPlan:
             t.zero_()
         self.dmulv.zero_()
         self.dw8.zero_()
+        if self.wide_head:
+            self.dw8h.zero_()
+            self.db8h.zero_()
 
 
 BATCH_FN = "vae_conv_bwd_filter_batch"
