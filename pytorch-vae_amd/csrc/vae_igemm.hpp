@@ -154,16 +154,29 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
     if (x.kind == VAE_X_BN_DY) t.c[z] = 0.f;
   }
   if (x.table) {
-    // precomputed by vae_bn_finalize: one coalesced copy (all loads of a thread in flight)
+    // precomputed by vae_bn_finalize: one coalesced copy, four channels of a thread per round of
+    // loads (the Autoencoder's 4096-channel tables: 4 rounds, not 16 dependent ones)
     const int C = x.channels;
     const bool dy = x.kind == VAE_X_BN_DY;
-    for (int ch = threadIdx.x; ch < C; ch += blockDim.x) {
-      const float v0 = x.table[ch], v1 = x.table[C + ch];
-      const float v2 = (dy || epi) ? x.table[2 * C + ch] : 0.f;
-      const float v3 = (!dy && epi) ? x.table[3 * C + ch] : 0.f;
-      t.a[ch] = v0; t.b[ch] = v1;
-      if (dy) t.c[ch] = v2;
-      else if (epi) { t.p[ch] = v2; t.q[ch] = v3; }
+    const int nt = blockDim.x;
+    for (int c0 = threadIdx.x; c0 < C; c0 += 4 * nt) {
+      float v[4][4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ch = c0 + u * nt, cc = ch < C ? ch : C - 1;
+        v[u][0] = x.table[cc];
+        v[u][1] = x.table[C + cc];
+        v[u][2] = (dy || epi) ? x.table[2 * C + cc] : 0.f;
+        v[u][3] = (!dy && epi) ? x.table[3 * C + cc] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ch = c0 + u * nt;
+        if (ch >= C) break;
+        t.a[ch] = v[u][0]; t.b[ch] = v[u][1];
+        if (dy) t.c[ch] = v[u][2];
+        else if (epi) { t.p[ch] = v[u][2]; t.q[ch] = v[u][3]; }
+      }
     }
     return;
   }

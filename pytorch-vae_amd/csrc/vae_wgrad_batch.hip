@@ -161,20 +161,43 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   // the batch, 256 -> 103 us, 512 -> 107, 768 -> 126); VAE_WG_GROUP_SLOTS0=0 keeps the
   // standalone plans
   static const int group_slots0 = tune_env("VAE_WG_GROUP_SLOTS0", kCUs);
+  // When a class's output tiles alone exceed that round (the Autoencoder's 1024-2048-channel
+  // layers: thousands of 128 x 128 tiles), the round-share would leave the long-K layers (its
+  // 64 x 64-pixel ConvT: 65536 pixels, 9 tiles) a handful of workgroups each running hundreds of
+  // K-steps behind everything else; there the K slices are sized instead so that every workgroup
+  // of the class runs about the same number of K-steps (the class's work over its tile count,
+  // >= 16 steps of 32 pixels).
   for (int c = group_slots0 > 0 ? 0 : 1; c < kClasses; ++c) {
     const int gs = c == 0 ? group_slots0 : group_slots;
     double macs = 0.0;
+    long tiles_sum = 0, work = 0;
     for (int i = 0; i < n; ++i)
-      if (cls[i] == c) macs += (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
+      if (cls[i] == c) {
+        macs += (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
+        const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
+        const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;
+        tiles_sum += tiles;
+        work += tiles * ks;
+      }
     if (macs <= 0.0) continue;
+    const bool balance = c > 0 && tiles_sum > gs;
+    long kt = balance ? (work + tiles_sum - 1) / tiles_sum : 0;
+    if (kt < 16) kt = 16;
     for (int i = 0; i < n; ++i) {
       if (cls[i] != c) continue;
       const double m = (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
       long slots = (long)(gs * m / macs + 0.5);
+      if (balance) {
+        const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
+        const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;
+        slots = tiles * ((ks + kt - 1) / kt);
+      }
       if (slots < 1) slots = 1;
       WgParams w = plans[i].p;
       w.slab = nullptr;
-      if (int rc = wg2_plan(w, querying() ? workspace : region(i), region_bytes(i), &plans[i], slots)) return rc;
+      // (balanced slices add into dw with atomics: their counts were not in the item's workspace)
+      void* wsi = balance ? nullptr : (querying() ? workspace : region(i));
+      if (int rc = wg2_plan(w, wsi, balance ? 0 : region_bytes(i), &plans[i], slots)) return rc;
       if (wg_class(plans[i]) != c) return fail(VAE_E_UNSUPPORTED, "conv_bwd_filter_batch: replanned class");
     }
   }

@@ -305,7 +305,7 @@ class StepPlan:
     def bn_xf(self, prefix: str, kind: int, count: int, aux=None, running: bool = False,
               table: Optional[bool] = None) -> L.Xform:
         if table is None:
-            table = not self.bn_in_consumer
+            table = not self.bn_in_consumer or self.wide_bn(prefix)
         net = self.net
         C = net.layout.bn_by_prefix[prefix].channels
         s = self.bnfwd[prefix]
@@ -330,6 +330,13 @@ class StepPlan:
             xf.running_var = net.run_var(prefix)
         return xf
 
+    def wide_bn(self, prefix: str) -> bool:
+        """A BatchNorm wider than 512 channels (the Autoencoder's 1024-4096): its coefficient table is
+        built once per step by vae_bn_finalize instead of in every consumer workgroup (the in-kernel
+        build reduces <= 512 channels in one round of loads; wider ones would loop per channel in each
+        of thousands of workgroups)."""
+        return self.bn_in_consumer and self.net.layout.bn_by_prefix[prefix].channels > 512
+
     def fwd_sums(self, arg, prefix: str):
         """Producer side of a BatchNorm's forward statistics (conv / convT fwd epilogue)."""
         s = self.bnfwd[prefix]
@@ -346,7 +353,7 @@ class StepPlan:
         """bn_in_consumer: the weight-gradient call of the conv feeding BatchNorm `prefix` also
         publishes that BatchNorm's dL/dgamma, dL/dbeta and the conv's bias gradient (what
         vae_bn_finalize mode 1 did)."""
-        if not self.bn_in_consumer:
+        if not self.bn_in_consumer or self.wide_bn(prefix):
             return
         xf = arg.dy_xf
         xf.dgamma_out = self.g(prefix + ".weight")
@@ -358,7 +365,7 @@ class StepPlan:
         """Queue vae_bn_finalize for one BatchNorm: mode 0 after the conv producing its input
         (table + running statistics), mode 1 after the kernel producing its backward sums
         (table + dγ, dβ + the producing conv's bias gradient in closed form)."""
-        if self.bn_in_consumer and mode in (0, 1):
+        if self.bn_in_consumer and mode in (0, 1) and not self.wide_bn(prefix):
             return
         C = self.net.layout.bn_by_prefix[prefix].channels
         a = L.BnArgs(mode=mode)
