@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 13
+#define VAE_ABI_VERSION 14
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -165,6 +165,11 @@ typedef struct vae_conv_args {
    * weight rows the bf16 convT2d_fwd / conv2d_bwd_data GEMMs read (vae_swap_axes).  NULL: the
    * call builds it at the end of the workspace first (one extra launch). */
   const void* wt_t;
+  /* bwd_filter: the stored innermost dimension of dw (c of a Conv2d's [k][r][s][c], k of a
+   * ConvTranspose2d's [c][r][s][k]); 0 = all of it.  Smaller: dw is the parameter's own gradient
+   * of an operand zero-padded on that axis (the 8-channel RGB image), indices >= dw_inner are
+   * dropped (bf16 weight-gradient GEMM path only; elsewhere VAE_E_UNSUPPORTED). */
+  int32_t dw_inner;
 } vae_conv_args;
 
 /* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,

@@ -20,6 +20,9 @@ extern "C" int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream) {
       return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
     }
   }
+  if (a->dw_inner > 0 && a->dw_inner < a->k)
+    return fail(VAE_E_UNSUPPORTED, "convT2d_bwd_filter: dw_inner %d < k %d needs the bf16 weight-gradient GEMM path",
+                a->dw_inner, a->k);
   if (!closed &&
       wgrad_ok(a->dtype, a->x_xf, a->dy_xf, (long)a->n * a->h * a->w * a->c, (long)a->n * a->p * a->q * a->k, a->c, a->k)) {
     // bf16 fast path: U = x (input grid, m = c), V = dy (output grid, j = k)

@@ -20,6 +20,9 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
       return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
     }
   }
+  if (a->dw_inner > 0 && a->dw_inner < a->c)
+    return fail(VAE_E_UNSUPPORTED, "conv2d_bwd_filter: dw_inner %d < c %d needs the bf16 weight-gradient GEMM path",
+                a->dw_inner, a->c);
   if (!a->x_nchw_f32 && !closed &&
       wgrad_ok(a->dtype, a->dy_xf, a->x_xf, (long)a->n * a->p * a->q * a->k, (long)a->n * a->h * a->w * a->c, a->k, a->c)) {
     // bf16 fast path: U = dy (output grid, m = k), V = x (input grid, j = c)

@@ -42,6 +42,8 @@ struct WgParams {
   long slab_ld;                      //   (plain stores; wg_slab_reduce adds the slices into dw)
   int own;                           // one K slice: each dW element has one writer, so it is
                                      // accumulated with a plain load + store instead of an atomic
+  int jst;                           // stored j extent of dw (0: J): dW is [M][R][R][jst], j >= jst
+                                     // dropped (vae_conv_args.dw_inner: a zero-padded operand)
 };
 
 template <int BM> constexpr int wg_rs() { return BM == 32 ? 64 : (BM == 64 ? 160 : 288); }
@@ -68,6 +70,7 @@ template <int BM, int BJ> constexpr int wgemm_lds_bytes() { return 2 * wg_kp<BM>
 template <int TM, int TJ>
 __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, const f32x4 (&acc)[TM][TJ], int mrow,
                                             int jcol, long rowstride, long coff) {
+  const int jst = p.jst > 0 ? p.jst : p.J;
   if (!part && p.own) {
     // in groups of fragment rows holding <= 32 values (registers: the 128 x 128 tiles run at 256)
     constexpr int GI = TJ * 4 * TM <= 32 ? TM : (32 / (TJ * 4) > 0 ? 32 / (TJ * 4) : 1);
@@ -81,7 +84,7 @@ __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, cons
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int mm = mrow + (i0 + i) * 16 + e, jj = jcol + j * 16;
-            old[i][j][e] = (mm < p.M && jj < p.J) ? p.dw[mm * rowstride + coff + jj] : 0.f;
+            old[i][j][e] = (mm < p.M && jj < jst) ? p.dw[mm * rowstride + coff + jj] : 0.f;
           }
 #pragma unroll
       for (int i = 0; i < GI; ++i)
@@ -90,7 +93,7 @@ __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, cons
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int mm = mrow + (i0 + i) * 16 + e, jj = jcol + j * 16;
-            if (mm < p.M && jj < p.J) p.dw[mm * rowstride + coff + jj] = old[i][j][e] + acc[i0 + i][j][e];
+            if (mm < p.M && jj < jst) p.dw[mm * rowstride + coff + jj] = old[i][j][e] + acc[i0 + i][j][e];
           }
     }
     return;
@@ -100,7 +103,7 @@ __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, cons
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int jj = jcol + j * 16;
-      if (jj >= p.J) continue;
+      if (jj >= jst) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int mm = mrow + i * 16 + e;
@@ -306,9 +309,10 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, cha
     }
   }
   // D[m][j]: lane holds rows 4g + e of fragment i, column li of fragment j
-  const long rowstride = (long)p.R * p.R * p.J;
+  const int jst = p.jst > 0 ? p.jst : p.J;
+  const long rowstride = (long)p.R * p.R * jst;
   float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
-  wg_epilogue<TM, TJ>(p, part, acc, m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)tap * p.J);
+  wg_epilogue<TM, TJ>(p, part, acc, m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)tap * jst);
 }
 
 template <int BM, int BJ, int XU, int XV>
@@ -537,11 +541,12 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
       if constexpr (NB == 2) buf ^= 1;
     }
   }
-  const long rowstride = (long)TAPS * p.J;
+  const int jst = p.jst > 0 ? p.jst : p.J;
+  const long rowstride = (long)TAPS * jst;
   float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
 #pragma unroll
   for (int t = 0; t < TAPS; ++t)
-    wg_epilogue<TM, TJ>(p, part, acc[t], m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)t * p.J);
+    wg_epilogue<TM, TJ>(p, part, acc[t], m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)t * jst);
 }
 
 template <int BM, int BJ, int XU, int XV, int RR>
@@ -693,7 +698,7 @@ inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots
   const int slab_min = tune_env("VAE_WG_SLAB_MIN", kWgSlabMin);      // read per call (tests lower it)
   p.slab = nullptr;
   p.slab_ld = cols;
-  if (split >= slab_min && split * cols * 4 <= kWgSlabMaxBytes && (ws || querying()) && cols % 4 == 0 &&
+  if (split >= slab_min && split * cols * 4 <= kWgSlabMaxBytes && (ws || querying()) && cols % 4 == 0 && !p.jst &&
       !getenv("VAE_NO_WG_SLAB")) {
     if (!ws_fits(split * cols * 4, ws_bytes, "wgemm K-slice partials")) return VAE_E_BADARG;
     p.slab = static_cast<float*>(ws);
@@ -753,6 +758,7 @@ inline bool conv_wg_params(const vae_conv_args* a, bool transposed, WgParams* w,
     w->n = a->n; w->hu = a->h; w->wu = a->w; w->M = a->c; w->hv = a->p; w->wv = a->q; w->J = a->k;
   }
   w->R = a->r; w->S = a->stride; w->P = a->pad; w->dw = a->dw;
+  w->jst = (a->dw_inner > 0 && a->dw_inner < w->J) ? a->dw_inner : 0;
   w->db = *closed ? a->db : nullptr;
   w->dy_is_v = transposed ? 1 : 0;
   return true;

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -53,7 +53,8 @@ class ConvArgs(ctypes.Structure):
                 ("dy", c_void_p), ("dy_xf", Xform), ("dx", c_void_p), ("dx_epi", Xform),
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
                 ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
-                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("wt_t", c_void_p)]
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("wt_t", c_void_p),
+                ("dw_inner", c_int32)]
 
 
 class LinearArgs(ctypes.Structure):

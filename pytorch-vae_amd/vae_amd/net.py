@@ -220,7 +220,7 @@ class StepPlan:
         # `bn_reps(C)` replicas so that the producing kernels' per-block atomics spread out.
         nbn = sum(4 * bn_reps(b.channels) * b.channels for b in net.layout.bns)
         nz = (_pad4(net.layout.total) + 4 + nbn + _pad4(BS) + _pad4(B * 2 * D) + _pad4(2 * len(net.layout.bns)) +
-              _pad4(h[0] * 9 * 8) + (_pad4(B * 2 * D) if self.latent_fused else 0) +
+              (_pad4(B * 2 * D) if self.latent_fused else 0) +
               (_pad4(8 * 9 * r[-1]) + 8 if self.wide_head else 0))
         self.zero = torch.zeros(nz, **f32)
         o = 0
@@ -237,7 +237,6 @@ class StepPlan:
         self.sse = self.zero[o:o + BS]; o += _pad4(BS)
         self.dmulv = self.zero[o:o + B * 2 * D]; o += _pad4(B * 2 * D)
         self.counters = self.zero[o:o + 2 * len(net.layout.bns)].view(torch.int32); o += _pad4(2 * len(net.layout.bns))
-        self.dw8 = self.zero[o:o + h[0] * 9 * 8]; o += _pad4(h[0] * 9 * 8)       # padded first-conv dW
         if self.latent_fused:       # vae_latent_fc_fwd accumulates mu|log_var: zero at every step
             self.mulv = self.zero[o:o + B * 2 * D].view(B, 2 * D); o += _pad4(B * 2 * D)
         if self.wide_head:          # the padded head's weight / bias gradients (vae_unpad_accumulate)
@@ -663,7 +662,9 @@ class StepPlan:
             f.dy = self.g_enc[i].data_ptr()
             f.dy_xf = dy_xf
             if i == 0 and self.pad_rgb:
-                f.c, f.x, f.dw = 8, self.x8.data_ptr(), self.dw8.data_ptr()
+                # the 8-channel padded image; dW lands in the parameter's own [k][3][3][3] layout
+                # (vaehip.h dw_inner: the weight-gradient GEMM drops the pad channels)
+                f.c, f.x, f.dw, f.dw_inner = 8, self.x8.data_ptr(), self.g("encoder.0.0.weight"), 3
             elif i == 0:
                 f.x_nchw_f32 = 1
                 f.x = self.x.data_ptr()
@@ -674,8 +675,6 @@ class StepPlan:
                 f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form (bn_finalize / bwd_extras)
             self.bwd_extras(f, enc_pre[i])
             self._add(Bw, "vae_conv2d_bwd_filter", f)
-            if i == 0 and self.pad_rgb:
-                Bw.append(("vae_unpad_accumulate", (h[0] * 9, 8, 3, self.dw8.data_ptr(), self.g("encoder.0.0.weight"))))
             if i > 0:
                 a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
                 a.dy = self.g_enc[i].data_ptr()
@@ -810,12 +809,11 @@ class StepPlan:
 
     def reset_backward(self):
         """Zero what the backward accumulates (gradients, BatchNorm-backward sums, d[mu|logvar],
-        the padded first-layer dW) so the backward of the same forward can run again."""
+        the padded head's dW) so the backward of the same forward can run again."""
         self.grads.zero_()
         for t in self.bnbwd.values():
             t.zero_()
         self.dmulv.zero_()
-        self.dw8.zero_()
         if self.wide_head:
             self.dw8h.zero_()
             self.db8h.zero_()

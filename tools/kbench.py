@@ -49,16 +49,17 @@ def main():
     for i in only:
         fn, ref = calls[i]
         for s in splits:
-            if ref is not None and hasattr(ref._obj, "split_k"):
-                ref._obj.split_k = s
+            obj = getattr(ref, "_obj", None)
+            if obj is not None and hasattr(obj, "split_k"):
+                obj.split_k = s
             elif s != 0:
                 continue
             torch.cuda._sleep(1000)                      # marker kernel (spin_kernel)
             for _ in range(args.reps):
                 call_one(fn, ref, sp)
             groups.append({"launch": i, "fn": fn, "split": s})
-            if ref is not None and hasattr(ref._obj, "split_k"):
-                ref._obj.split_k = 0
+            if obj is not None and hasattr(obj, "split_k"):
+                obj.split_k = 0
     torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
