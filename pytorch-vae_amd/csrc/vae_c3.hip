@@ -1,0 +1,546 @@
+// 3x3 / stride-1 / pad-1 convolution on a 16 x 16 grid as an image-tile implicit GEMM: the
+// VQ-VAE's residual-stack convolutions (models/vq_vae.py:57-70, the Conv3x3 layers at :94-166),
+// forward and data gradient (the data gradient of a stride-1 conv is the same correlation with the
+// taps flipped, over the swapped-axes weights).
+//
+//   out[n, h, w, j] = Σ_{r,s,c} A[n, h+dr(r)-1, w+ds(s)-1, c] · B[j][r][s][c]   (+ epilogue)
+//
+// Why not the conv-GEMM (vae_cgemm.hpp): there, a 128 x 128 tile gathers its A rows per tap from
+// L2 — every input element is fetched 9 times and every K-step streams 32 KB for 2.1 MFLOP, at the
+// per-CU L2 bandwidth edge (23-31 % of bf16 peak, 50-55 us per call at B=128).  Here one
+// workgroup owns one whole image (256 output pixels) x 128 output channels: per 32-channel chunk
+// it stages the image's 18 x 18 halo patch once (21 KB) and the chunk's 9 taps x 128 weight rows
+// (74 KB) in LDS, then every tap reads its A fragments from the patch at a shifted row — 18.9
+// MFLOP per 94 KB staged, 3x the reuse of the 128 x 128 tile.
+//
+// Block: 512 threads = 8 waves, wave (wm, wn) = output rows 4wm..4wm+3 (one 16-pixel MFMA row
+// block each) x output channels 64wn..64wn+63; v_mfma_f32_16x16x32_bf16 (lane l: A row l&15 =
+// output column, k 8*(l>>4)..+7; B column l&15; accumulator rows 4*(l>>4)..+3).  LDS rows are
+// 32 bf16 (64 B) with the 16-byte chunk c of row P stored at slot c ^ ((P >> 1) & 2): the lane
+// groups of ds_read_b128 ({0-3,12-15,20-27}, ... — MI355X_MICROARCH.md LDS table) then hit 16
+// distinct 4-bank groups for ANY first row (the A reads start at a tap-shifted patch row); an
+// 80-B padded row measured 48 % of the LDS cycles as bank conflicts (SQ_LDS_BANK_CONFLICT).
+// The next chunk's global loads are issued before the current chunk's MFMAs (register prefetch,
+// 12 x 16 B per thread), so their latency hides behind 144 MFMAs per wave.
+#include "vae_c3.hpp"
+#include "vae_igemm.hpp"
+#include <stdlib.h>
+
+namespace vae {
+namespace {
+
+constexpr int C3_LD = 32;                         // bf16 per LDS operand row (32 channels, swizzled)
+constexpr int C3_PW = 18;                         // halo patch width (16 + 2)
+constexpr int C3_PATCH = C3_PW * C3_PW;           // 324 pixels
+constexpr int C3_BN = 128;                        // output channels per workgroup
+constexpr int C3_A_ITEMS = C3_PATCH * 4;          // 16-byte chunks of the patch (1296)
+constexpr int C3_B_ITEMS = 9 * C3_BN * 4;         // 16-byte chunks of the weight tile (4608)
+constexpr int C3_NT = 512;
+constexpr int C3_AP = (C3_A_ITEMS + C3_NT - 1) / C3_NT;   // 3
+constexpr int C3_BP = C3_B_ITEMS / C3_NT;                 // 9
+constexpr int C3_LDC = C3_BN + 4;                 // fp32 epilogue tile row
+constexpr int C3_OPER_BYTES = (C3_PATCH + 9 * C3_BN) * C3_LD * 2;   // 118080
+constexpr int C3_EPI_BYTES = 256 * C3_LDC * 4;                      // 135168
+constexpr int C3_LDS = C3_OPER_BYTES > C3_EPI_BYTES ? C3_OPER_BYTES : C3_EPI_BYTES;
+static_assert(C3_B_ITEMS % C3_NT == 0, "weight tile loads");
+
+struct C3Params {
+  const void* a;
+  const void* b;
+  void* out;
+  const float* bias;
+  const void* residual;
+  const void* aux;
+  uint32_t a_bytes, b_bytes, o_bytes;
+  float a_slope, aux_slope;
+  int a_act, flip, C, N;
+};
+
+// element offset of 16-byte chunk c of LDS row P (the bank-conflict swizzle above)
+__device__ __forceinline__ int c3_sw(int P, int c) { return P * C3_LD + ((c ^ ((P >> 1) & 2)) << 3); }
+
+__device__ __forceinline__ uint32_t lrelu_pk(uint32_t w, float slope) {
+  f32x2 v = f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+  v = __builtin_elementwise_max(v, v * f32x2{slope, slope});
+  bf16x2 pk;
+  pk[0] = (__bf16)v[0];
+  pk[1] = (__bf16)v[1];
+  return *reinterpret_cast<uint32_t*>(&pk);
+}
+
+__global__ void __launch_bounds__(C3_NT) c3_kernel(const C3Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[C3_LDS];
+  __bf16* As = reinterpret_cast<__bf16*>(smem);                  // [324][40]
+  __bf16* Bs = As + C3_PATCH * C3_LD;                             // [9][128][40]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware order: workgroup b runs on XCD b % 8; each XCD takes a contiguous tile range, so
+  // the two channel tiles of an image share that XCD's L2 copy of the patch
+  const int nt = p.N / C3_BN;
+  int tile;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
+  }
+  const int img = tile / nt, n0 = (tile - img * nt) * C3_BN;
+  const rsrc_t ra = make_rsrc(p.a, p.a_bytes);
+  const rsrc_t rb = make_rsrc(p.b, p.b_bytes);
+  const int C = p.C;
+
+  // per-thread load slots: A patch chunk (pixel, 16-B column) and weight row chunk
+  uint32_t abase[C3_AP];
+  bool aok[C3_AP];
+#pragma unroll
+  for (int k = 0; k < C3_AP; ++k) {
+    const int it = tid + C3_NT * k;
+    const int pix = it >> 2, ch = it & 3;
+    const int ph = pix / C3_PW, pw = pix - ph * C3_PW;
+    const int h = ph - 1, w = pw - 1;
+    aok[k] = it < C3_A_ITEMS && (unsigned)h < 16u && (unsigned)w < 16u;
+    abase[k] = (uint32_t)((((img * 16 + (aok[k] ? h : 0)) * 16 + (aok[k] ? w : 0)) * C + ch * 8) * 2);
+  }
+  uint32_t bbase[C3_BP];
+#pragma unroll
+  for (int k = 0; k < C3_BP; ++k) {
+    const int it = tid + C3_NT * k;
+    const int row = it >> 2, ch = it & 3;
+    const int t = row >> 7, nl = row & (C3_BN - 1);
+    bbase[k] = (uint32_t)((((n0 + nl) * 9 + t) * C + ch * 8) * 2);
+  }
+  uint32_t ar[C3_AP][4], br[C3_BP][4];
+  auto load = [&](int c0) {
+    const uint32_t cb = (uint32_t)c0 * 2u;
+#pragma unroll
+    for (int k = 0; k < C3_AP; ++k) bload<16>(ra, aok[k] ? abase[k] + cb : kOOB, ar[k]);
+#pragma unroll
+    for (int k = 0; k < C3_BP; ++k) bload<16>(rb, bbase[k] + cb, br[k]);
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < C3_AP; ++k) {
+      const int it = tid + C3_NT * k;
+      if (it < C3_A_ITEMS) {
+        uint4 v = uint4{ar[k][0], ar[k][1], ar[k][2], ar[k][3]};
+        if (p.a_act) {
+          v.x = lrelu_pk(v.x, p.a_slope); v.y = lrelu_pk(v.y, p.a_slope);
+          v.z = lrelu_pk(v.z, p.a_slope); v.w = lrelu_pk(v.w, p.a_slope);
+        }
+        *reinterpret_cast<uint4*>(As + c3_sw(it >> 2, it & 3)) = v;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < C3_BP; ++k) {
+      const int it = tid + C3_NT * k;
+      *reinterpret_cast<uint4*>(Bs + c3_sw(it >> 2, it & 3)) = uint4{br[k][0], br[k][1], br[k][2], br[k][3]};
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kq = lane >> 4, lr = lane & 15;
+  // the fragments of tap t+1 are read from LDS while tap t's 16 MFMAs run (their latency was
+  // exposed at the head of every tap)
+  auto frags = [&](int t, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
+    const int r = t / 3, s = t - 3 * (t / 3);
+    const int dr = p.flip ? 2 - r : r, ds = p.flip ? 2 - s : s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(As + c3_sw((wm * 4 + i + dr) * C3_PW + lr + ds, kq));
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + c3_sw(t * C3_BN + wn * 64 + j * 16 + lr, kq));
+  };
+  auto compute = [&]() {
+    bf16x8 af[2][4], bfr[2][4];
+    frags(0, af[0], bfr[0]);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // this tap's fragments (read during the previous tap) have landed: one wait here, so the
+      // next tap's reads issued between the MFMAs below need none (lgkmcnt counts in order)
+      __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < 9) frags(t + 1, af[(t + 1) & 1], bfr[(t + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t & 1][i], bfr[t & 1][j], acc[i][j], 0, 0, 0);
+      if (t + 1 < 9) {
+        // interleave: 2 MFMAs, then one of the next tap's 8 LDS reads (the scheduler otherwise
+        // sinks the reads to their first use)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+    }
+  };
+
+  const int nchunks = C / 32;
+  load(0);
+  store();
+  __syncthreads();
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const bool more = kc + 1 < nchunks;
+    // unconditional (the last chunk reloads itself, unused): a load under a branch makes the
+    // compiler merge the prefetch registers with copies that wait for the loads right here,
+    // before the MFMAs they were meant to hide behind
+    load((more ? kc + 1 : kc) * 32);
+    __builtin_amdgcn_sched_barrier(0);      // (keep the loads ahead of the MFMAs)
+    compute();
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue through LDS: fp32 tile [256 pixels][128 (+4)], then 16-byte rows
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[((wm * 4 + i) * 16 + 4 * (lane >> 4) + e) * C3_LDC + wn * 64 + j * 16 + lr] = acc[i][j][e];
+  __syncthreads();
+  const rsrc_t rres = make_rsrc(p.residual ? p.residual : p.out, p.residual ? p.o_bytes : 0u);
+  const rsrc_t raux = make_rsrc(p.aux ? p.aux : p.out, p.aux ? p.o_bytes : 0u);
+  __bf16* out = static_cast<__bf16*>(p.out);
+#pragma unroll 2
+  for (int k = 0; k < 8; ++k) {
+    const int it = tid + C3_NT * k;
+    const int pix = it >> 4, cg = (it & 15) * 8;
+    const uint32_t o = (uint32_t)((img * 256 + pix) * p.N + n0 + cg);
+    uint32_t rs[4], ax[4];
+    bload<16>(rres, p.residual ? o * 2u : kOOB, rs);
+    bload<16>(raux, p.aux ? o * 2u : kOOB, ax);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + pix * C3_LDC + cg);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + pix * C3_LDC + cg + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    uint32_t pk[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float g0 = v[2 * e] + __uint_as_float(rs[e] << 16);
+      float g1 = v[2 * e + 1] + __uint_as_float(rs[e] & 0xffff0000u);
+      if (p.bias) { g0 += p.bias[n0 + cg + 2 * e]; g1 += p.bias[n0 + cg + 2 * e + 1]; }
+      if (p.aux) {
+        if (!(__uint_as_float(ax[e] << 16) > 0.f)) g0 *= p.aux_slope;
+        if (!(__uint_as_float(ax[e] & 0xffff0000u) > 0.f)) g1 *= p.aux_slope;
+      }
+      bf16x2 h;
+      h[0] = (__bf16)g0;
+      h[1] = (__bf16)g1;
+      pk[e] = *reinterpret_cast<uint32_t*>(&h);
+    }
+    *reinterpret_cast<uint4*>(out + o) = uint4{pk[0], pk[1], pk[2], pk[3]};
+  }
+}
+
+// ------------------------------------------------------------------ weight gradient
+//   dW[m][r][s][c] += Σ_{n,h,w} U[n,h,w,m] · V'[n, h+r-1, w+s-1, c]     (U = dy, V' = xf(x))
+// One workgroup: 128 m x 32 c x all 9 taps over a group of G images.  Per image it stages U
+// ([256 pixels][128 m], 288-B rows) and V's 18 x 18 halo patch ([324][32 c], 64-B rows) once, and
+// every tap reads its B fragments from the patch at a shifted pixel — the per-tap weight-gradient
+// GEMM (vae_wgemm.hpp) gathered V from L2 once per tap.  6 waves: wave (jh, r) = m rows 64jh..+63
+// (4 A fragments, reused by all 3 taps of its tap row) x the 32 c x taps (r, 0..2): 24 MFMAs per
+// 20 transposed LDS reads per 32-pixel K-step.  Operands are [pixel][channel] in LDS; the
+// K = pixel direction is read with ds_read_b64_tr_b16 (vae_wgemm.hpp).  Each workgroup writes its
+// partial dW tile to slab slice `group` (plain stores); c3w_reduce adds the slices into dW.
+typedef __bf16 __attribute__((ext_vector_type(4))) __attribute__((address_space(3))) w3_lds_bf16x4;
+typedef __bf16 w3_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ w3_bf16x4 w3_tr_read(const char* generic_lds_addr) {
+  const uint32_t off = (uint32_t)(uintptr_t)generic_lds_addr;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((w3_lds_bf16x4*)(uintptr_t)off);
+}
+
+constexpr int W3_NT = 384;
+constexpr int W3_BM = 128, W3_BC = 32;
+// LDS rows: U 256 B with its 32-byte slots XOR-swizzled by (P & 3) | ((P >> 1) & 4), V 64 B with
+// slots swizzled by (P >> 3) & 1: the 32-lane groups of ds_read_b64_tr_b16 read pixel rows
+// {0-3, 8-11} (+4) of a block, which then fall in 8 distinct 8-bank windows (a 288-B padded U row
+// left rows r and r+8 on the same banks: 42 % of the LDS cycles were conflicts)
+constexpr int W3_URS = 256, W3_VRS = 64;                  // LDS row bytes
+constexpr int W3_U_BYTES = 256 * W3_URS;                  // 65536
+constexpr int W3_V_BYTES = C3_PATCH * W3_VRS;             // 20736
+constexpr int W3_UI = 256 * (W3_BM / 8);                  // 16-B chunks of a U tile (4096)
+constexpr int W3_VI = C3_PATCH * (W3_BC / 8);             // of a V patch (1296)
+constexpr int W3_UP = (W3_UI + W3_NT - 1) / W3_NT;        // 11
+constexpr int W3_VP = (W3_VI + W3_NT - 1) / W3_NT;        // 4
+
+// byte offset of 32-byte slot c of LDS row P (U tile / V patch), with the swizzles above
+__device__ __forceinline__ int w3_usw(int P, int c) { return P * W3_URS + ((c ^ ((P & 3) | ((P >> 1) & 4))) << 5); }
+__device__ __forceinline__ int w3_vsw(int P, int c) { return P * W3_VRS + ((c ^ ((P >> 3) & 1)) << 5); }
+
+struct W3Params {
+  const void* u;
+  const void* v;
+  float* slab;
+  long slab_ld;
+  uint32_t u_bytes, v_bytes;
+  float v_slope;
+  int v_act, n, M, J, G;
+};
+
+__global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[W3_U_BYTES + W3_V_BYTES];
+  char* const Us = smem;
+  char* const Vs = smem + W3_U_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int jh = wave & 1, tr = wave >> 1;
+  const int ntc = p.J / W3_BC, per = (p.M / W3_BM) * ntc;
+  int tile;
+  {
+    // XCD-aware order (workgroup b on XCD b % 8): contiguous ranges are image-group major, so
+    // the tiles reading the same images share an XCD's L2
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
+  }
+  const int grp = tile / per, rem = tile - grp * per;
+  const int tj = rem / ntc, tc = rem - tj * ntc;
+  const int j0 = tj * W3_BM, c0 = tc * W3_BC;
+  const int img0 = grp * p.G, img1 = min(p.n, img0 + p.G);
+  const rsrc_t ru = make_rsrc(p.u, p.u_bytes);
+  const rsrc_t rv = make_rsrc(p.v, p.v_bytes);
+
+  uint32_t ubase[W3_UP], vbase[W3_VP];
+  bool vok[W3_VP];
+#pragma unroll
+  for (int k = 0; k < W3_UP; ++k) {
+    const int it = min(tid + W3_NT * k, W3_UI - 1);
+    ubase[k] = (uint32_t)(((it >> 4) * p.M + j0 + (it & 15) * 8) * 2);
+  }
+#pragma unroll
+  for (int k = 0; k < W3_VP; ++k) {
+    const int it = tid + W3_NT * k;
+    const int pix = it >> 2, ph = pix / C3_PW, pw = pix - ph * C3_PW;
+    const int h = ph - 1, w = pw - 1;
+    vok[k] = it < W3_VI && (unsigned)h < 16u && (unsigned)w < 16u;
+    vbase[k] = vok[k] ? (uint32_t)(((h * 16 + w) * p.J + c0 + (it & 3) * 8) * 2) : 0u;
+  }
+  uint32_t ur[W3_UP][4], vr[W3_VP][4];
+  auto load = [&](int img) {
+    const uint32_t uo = (uint32_t)img * 256u * (uint32_t)p.M * 2u, vo = (uint32_t)img * 256u * (uint32_t)p.J * 2u;
+#pragma unroll
+    for (int k = 0; k < W3_UP; ++k) bload<16>(ru, ubase[k] + uo, ur[k]);
+#pragma unroll
+    for (int k = 0; k < W3_VP; ++k) bload<16>(rv, vok[k] ? vbase[k] + vo : kOOB, vr[k]);
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < W3_UP; ++k) {
+      const int it = tid + W3_NT * k;
+      if (it < W3_UI)
+        *reinterpret_cast<uint4*>(Us + w3_usw(it >> 4, (it & 15) >> 1) + (it & 1) * 16) = uint4{ur[k][0], ur[k][1], ur[k][2], ur[k][3]};
+    }
+#pragma unroll
+    for (int k = 0; k < W3_VP; ++k) {
+      const int it = tid + W3_NT * k;
+      if (it < W3_VI) {
+        uint4 v = uint4{vr[k][0], vr[k][1], vr[k][2], vr[k][3]};
+        if (p.v_act) {
+          v.x = lrelu_pk(v.x, p.v_slope); v.y = lrelu_pk(v.y, p.v_slope);
+          v.z = lrelu_pk(v.z, p.v_slope); v.w = lrelu_pk(v.w, p.v_slope);
+        }
+        *reinterpret_cast<uint4*>(Vs + w3_vsw(it >> 2, (it & 3) >> 1) + (it & 1) * 16) = v;
+      }
+    }
+  };
+
+  f32x4 acc[4][2][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) acc[i][cb][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read addresses: lane 4q+p of 16-lane group g reads K rows 8g+4h+q, columns 4p..4p+3
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  int aoff[4][2], prow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q4;                      // pixel within a 32-pixel K block
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i][h] = w3_usw(row, jh * 4 + i) + 8 * p4;       // (row & 15 fixed over kb)
+    // K block kb = output rows 2kb, 2kb+1; this lane's pixel: output (2kb + (g >> 1), 8(g & 1) + 4h + q)
+    // -> patch pixel (2kb + (g >> 1) + r, 8(g & 1) + 4h + q + s)
+    prow[h] = ((g >> 1) + tr) * C3_PW + 8 * (g & 1) + 4 * h + q4;
+  }
+  auto afrag = [&](int kb, bf16x8 (&af)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const w3_bf16x4 a0 = w3_tr_read(Us + kb * 32 * W3_URS + aoff[i][0]);
+      const w3_bf16x4 a1 = w3_tr_read(Us + kb * 32 * W3_URS + aoff[i][1]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+    }
+  };
+  auto bfrag = [&](int kb, int s, bf16x8 (&bfr)[2]) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int P0 = prow[0] + kb * 2 * C3_PW + s, P1 = prow[1] + kb * 2 * C3_PW + s;
+      const w3_bf16x4 b0 = w3_tr_read(Vs + w3_vsw(P0, cb) + 8 * p4);
+      const w3_bf16x4 b1 = w3_tr_read(Vs + w3_vsw(P1, cb) + 8 * p4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bfr[cb][e] = b0[e]; bfr[cb][4 + e] = b1[e]; }
+    }
+  };
+  // 24 steps (K block kb, tap column s); the next step's B fragments are read between this step's
+  // 8 MFMAs after one wait at the step's head (as c3_kernel); A once per K block
+  auto compute = [&]() {
+    bf16x8 af[4], bfr[2][2];
+    bfrag(0, 0, bfr[0]);
+#pragma unroll 1
+    for (int kb = 0; kb < 8; ++kb) {
+      afrag(kb, af);                                       // (one exposed read per K block)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        // next step's B: (kb, s+1), or (kb+1, 0) — past the end a harmless re-read of block 7
+        bfrag(s < 2 ? kb : min(kb + 1, 7), s < 2 ? s + 1 : 0, bfr[(s + 1) & 1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            acc[i][cb][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s & 1][cb], acc[i][cb][s], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+      // (3 steps per K block: step s = 2 filled bfr[1] for the next block's s = 0 — swap roles)
+      bfr[0][0] = bfr[1][0]; bfr[0][1] = bfr[1][1];
+    }
+  };
+
+  load(img0);
+  store();
+  __syncthreads();
+  for (int img = img0; img < img1; ++img) {
+    const bool more = img + 1 < img1;
+    load(more ? img + 1 : img);                // (unconditional: see c3_kernel)
+    __builtin_amdgcn_sched_barrier(0);
+    compute();
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  // partial tile -> slab slice grp: lane holds rows 4g+e of fragment i (m), column li of fragment cb (c)
+  float* part = p.slab + (long)grp * p.slab_ld;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = j0 + jh * 64 + i * 16 + 4 * g + e;
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          part[((long)m * 9 + tr * 3 + s) * p.J + c0 + cb * 16 + li] = acc[i][cb][s][e];
+    }
+}
+
+// dw[i] += Σ_s slab[s * ld + i] (each element one writer), 4 consecutive floats per thread
+__global__ void __launch_bounds__(256) c3w_reduce(const float* slab, long ld, int slices, long cols, float* dw) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= cols) return;
+  f32x4 s = *reinterpret_cast<const f32x4*>(slab + i);
+  for (int k = 1; k < slices; ++k) s += *reinterpret_cast<const f32x4*>(slab + (long)k * ld + i);
+  f32x4 d;
+  d[0] = dw[i]; d[1] = dw[i + 1]; d[2] = dw[i + 2]; d[3] = dw[i + 3];     // (parameter slices: 4-B aligned)
+  d += s;
+  dw[i] = d[0]; dw[i + 1] = d[1]; dw[i + 2] = d[2]; dw[i + 3] = d[3];
+}
+
+inline void c3w_plan(int n, int M, int J, int* G, int* groups) {
+  const int tiles = (M / W3_BM) * (J / W3_BC);
+  int ng = 256 / tiles;
+  if (ng < 1) ng = 1;
+  if (ng > n) ng = n;
+  *G = (n + ng - 1) / ng;
+  *groups = (n + *G - 1) / *G;
+}
+
+inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+
+}  // namespace
+
+bool c3_enabled() {
+  static const bool on = !getenv("VAE_NO_C3");
+  return on;
+}
+
+bool c3_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int C, int N) {
+  return n > 0 && h == 16 && w == 16 && p == 16 && q == 16 && r == 3 && stride == 1 && pad == 1 && C % 32 == 0 &&
+         C >= 32 && N % C3_BN == 0 && N > 0 && (long)n * 256 * (C > N ? C : N) * 2 < (1l << 31);
+}
+
+int c3_launch(const C3Args& a, hipStream_t st) {
+  if (!c3_shape_ok(a.n, 16, 16, 16, 16, 3, 1, 1, a.C, a.N)) return fail(VAE_E_BADSHAPE, "c3: shape");
+  if (!al16(a.a) || !al16(a.b) || !al16(a.out) || (a.residual && !al16(a.residual)) || (a.aux && !al16(a.aux)))
+    return fail(VAE_E_BADARG, "c3: tensors must be 16-byte aligned");
+  C3Params p;
+  p.a = a.a; p.b = a.b; p.out = a.out; p.bias = a.bias; p.residual = a.residual; p.aux = a.aux;
+  p.a_bytes = (uint32_t)((long)a.n * 256 * a.C * 2);
+  p.b_bytes = (uint32_t)((long)a.N * 9 * a.C * 2);
+  p.o_bytes = (uint32_t)((long)a.n * 256 * a.N * 2);
+  p.a_slope = a.a_slope; p.aux_slope = a.aux_slope;
+  p.a_act = a.a_act; p.flip = a.flip; p.C = a.C; p.N = a.N;
+  const unsigned grid = (unsigned)(a.n * (a.N / C3_BN));
+  VAE_LAUNCH(c3_kernel, dim3(grid), dim3(C3_NT), 0, st, p);
+  return check_launch("c3");
+}
+
+}  // namespace vae
+
+namespace vae {
+
+bool c3w_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int M, int J) {
+  return n > 0 && h == 16 && w == 16 && p == 16 && q == 16 && r == 3 && stride == 1 && pad == 1 && M % W3_BM == 0 &&
+         J % W3_BC == 0 && (long)n * 256 * (M > J ? M : J) * 2 < (1l << 31);
+}
+
+long c3w_workspace(int n, int M, int J) {
+  int G, groups;
+  c3w_plan(n, M, J, &G, &groups);
+  return (long)groups * M * 9 * J * 4;
+}
+
+int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st) {
+  if (!c3w_shape_ok(a.n, 16, 16, 16, 16, 3, 1, 1, a.M, a.J)) return fail(VAE_E_BADSHAPE, "c3w: shape");
+  if (!al16(a.u) || !al16(a.v) || ((uintptr_t)a.dw & 3u)) return fail(VAE_E_BADARG, "c3w: alignment");
+  W3Params p;
+  int groups;
+  c3w_plan(a.n, a.M, a.J, &p.G, &groups);
+  const long cols = (long)a.M * 9 * a.J;
+  if (!ws_fits((long)groups * cols * 4, ws ? ws_bytes : 0, "c3w slab")) return VAE_E_BADARG;
+  p.u = a.u; p.v = a.v; p.slab = static_cast<float*>(ws); p.slab_ld = cols;
+  p.u_bytes = (uint32_t)((long)a.n * 256 * a.M * 2);
+  p.v_bytes = (uint32_t)((long)a.n * 256 * a.J * 2);
+  p.v_act = a.v_act; p.v_slope = a.v_slope;
+  p.n = a.n; p.M = a.M; p.J = a.J;
+  const unsigned grid = (unsigned)(groups * (a.M / W3_BM) * (a.J / W3_BC));
+  VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
+  if (int rc = check_launch("c3w")) return rc;
+  VAE_LAUNCH(c3w_reduce, dim3((unsigned)((cols / 4 + 255) / 256)), dim3(256), 0, st, (const float*)p.slab, cols, groups,
+             cols, a.dw);
+  return check_launch("c3w_reduce");
+}
+
+}  // namespace vae

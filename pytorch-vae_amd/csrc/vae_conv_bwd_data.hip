@@ -1,6 +1,7 @@
 // C-ABI entry points of Conv2d (encoder blocks, models/vanilla_vae.py:28-29 run at :84).
 #include "vae_launch.hpp"
 #include "vae_wgrad.hpp"
+#include "vae_c3.hpp"
 
 using namespace vae;
 
@@ -14,6 +15,19 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   if (a->h % S || a->w % S || a->h / S != a->p || a->w / S != a->q)
     return fail(VAE_E_BADSHAPE, "conv2d_bwd_data: needs h == p*stride (got h=%d p=%d S=%d)", a->h, a->p, S);
   const long wbytes = (long)a->k * a->r * a->r * a->c * 2;
+  // 3x3 stride-1 on a 16 x 16 grid (the VQ-VAE's residual stacks): the image-tile kernel, taps
+  // flipped, over the caller's swapped-axes weights WT[c][r][s][k]
+  if (a->dtype == VAE_BF16 && a->wt_t && c3_enabled() &&
+      c3_shape_ok(a->n, a->p, a->q, a->h, a->w, a->r, a->stride, a->pad, a->k, a->c) &&
+      a->dy_xf.kind == VAE_X_NONE && (a->dx_epi.kind == VAE_X_NONE || a->dx_epi.kind == VAE_X_ACT) &&
+      !a->dx_dgamma && !a->bn_finalize && a->split_k <= 0) {
+    C3Args c;
+    memset(&c, 0, sizeof(c));
+    c.a = a->dy; c.b = a->wt_t; c.flip = 1; c.out = a->dx; c.residual = a->residual;
+    if (a->dx_epi.kind == VAE_X_ACT) { c.aux = a->dx_epi.aux; c.aux_slope = a->dx_epi.slope; }
+    c.n = a->n; c.C = a->k; c.N = a->c;
+    return c3_launch(c, (hipStream_t)stream);
+  }
   if (a->dtype == VAE_BF16) {
     // bf16 conv-GEMM: phase gather of dy (any stride; stride 1 is one phase of R*R taps) against
     // the swapped-axes weights WT[c][r][s][k] (caller's wt_t, or built at the workspace's end)

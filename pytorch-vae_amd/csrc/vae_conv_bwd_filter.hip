@@ -2,6 +2,7 @@
 #include "vae_launch.hpp"
 #include "vae_wgrad.hpp"
 #include "vae_wgemm.hpp"
+#include "vae_c3.hpp"
 
 using namespace vae;
 
@@ -10,6 +11,19 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "conv2d_bwd_filter") || !a->dy || !a->x || !a->dw) return fail(VAE_E_BADARG, "conv2d_bwd_filter: null tensor");
   if (!xf_ok(a->dy_xf, "conv2d_bwd_filter.dy") || !xf_ok(a->x_xf, "conv2d_bwd_filter.x")) return VAE_E_BADARG;
   const bool closed = a->db && a->dy_xf.kind == VAE_X_BN_DY;   // Σdy from the BN sums
+  // 3x3 stride-1 on a 16 x 16 grid (the VQ-VAE's residual stacks): image-group tiles with the
+  // halo patch staged once per image (vae_c3.hip); needs a workspace for the partial slabs
+  if (a->dtype == VAE_BF16 && !a->x_nchw_f32 && c3_enabled() && (a->workspace || querying()) &&
+      c3w_shape_ok(a->n, a->h, a->w, a->p, a->q, a->r, a->stride, a->pad, a->k, a->c) &&
+      a->dy_xf.kind == VAE_X_NONE && (a->x_xf.kind == VAE_X_NONE || a->x_xf.kind == VAE_X_ACT) &&
+      (a->dw_inner <= 0 || a->dw_inner == a->c)) {
+    C3WArgs c;
+    c.u = a->dy; c.v = a->x; c.v_act = a->x_xf.kind == VAE_X_ACT; c.v_slope = a->x_xf.slope;
+    c.dw = static_cast<float*>(a->dw); c.n = a->n; c.M = a->k; c.J = a->c;
+    int rc = c3w_launch(c, a->workspace, a->workspace_bytes, (hipStream_t)stream);
+    if (rc || !a->db) return rc;
+    return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
+  }
   {
     // bf16 weight-gradient GEMM (vae_wgemm.hpp)
     WgParams w;

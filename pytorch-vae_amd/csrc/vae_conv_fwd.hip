@@ -1,6 +1,7 @@
 // C-ABI entry points of Conv2d (encoder blocks, models/vanilla_vae.py:28-29 run at :84).
 #include "vae_launch.hpp"
 #include "vae_wgrad.hpp"
+#include "vae_c3.hpp"
 
 using namespace vae;
 
@@ -8,6 +9,18 @@ using namespace vae;
 extern "C" int vae_conv2d_fwd(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "conv2d_fwd") || !a->x || !a->wt || !a->y) return fail(VAE_E_BADARG, "conv2d_fwd: null tensor");
   if (!xf_ok(a->x_xf, "conv2d_fwd.x")) return VAE_E_BADARG;
+  // 3x3 stride-1 convs on a 16 x 16 grid (the VQ-VAE's residual stacks): image-tile kernel
+  if (a->dtype == VAE_BF16 && !a->x_nchw_f32 && c3_enabled() &&
+      c3_shape_ok(a->n, a->h, a->w, a->p, a->q, a->r, a->stride, a->pad, a->c, a->k) &&
+      (a->x_xf.kind == VAE_X_NONE || a->x_xf.kind == VAE_X_ACT) && !a->y_sum && !a->y_sumsq && !a->residual &&
+      !a->bn_finalize && a->split_k <= 0) {
+    C3Args c;
+    memset(&c, 0, sizeof(c));
+    c.a = a->x; c.a_act = a->x_xf.kind == VAE_X_ACT; c.a_slope = a->x_xf.slope;
+    c.b = a->wt; c.flip = 0; c.out = a->y; c.bias = a->bias;
+    c.n = a->n; c.C = a->c; c.N = a->k;
+    return c3_launch(c, (hipStream_t)stream);
+  }
   GemmParams p = base_params();
   p.M = a->n * a->p * a->q; p.N = a->k; p.K = a->r * a->r * a->c;
   p.a_ptr = a->x; p.a_xf = sanitize(a->x_xf); p.g_nchw = a->x_nchw_f32;

@@ -1,0 +1,113 @@
+"""The image-tile 3x3 convolution (csrc/vae_c3.hip: stride 1, pad 1, 16 x 16 grid — the VQ-VAE's
+residual stacks, vq_vae.py:57-70 and the Conv3x3 layers at :94-166) through the C ABI
+(vae_conv2d_fwd / vae_conv2d_bwd_data pick it for these shapes in bf16) vs PyTorch-CPU fp32 on the
+same bf16-rounded operands.  Tolerance 1e-2 max-relative: fp32 accumulation, bf16 output."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gpu_util import give_workspace, nhwc, rel, to_nchw
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-2
+
+
+def _bf(t):
+    return t.bfloat16().float()
+
+
+@pytest.mark.parametrize("n,cin,cout,act,bias", [(4, 256, 256, True, False), (3, 64, 256, False, True),
+                                                 (9, 32, 128, True, True), (2, 128, 384, False, False)])
+def test_c3_forward(n, cin, cout, act, bias):
+    from vae_amd import _lib as L
+    torch.manual_seed(11)
+    x = _bf(torch.randn(n, cin, 16, 16))
+    w = _bf(torch.randn(cout, cin, 3, 3) * (1.0 / (3 * cin ** 0.5)))
+    b = torch.randn(cout) * 0.1 if bias else None
+    ref = F.conv2d(F.leaky_relu(x, 0.01) if act else x, w, b, padding=1)
+    xd = nhwc(x, torch.bfloat16)
+    wd = w.permute(0, 2, 3, 1).contiguous().to("cuda", torch.bfloat16)
+    bd = b.cuda() if bias else None
+    out = torch.empty(n, 16, 16, cout, device="cuda", dtype=torch.bfloat16)
+    a = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=cin, k=cout, p=16, q=16, r=3, stride=1, pad=1)
+    a.x, a.wt, a.y = xd.data_ptr(), wd.data_ptr(), out.data_ptr()
+    if act:
+        a.x_xf = L.Xform(kind=L.X_ACT, channels=cin, slope=0.01)
+    if bias:
+        a.bias = bd.data_ptr()
+    L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel(to_nchw(out), ref) < TOL
+
+
+@pytest.mark.parametrize("n,cin,cout,res,act", [(4, 256, 256, True, True), (3, 256, 64, True, False),
+                                                (5, 128, 128, False, True)])
+def test_c3_backward_data(n, cin, cout, res, act):
+    """dx = conv2d's input gradient (+ skip gradient) * lrelu'(x0) — the ResidualLayer backward."""
+    from vae_amd import _lib as L
+    torch.manual_seed(12)
+    x = torch.randn(n, cin, 16, 16, requires_grad=True)
+    w = _bf(torch.randn(cout, cin, 3, 3) * (1.0 / (3 * cin ** 0.5)))
+    y = F.conv2d(x, w, padding=1)
+    gy = _bf(torch.randn_like(y))
+    y.backward(gy)
+    ref = x.grad.clone()
+    r = _bf(torch.randn(n, cin, 16, 16)) if res else None
+    aux = _bf(torch.randn(n, cin, 16, 16)) if act else None
+    if res:
+        ref = ref + r
+    if act:
+        ref = torch.where(aux > 0, ref, ref * 0.01)
+    gyd = nhwc(gy, torch.bfloat16)
+    wt = w.permute(1, 2, 3, 0).contiguous().to("cuda", torch.bfloat16)          # WT[c][r][s][k]
+    wd = w.permute(0, 2, 3, 1).contiguous().to("cuda", torch.bfloat16)
+    dx = torch.empty(n, 16, 16, cin, device="cuda", dtype=torch.bfloat16)
+    a = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=cin, k=cout, p=16, q=16, r=3, stride=1, pad=1)
+    a.dy, a.wt, a.wt_t, a.dx = gyd.data_ptr(), wd.data_ptr(), wt.data_ptr(), dx.data_ptr()
+    keep = []
+    if res:
+        rd = nhwc(r, torch.bfloat16)
+        keep.append(rd)
+        a.residual = rd.data_ptr()
+    if act:
+        ad = nhwc(aux, torch.bfloat16)
+        keep.append(ad)
+        a.dx_epi = L.Xform(kind=L.X_ACT, channels=cin, slope=0.01, aux=ad.data_ptr())
+    L.call("vae_conv2d_bwd_data", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel(to_nchw(dx), ref) < TOL
+
+
+@pytest.mark.parametrize("n,cin,cout,act,bias", [(8, 256, 256, True, False), (5, 64, 256, False, True),
+                                                 (3, 32, 128, True, True)])
+def test_c3_backward_filter(n, cin, cout, act, bias):
+    """dW (accumulated onto a nonzero start) and db of a 3x3 stride-1 conv on a 16 x 16 grid."""
+    from vae_amd import _lib as L
+    torch.manual_seed(13)
+    x = _bf(torch.randn(n, cin, 16, 16))
+    w = torch.zeros(cout, cin, 3, 3, requires_grad=True)
+    b = torch.zeros(cout, requires_grad=True)
+    y = F.conv2d(F.leaky_relu(x, 0.01) if act else x, w, b, padding=1)
+    gy = _bf(torch.randn_like(y))
+    y.backward(gy)
+    dw0 = torch.randn(cout, 3, 3, cin) * 0.1
+    xd = nhwc(x, torch.bfloat16)
+    gyd = nhwc(gy, torch.bfloat16)
+    dw = dw0.clone().cuda()
+    db = torch.zeros(cout, device="cuda")
+    a = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=cin, k=cout, p=16, q=16, r=3, stride=1, pad=1)
+    a.x, a.dy, a.dw = xd.data_ptr(), gyd.data_ptr(), dw.data_ptr()
+    if act:
+        a.x_xf = L.Xform(kind=L.X_ACT, channels=cin, slope=0.01)
+    if bias:
+        a.db = db.data_ptr()
+    ws = give_workspace(a, "vae_conv2d_bwd_filter")
+    L.call("vae_conv2d_bwd_filter", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    del ws
+    got = (dw.cpu() - dw0).permute(0, 3, 1, 2)
+    assert rel(got, w.grad) < 2e-3
+    if bias:
+        assert rel(db.cpu(), b.grad) < 2e-3
