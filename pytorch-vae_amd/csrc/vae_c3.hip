@@ -32,17 +32,22 @@ namespace {
 constexpr int C3_LD = 32;                         // bf16 per LDS operand row (32 channels, swizzled)
 constexpr int C3_PW = 18;                         // halo patch width (16 + 2)
 constexpr int C3_PATCH = C3_PW * C3_PW;           // 324 pixels
-constexpr int C3_BN = 128;                        // output channels per workgroup
 constexpr int C3_A_ITEMS = C3_PATCH * 4;          // 16-byte chunks of the patch (1296)
-constexpr int C3_B_ITEMS = 9 * C3_BN * 4;         // 16-byte chunks of the weight tile (4608)
-constexpr int C3_NT = 512;
-constexpr int C3_AP = (C3_A_ITEMS + C3_NT - 1) / C3_NT;   // 3
-constexpr int C3_BP = C3_B_ITEMS / C3_NT;                 // 9
-constexpr int C3_LDC = C3_BN + 4;                 // fp32 epilogue tile row
-constexpr int C3_OPER_BYTES = (C3_PATCH + 9 * C3_BN) * C3_LD * 2;   // 118080
-constexpr int C3_EPI_BYTES = 256 * C3_LDC * 4;                      // 135168
-constexpr int C3_LDS = C3_OPER_BYTES > C3_EPI_BYTES ? C3_OPER_BYTES : C3_EPI_BYTES;
-static_assert(C3_B_ITEMS % C3_NT == 0, "weight tile loads");
+// BN output channels per workgroup, 64 threads per 16 channels (waves of 64 pixel rows x 64
+// channels): BN = 128 — 512 threads, 135 KB of LDS (one workgroup per CU); BN = 64 — 256 threads,
+// 70 KB, two workgroups per CU whose load / store / epilogue phases overlap each other's MFMAs
+template <int BN> struct C3T {
+  static constexpr int NT = BN * 4;
+  static constexpr int WN = BN / 64;                                // waves across the channels
+  static constexpr int B_ITEMS = 9 * BN * 4;                        // 16-byte chunks of the weights
+  static constexpr int AP = (C3_A_ITEMS + NT - 1) / NT;
+  static constexpr int BP = B_ITEMS / NT;                           // 9
+  static constexpr int LDC = BN + 4;                                // fp32 epilogue tile row
+  static constexpr int OPER = (C3_PATCH + 9 * BN) * C3_LD * 2;
+  static constexpr int EPI = 256 * LDC * 4;
+  static constexpr int LDS = OPER > EPI ? OPER : EPI;
+  static_assert(B_ITEMS % NT == 0, "weight tile loads");
+};
 
 struct C3Params {
   const void* a;
@@ -54,6 +59,7 @@ struct C3Params {
   uint32_t a_bytes, b_bytes, o_bytes;
   float a_slope, aux_slope;
   int a_act, flip, C, N;
+  int dbg;                  // diagnostics (VAE_C3_DBG): 1 no loads in the loop, 2 no MFMAs, 4 no LDS stores
 };
 
 // element offset of 16-byte chunk c of LDS row P (the bank-conflict swizzle above)
@@ -68,14 +74,17 @@ __device__ __forceinline__ uint32_t lrelu_pk(uint32_t w, float slope) {
   return *reinterpret_cast<uint32_t*>(&pk);
 }
 
-__global__ void __launch_bounds__(C3_NT) c3_kernel(const C3Params p) {
-  __shared__ __attribute__((aligned(16))) char smem[C3_LDS];
+template <int BN>
+__global__ void __launch_bounds__(BN * 4) c3_kernel(const C3Params p) {
+  using T = C3T<BN>;
+  constexpr int C3_NT = T::NT, C3_AP = T::AP, C3_BP = T::BP, C3_LDC = T::LDC, C3_BN = BN;
+  __shared__ __attribute__((aligned(16))) char smem[T::LDS];
   __bf16* As = reinterpret_cast<__bf16*>(smem);                  // [324][40]
   __bf16* Bs = As + C3_PATCH * C3_LD;                             // [9][128][40]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / T::WN, wn = wave % T::WN;
   // XCD-aware order: workgroup b runs on XCD b % 8; each XCD takes a contiguous tile range, so
   // the two channel tiles of an image share that XCD's L2 copy of the patch
   const int nt = p.N / C3_BN;
@@ -107,7 +116,7 @@ __global__ void __launch_bounds__(C3_NT) c3_kernel(const C3Params p) {
   for (int k = 0; k < C3_BP; ++k) {
     const int it = tid + C3_NT * k;
     const int row = it >> 2, ch = it & 3;
-    const int t = row >> 7, nl = row & (C3_BN - 1);
+    const int t = row / C3_BN, nl = row % C3_BN;
     bbase[k] = (uint32_t)((((n0 + nl) * 9 + t) * C + ch * 8) * 2);
   }
   uint32_t ar[C3_AP][4], br[C3_BP][4];
@@ -173,13 +182,15 @@ __global__ void __launch_bounds__(C3_NT) c3_kernel(const C3Params p) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t & 1][i], bfr[t & 1][j], acc[i][j], 0, 0, 0);
       if (t + 1 < 9) {
-        // interleave: 2 MFMAs, then one of the next tap's 8 LDS reads (the scheduler otherwise
-        // sinks the reads to their first use)
+        // interleave: the next tap's 8 LDS reads one per MFMA over the first half of this tap's
+        // 16, so they have landed by the next tap's head (the scheduler otherwise sinks them to
+        // their first use)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
       }
     }
   };
@@ -193,11 +204,11 @@ __global__ void __launch_bounds__(C3_NT) c3_kernel(const C3Params p) {
     // unconditional (the last chunk reloads itself, unused): a load under a branch makes the
     // compiler merge the prefetch registers with copies that wait for the loads right here,
     // before the MFMAs they were meant to hide behind
-    load((more ? kc + 1 : kc) * 32);
+    if (!(p.dbg & 1)) load((more ? kc + 1 : kc) * 32);
     __builtin_amdgcn_sched_barrier(0);      // (keep the loads ahead of the MFMAs)
-    compute();
+    if (!(p.dbg & 2)) compute();
     __syncthreads();
-    if (more) {
+    if (more && !(p.dbg & 4)) {
       store();
       __syncthreads();
     }
@@ -219,7 +230,7 @@ __global__ void __launch_bounds__(C3_NT) c3_kernel(const C3Params p) {
 #pragma unroll 2
   for (int k = 0; k < 8; ++k) {
     const int it = tid + C3_NT * k;
-    const int pix = it >> 4, cg = (it & 15) * 8;
+    const int pix = it / (C3_BN / 8), cg = (it % (C3_BN / 8)) * 8;
     const uint32_t o = (uint32_t)((img * 256 + pix) * p.N + n0 + cg);
     uint32_t rs[4], ax[4];
     bload<16>(rres, p.residual ? o * 2u : kOOB, rs);
@@ -418,9 +429,10 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
             acc[i][cb][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s & 1][cb], acc[i][cb][s], 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       }
       // (3 steps per K block: step s = 2 filled bfr[1] for the next block's s = 0 — swap roles)
       bfr[0][0] = bfr[1][0]; bfr[0][1] = bfr[1][1];
@@ -460,12 +472,157 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
 __global__ void __launch_bounds__(256) c3w_reduce(const float* slab, long ld, int slices, long cols, float* dw) {
   const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i >= cols) return;
-  f32x4 s = *reinterpret_cast<const f32x4*>(slab + i);
-  for (int k = 1; k < slices; ++k) s += *reinterpret_cast<const f32x4*>(slab + (long)k * ld + i);
+  // 8 slice loads in flight per thread (a plain loop waited for each one: 16-64 dependent HBM
+  // round trips per thread, 18.7 us average per call in the VQ-VAE step)
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= slices; k += 8) {
+    f32x4 t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab + (long)(k + u) * ld + i));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += t[u];
+  }
+  for (; k < slices; ++k) s += *reinterpret_cast<const f32x4*>(slab + (long)k * ld + i);
   f32x4 d;
   d[0] = dw[i]; d[1] = dw[i + 1]; d[2] = dw[i + 2]; d[3] = dw[i + 3];     // (parameter slices: 4-B aligned)
   d += s;
   dw[i] = d[0]; dw[i + 1] = d[1]; dw[i + 2] = d[2]; dw[i + 3] = d[3];
+}
+
+// 1x1 (pointwise) weight gradient on the same grid (the ResidualLayer's Conv1x1, vq_vae.py:64-68):
+//   dW[m][c] += Σ_pix U[pix][m] · V'[pix][c]
+// One workgroup: 128 m x 128 c over G images (both operands staged per image as [pixel][channel]
+// 256-B rows, swizzled as c3w's U); 8 waves of 64 m x 32 c; partials to slab slice `group`.
+constexpr int W1_NT = 512;
+constexpr int W1_T = 128;
+constexpr int W1_LP = 256 * (W1_T / 8) / W1_NT;            // 16-B loads per thread per operand (8)
+
+struct W1Params {
+  const void* u;
+  const void* v;
+  float* slab;
+  long slab_ld;
+  uint32_t u_bytes, v_bytes;
+  float v_slope;
+  int v_act, n, M, J, G;
+};
+
+__global__ void __launch_bounds__(W1_NT) c1w_kernel(const W1Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 256 * W3_URS];
+  char* const Us = smem;
+  char* const Vs = smem + 256 * W3_URS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wc = wave >> 1;
+  const int ntc = p.J / W1_T, per = (p.M / W1_T) * ntc;
+  int tile;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
+  }
+  const int grp = tile / per, rem = tile - grp * per;
+  const int tm = rem / ntc, tc = rem - tm * ntc;
+  const int m0 = tm * W1_T, c0 = tc * W1_T;
+  const int img0 = grp * p.G, img1 = min(p.n, img0 + p.G);
+  const rsrc_t ru = make_rsrc(p.u, p.u_bytes);
+  const rsrc_t rv = make_rsrc(p.v, p.v_bytes);
+  uint32_t ur[W1_LP][4], vr[W1_LP][4];
+  auto load = [&](int img) {
+#pragma unroll
+    for (int k = 0; k < W1_LP; ++k) {
+      const int it = tid + W1_NT * k;
+      const uint32_t pix = (uint32_t)img * 256u + (uint32_t)(it >> 4);
+      bload<16>(ru, (pix * (uint32_t)p.M + (uint32_t)(m0 + (it & 15) * 8)) * 2u, ur[k]);
+      bload<16>(rv, (pix * (uint32_t)p.J + (uint32_t)(c0 + (it & 15) * 8)) * 2u, vr[k]);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int k = 0; k < W1_LP; ++k) {
+      const int it = tid + W1_NT * k;
+      const int off = w3_usw(it >> 4, (it & 15) >> 1) + (it & 1) * 16;
+      *reinterpret_cast<uint4*>(Us + off) = uint4{ur[k][0], ur[k][1], ur[k][2], ur[k][3]};
+      uint4 v = uint4{vr[k][0], vr[k][1], vr[k][2], vr[k][3]};
+      if (p.v_act) {
+        v.x = lrelu_pk(v.x, p.v_slope); v.y = lrelu_pk(v.y, p.v_slope);
+        v.z = lrelu_pk(v.z, p.v_slope); v.w = lrelu_pk(v.w, p.v_slope);
+      }
+      *reinterpret_cast<uint4*>(Vs + off) = v;
+    }
+  };
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) acc[i][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  int aoff[4][2], boff[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i][h] = w3_usw(row, wm * 4 + i) + 8 * p4;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) boff[cb][h] = w3_usw(row, wc * 2 + cb) + 8 * p4;
+  }
+  auto compute = [&]() {
+#pragma unroll 2
+    for (int kb = 0; kb < 8; ++kb) {
+      bf16x8 af[4], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const w3_bf16x4 a0 = w3_tr_read(Us + kb * 32 * W3_URS + aoff[i][0]);
+        const w3_bf16x4 a1 = w3_tr_read(Us + kb * 32 * W3_URS + aoff[i][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const w3_bf16x4 b0 = w3_tr_read(Vs + kb * 32 * W3_URS + boff[cb][0]);
+        const w3_bf16x4 b1 = w3_tr_read(Vs + kb * 32 * W3_URS + boff[cb][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bfr[cb][e] = b0[e]; bfr[cb][4 + e] = b1[e]; }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) acc[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[cb], acc[i][cb], 0, 0, 0);
+    }
+  };
+  load(img0);
+  store();
+  __syncthreads();
+  for (int img = img0; img < img1; ++img) {
+    const bool more = img + 1 < img1;
+    load(more ? img + 1 : img);
+    __builtin_amdgcn_sched_barrier(0);
+    compute();
+    __syncthreads();
+    if (more) {
+      store();
+      __syncthreads();
+    }
+  }
+  float* part = p.slab + (long)grp * p.slab_ld;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + wm * 64 + i * 16 + 4 * g + e;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) part[(long)m * p.J + c0 + wc * 32 + cb * 16 + li] = acc[i][cb][e];
+    }
+}
+
+inline void c1w_plan(int n, int M, int J, int* G, int* groups) {
+  const int tiles = (M / W1_T) * (J / W1_T);
+  int ng = 256 / tiles;
+  if (ng < 1) ng = 1;
+  if (ng > n) ng = n;
+  *G = (n + ng - 1) / ng;
+  *groups = (n + *G - 1) / *G;
 }
 
 inline void c3w_plan(int n, int M, int J, int* G, int* groups) {
@@ -488,7 +645,7 @@ bool c3_enabled() {
 
 bool c3_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int C, int N) {
   return n > 0 && h == 16 && w == 16 && p == 16 && q == 16 && r == 3 && stride == 1 && pad == 1 && C % 32 == 0 &&
-         C >= 32 && N % C3_BN == 0 && N > 0 && (long)n * 256 * (C > N ? C : N) * 2 < (1l << 31);
+         C >= 32 && N % 128 == 0 && N > 0 && (long)n * 256 * (C > N ? C : N) * 2 < (1l << 31);
 }
 
 int c3_launch(const C3Args& a, hipStream_t st) {
@@ -502,8 +659,13 @@ int c3_launch(const C3Args& a, hipStream_t st) {
   p.o_bytes = (uint32_t)((long)a.n * 256 * a.N * 2);
   p.a_slope = a.a_slope; p.aux_slope = a.aux_slope;
   p.a_act = a.a_act; p.flip = a.flip; p.C = a.C; p.N = a.N;
-  const unsigned grid = (unsigned)(a.n * (a.N / C3_BN));
-  VAE_LAUNCH(c3_kernel, dim3(grid), dim3(C3_NT), 0, st, p);
+  static const int dbg = getenv("VAE_C3_DBG") ? atoi(getenv("VAE_C3_DBG")) : 0;
+  p.dbg = dbg;
+  // VAE_C3_BN=64: two 256-thread workgroups per CU (A/B timing: 65 vs 48 us forward, slower)
+  static const int bn = (getenv("VAE_C3_BN") && atoi(getenv("VAE_C3_BN")) == 64) ? 64 : 128;
+  const unsigned grid = (unsigned)(a.n * (a.N / bn));
+  if (bn == 128) VAE_LAUNCH(c3_kernel<128>, dim3(grid), dim3(512), 0, st, p);
+  else VAE_LAUNCH(c3_kernel<64>, dim3(grid), dim3(256), 0, st, p);
   return check_launch("c3");
 }
 
@@ -538,6 +700,36 @@ int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st) {
   const unsigned grid = (unsigned)(groups * (a.M / W3_BM) * (a.J / W3_BC));
   VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
   if (int rc = check_launch("c3w")) return rc;
+  VAE_LAUNCH(c3w_reduce, dim3((unsigned)((cols / 4 + 255) / 256)), dim3(256), 0, st, (const float*)p.slab, cols, groups,
+             cols, a.dw);
+  return check_launch("c3w_reduce");
+}
+
+}  // namespace vae
+
+namespace vae {
+
+bool c1w_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int M, int J) {
+  return n > 0 && h == 16 && w == 16 && p == 16 && q == 16 && r == 1 && stride == 1 && pad == 0 && M % W1_T == 0 &&
+         J % W1_T == 0 && (long)n * 256 * (M > J ? M : J) * 2 < (1l << 31);
+}
+
+int c1w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st) {
+  if (!c1w_shape_ok(a.n, 16, 16, 16, 16, 1, 1, 0, a.M, a.J)) return fail(VAE_E_BADSHAPE, "c1w: shape");
+  if (!al16(a.u) || !al16(a.v) || ((uintptr_t)a.dw & 3u)) return fail(VAE_E_BADARG, "c1w: alignment");
+  W1Params p;
+  int groups;
+  c1w_plan(a.n, a.M, a.J, &p.G, &groups);
+  const long cols = (long)a.M * a.J;
+  if (!ws_fits((long)groups * cols * 4, ws ? ws_bytes : 0, "c1w slab")) return VAE_E_BADARG;
+  p.u = a.u; p.v = a.v; p.slab = static_cast<float*>(ws); p.slab_ld = cols;
+  p.u_bytes = (uint32_t)((long)a.n * 256 * a.M * 2);
+  p.v_bytes = (uint32_t)((long)a.n * 256 * a.J * 2);
+  p.v_act = a.v_act; p.v_slope = a.v_slope;
+  p.n = a.n; p.M = a.M; p.J = a.J;
+  const unsigned grid = (unsigned)(groups * (a.M / W1_T) * (a.J / W1_T));
+  VAE_LAUNCH(c1w_kernel, dim3(grid), dim3(W1_NT), 0, st, p);
+  if (int rc = check_launch("c1w")) return rc;
   VAE_LAUNCH(c3w_reduce, dim3((unsigned)((cols / 4 + 255) / 256)), dim3(256), 0, st, (const float*)p.slab, cols, groups,
              cols, a.dw);
   return check_launch("c3w_reduce");

@@ -38,6 +38,10 @@ struct C3WArgs {
 bool c3w_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int M, int J);
 long c3w_workspace(int n, int M, int J);
 int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st);
+// 1x1 stride-1 (pointwise) weight gradient on the same grid: dW[m][c] += Σ U[pix][m] · xf(V)[pix][c]
+// (the ResidualLayer's Conv1x1); M % 128 == 0, J % 128 == 0; slab partials as c3w.
+bool c1w_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int M, int J);
+int c1w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st);
 // VAE_NO_C3=1 keeps these convolutions on the conv-GEMM (A/B timing)
 bool c3_enabled();
 

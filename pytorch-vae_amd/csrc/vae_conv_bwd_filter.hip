@@ -24,6 +24,17 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
     if (rc || !a->db) return rc;
     return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
   }
+  if (a->dtype == VAE_BF16 && !a->x_nchw_f32 && c3_enabled() && (a->workspace || querying()) &&
+      c1w_shape_ok(a->n, a->h, a->w, a->p, a->q, a->r, a->stride, a->pad, a->k, a->c) &&
+      a->dy_xf.kind == VAE_X_NONE && (a->x_xf.kind == VAE_X_NONE || a->x_xf.kind == VAE_X_ACT) &&
+      (a->dw_inner <= 0 || a->dw_inner == a->c)) {
+    C3WArgs c;
+    c.u = a->dy; c.v = a->x; c.v_act = a->x_xf.kind == VAE_X_ACT; c.v_slope = a->x_xf.slope;
+    c.dw = static_cast<float*>(a->dw); c.n = a->n; c.M = a->k; c.J = a->c;
+    int rc = c1w_launch(c, a->workspace, a->workspace_bytes, (hipStream_t)stream);
+    if (rc || !a->db) return rc;
+    return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
+  }
   {
     // bf16 weight-gradient GEMM (vae_wgemm.hpp)
     WgParams w;

@@ -111,3 +111,28 @@ def test_c3_backward_filter(n, cin, cout, act, bias):
     assert rel(got, w.grad) < 2e-3
     if bias:
         assert rel(db.cpu(), b.grad) < 2e-3
+
+
+@pytest.mark.parametrize("n,cin,cout,act", [(8, 256, 256, True), (3, 128, 256, False)])
+def test_c1_backward_filter(n, cin, cout, act):
+    """Pointwise (1x1) weight gradient on a 16 x 16 grid (vae_c3.hip c1w), accumulated."""
+    from vae_amd import _lib as L
+    torch.manual_seed(14)
+    x = _bf(torch.randn(n, cin, 16, 16))
+    w = torch.zeros(cout, cin, 1, 1, requires_grad=True)
+    y = F.conv2d(F.relu(x) if act else x, w)
+    gy = _bf(torch.randn_like(y))
+    y.backward(gy)
+    dw0 = torch.randn(cout, 1, 1, cin) * 0.1
+    xd = nhwc(x, torch.bfloat16)
+    gyd = nhwc(gy, torch.bfloat16)
+    dw = dw0.clone().cuda()
+    a = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=cin, k=cout, p=16, q=16, r=1, stride=1, pad=0)
+    a.x, a.dy, a.dw = xd.data_ptr(), gyd.data_ptr(), dw.data_ptr()
+    if act:
+        a.x_xf = L.Xform(kind=L.X_ACT, channels=cin, slope=0.0)
+    ws = give_workspace(a, "vae_conv2d_bwd_filter")
+    L.call("vae_conv2d_bwd_filter", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    del ws
+    assert rel((dw.cpu() - dw0).permute(0, 3, 1, 2), w.grad) < 2e-3

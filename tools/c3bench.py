@@ -46,6 +46,21 @@ def main():
         torch.cuda.synchronize()
         us = ev[0].elapsed_time(ev[1]) * 1000 / reps
         print(f"{fn:24s} {us:8.2f} us/call  {2 * n * 256 * K * 9 * C / us / 1e6:7.1f} TF/s", flush=True)
+    # the ResidualLayer's 1x1 weight gradient
+    b = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=C, k=K, p=16, q=16, r=1, stride=1, pad=0)
+    b.x, b.dy, b.dw = x.data_ptr(), dy.data_ptr(), dw.data_ptr()
+    b.x_xf = L.Xform(kind=L.X_ACT, channels=C, slope=0.0)
+    b.workspace, b.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+    for _ in range(reps):
+        L.call("vae_conv2d_bwd_filter", ctypes.byref(b), st)
+    torch.cuda.synchronize()
+    ev[0].record()
+    for _ in range(reps):
+        L.call("vae_conv2d_bwd_filter", ctypes.byref(b), st)
+    ev[1].record()
+    torch.cuda.synchronize()
+    us = ev[0].elapsed_time(ev[1]) * 1000 / reps
+    print(f"{'1x1 bwd_filter':24s} {us:8.2f} us/call  {2 * n * 256 * K * C / us / 1e6:7.1f} TF/s", flush=True)
 
 
 if __name__ == "__main__":
