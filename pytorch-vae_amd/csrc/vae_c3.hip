@@ -262,9 +262,10 @@ __global__ void __launch_bounds__(BN * 4) c3_kernel(const C3Params p) {
 // One workgroup: 128 m x 32 c x all 9 taps over a group of G images.  Per image it stages U
 // ([256 pixels][128 m], 288-B rows) and V's 18 x 18 halo patch ([324][32 c], 64-B rows) once, and
 // every tap reads its B fragments from the patch at a shifted pixel — the per-tap weight-gradient
-// GEMM (vae_wgemm.hpp) gathered V from L2 once per tap.  6 waves: wave (jh, r) = m rows 64jh..+63
-// (4 A fragments, reused by all 3 taps of its tap row) x the 32 c x taps (r, 0..2): 24 MFMAs per
-// 20 transposed LDS reads per 32-pixel K-step.  Operands are [pixel][channel] in LDS; the
+// GEMM (vae_wgemm.hpp) gathered V from L2 once per tap.  12 waves (3 per SIMD: 6 left two SIMDs
+// with twice the MFMAs of the other two): wave (mq, r) = m rows 32mq..+31 (2 A fragments, reused
+// by the 3 taps of its tap row) x the 32 c x taps (r, 0..2): 12 MFMAs per 16 transposed LDS reads
+// per 32-pixel K-step.  Operands are [pixel][channel] in LDS; the
 // K = pixel direction is read with ds_read_b64_tr_b16 (vae_wgemm.hpp).  Each workgroup writes its
 // partial dW tile to slab slice `group` (plain stores); c3w_reduce adds the slices into dW.
 typedef __bf16 __attribute__((ext_vector_type(4))) __attribute__((address_space(3))) w3_lds_bf16x4;
@@ -274,7 +275,7 @@ __device__ __forceinline__ w3_bf16x4 w3_tr_read(const char* generic_lds_addr) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((w3_lds_bf16x4*)(uintptr_t)off);
 }
 
-constexpr int W3_NT = 384;
+constexpr int W3_NT = 768;
 constexpr int W3_BM = 128, W3_BC = 32;
 // LDS rows: U 256 B with its 32-byte slots XOR-swizzled by (P & 3) | ((P >> 1) & 4), V 64 B with
 // slots swizzled by (P >> 3) & 1: the 32-lane groups of ds_read_b64_tr_b16 read pixel rows
@@ -285,8 +286,8 @@ constexpr int W3_U_BYTES = 256 * W3_URS;                  // 65536
 constexpr int W3_V_BYTES = C3_PATCH * W3_VRS;             // 20736
 constexpr int W3_UI = 256 * (W3_BM / 8);                  // 16-B chunks of a U tile (4096)
 constexpr int W3_VI = C3_PATCH * (W3_BC / 8);             // of a V patch (1296)
-constexpr int W3_UP = (W3_UI + W3_NT - 1) / W3_NT;        // 11
-constexpr int W3_VP = (W3_VI + W3_NT - 1) / W3_NT;        // 4
+constexpr int W3_UP = (W3_UI + W3_NT - 1) / W3_NT;        // 6
+constexpr int W3_VP = (W3_VI + W3_NT - 1) / W3_NT;        // 2
 
 // byte offset of 32-byte slot c of LDS row P (U tile / V patch), with the swizzles above
 __device__ __forceinline__ int w3_usw(int P, int c) { return P * W3_URS + ((c ^ ((P & 3) | ((P >> 1) & 4))) << 5); }
@@ -308,7 +309,7 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
   char* const Vs = smem + W3_U_BYTES;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int jh = wave & 1, tr = wave >> 1;
+  const int mq = wave / 3, tr = wave - 3 * (wave / 3);   // m rows 32mq..+31, tap row tr
   const int ntc = p.J / W3_BC, per = (p.M / W3_BM) * ntc;
   int tile;
   {
@@ -369,9 +370,9 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
     }
   };
 
-  f32x4 acc[4][2][3];
+  f32x4 acc[2][2][3];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -379,19 +380,19 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
 
   // transposed-read addresses: lane 4q+p of 16-lane group g reads K rows 8g+4h+q, columns 4p..4p+3
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  int aoff[4][2], prow[2];
+  int aoff[2][2], prow[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = 8 * g + 4 * h + q4;                      // pixel within a 32-pixel K block
 #pragma unroll
-    for (int i = 0; i < 4; ++i) aoff[i][h] = w3_usw(row, jh * 4 + i) + 8 * p4;       // (row & 15 fixed over kb)
+    for (int i = 0; i < 2; ++i) aoff[i][h] = w3_usw(row, mq * 2 + i) + 8 * p4;       // (row & 15 fixed over kb)
     // K block kb = output rows 2kb, 2kb+1; this lane's pixel: output (2kb + (g >> 1), 8(g & 1) + 4h + q)
     // -> patch pixel (2kb + (g >> 1) + r, 8(g & 1) + 4h + q + s)
     prow[h] = ((g >> 1) + tr) * C3_PW + 8 * (g & 1) + 4 * h + q4;
   }
-  auto afrag = [&](int kb, bf16x8 (&af)[4]) {
+  auto afrag = [&](int kb, bf16x8 (&af)[2]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 2; ++i) {
       const w3_bf16x4 a0 = w3_tr_read(Us + kb * 32 * W3_URS + aoff[i][0]);
       const w3_bf16x4 a1 = w3_tr_read(Us + kb * 32 * W3_URS + aoff[i][1]);
 #pragma unroll
@@ -411,7 +412,7 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
   // 24 steps (K block kb, tap column s); the next step's B fragments are read between this step's
   // 8 MFMAs after one wait at the step's head (as c3_kernel); A once per K block
   auto compute = [&]() {
-    bf16x8 af[4], bfr[2][2];
+    bf16x8 af[2], bfr[2][2];
     bfrag(0, 0, bfr[0]);
 #pragma unroll 1
     for (int kb = 0; kb < 8; ++kb) {
@@ -423,7 +424,7 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
         // next step's B: (kb, s+1), or (kb+1, 0) — past the end a harmless re-read of block 7
         bfrag(s < 2 ? kb : min(kb + 1, 7), s < 2 ? s + 1 : 0, bfr[(s + 1) & 1]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb)
             acc[i][cb][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s & 1][cb], acc[i][cb][s], 0, 0, 0);
@@ -432,7 +433,6 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
       }
       // (3 steps per K block: step s = 2 filled bfr[1] for the next block's s = 0 — swap roles)
       bfr[0][0] = bfr[1][0]; bfr[0][1] = bfr[1][1];
@@ -456,10 +456,10 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
   // partial tile -> slab slice grp: lane holds rows 4g+e of fragment i (m), column li of fragment cb (c)
   float* part = p.slab + (long)grp * p.slab_ld;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int m = j0 + jh * 64 + i * 16 + 4 * g + e;
+      const int m = j0 + mq * 32 + i * 16 + 4 * g + e;
 #pragma unroll
       for (int s = 0; s < 3; ++s)
 #pragma unroll
