@@ -42,6 +42,26 @@ int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st);
 // (the ResidualLayer's Conv1x1); M % 128 == 0, J % 128 == 0; slab partials as c3w.
 bool c1w_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int M, int J);
 int c1w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st);
+// Pointwise (1x1 stride-1) conv forward / data gradient as a pixel-tile GEMM (vae_p1.hip):
+//   out[pix][n] = Σ_c xf(A)[pix][c] · B[n][c] (+ bias, + xf(residual)) (* act'(aux))
+// M (pixels) % 256 == 0, C % 128 == 0, N % 128 == 0, 16-byte aligned tensors.
+struct P1Args {
+  const void* a;
+  int a_act;
+  float a_slope;
+  const void* b;            // [N][C] bf16
+  void* out;                // [M][N] bf16
+  const float* bias;
+  const void* residual;
+  int res_act;
+  float res_slope;
+  const void* aux;
+  float aux_slope;
+  long M;
+  int C, N;
+};
+bool p1_shape_ok(long M, int C, int N);
+int p1_launch(const P1Args& a, hipStream_t st);
 // VAE_NO_C3=1 keeps these convolutions on the conv-GEMM (A/B timing)
 bool c3_enabled();
 

@@ -15,6 +15,18 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
   if (a->h % S || a->w % S || a->h / S != a->p || a->w / S != a->q)
     return fail(VAE_E_BADSHAPE, "conv2d_bwd_data: needs h == p*stride (got h=%d p=%d S=%d)", a->h, a->p, S);
   const long wbytes = (long)a->k * a->r * a->r * a->c * 2;
+  // 1x1 stride 1 (the VQ-VAE ResidualLayer's Conv1x1): pixel-tile GEMM over WT[c][k]
+  if (a->dtype == VAE_BF16 && a->wt_t && c3_enabled() && a->r == 1 && a->stride == 1 && a->pad == 0 &&
+      a->h == a->p && a->w == a->q && p1_shape_ok((long)a->n * a->h * a->w, a->k, a->c) &&
+      a->dy_xf.kind == VAE_X_NONE && (a->dx_epi.kind == VAE_X_NONE || a->dx_epi.kind == VAE_X_ACT) &&
+      !a->dx_dgamma && !a->bn_finalize && a->split_k <= 0) {
+    P1Args c;
+    memset(&c, 0, sizeof(c));
+    c.a = a->dy; c.b = a->wt_t; c.out = a->dx; c.residual = a->residual;
+    if (a->dx_epi.kind == VAE_X_ACT) { c.aux = a->dx_epi.aux; c.aux_slope = a->dx_epi.slope; }
+    c.M = (long)a->n * a->h * a->w; c.C = a->k; c.N = a->c;
+    return p1_launch(c, (hipStream_t)stream);
+  }
   // 3x3 stride-1 on a 16 x 16 grid (the VQ-VAE's residual stacks): the image-tile kernel, taps
   // flipped, over the caller's swapped-axes weights WT[c][r][s][k]
   if (a->dtype == VAE_BF16 && a->wt_t && c3_enabled() &&

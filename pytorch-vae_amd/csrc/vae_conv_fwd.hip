@@ -9,6 +9,20 @@ using namespace vae;
 extern "C" int vae_conv2d_fwd(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "conv2d_fwd") || !a->x || !a->wt || !a->y) return fail(VAE_E_BADARG, "conv2d_fwd: null tensor");
   if (!xf_ok(a->x_xf, "conv2d_fwd.x")) return VAE_E_BADARG;
+  // 1x1 stride-1 convs (the VQ-VAE ResidualLayer's Conv1x1 + skip add): pixel-tile kernel
+  if (a->dtype == VAE_BF16 && !a->x_nchw_f32 && c3_enabled() && a->r == 1 && a->stride == 1 && a->pad == 0 &&
+      a->h == a->p && a->w == a->q && p1_shape_ok((long)a->n * a->p * a->q, a->c, a->k) &&
+      (a->x_xf.kind == VAE_X_NONE || a->x_xf.kind == VAE_X_ACT) &&
+      (a->residual_xf.kind == VAE_X_NONE || a->residual_xf.kind == VAE_X_ACT) && !a->y_sum && !a->y_sumsq &&
+      !a->bn_finalize && a->split_k <= 0) {
+    P1Args c;
+    memset(&c, 0, sizeof(c));
+    c.a = a->x; c.a_act = a->x_xf.kind == VAE_X_ACT; c.a_slope = a->x_xf.slope;
+    c.b = a->wt; c.out = a->y; c.bias = a->bias;
+    c.residual = a->residual; c.res_act = a->residual && a->residual_xf.kind == VAE_X_ACT; c.res_slope = a->residual_xf.slope;
+    c.M = (long)a->n * a->p * a->q; c.C = a->c; c.N = a->k;
+    return p1_launch(c, (hipStream_t)stream);
+  }
   // 3x3 stride-1 convs on a 16 x 16 grid (the VQ-VAE's residual stacks): image-tile kernel
   if (a->dtype == VAE_BF16 && !a->x_nchw_f32 && c3_enabled() &&
       c3_shape_ok(a->n, a->h, a->w, a->p, a->q, a->r, a->stride, a->pad, a->c, a->k) &&

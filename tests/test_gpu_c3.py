@@ -136,3 +136,61 @@ def test_c1_backward_filter(n, cin, cout, act):
     torch.cuda.synchronize()
     del ws
     assert rel((dw.cpu() - dw0).permute(0, 3, 1, 2), w.grad) < 2e-3
+
+
+@pytest.mark.parametrize("n,cin,cout,act,res,res_act,bias", [(4, 256, 256, True, True, True, False),
+                                                             (3, 128, 256, False, True, False, True),
+                                                             (2, 256, 128, True, False, False, False)])
+def test_p1_forward(n, cin, cout, act, res, res_act, bias):
+    """1x1 conv forward on the pixel-tile kernel (vae_p1.hip): relu/lrelu(x) @ W^T + b + xf(skip)."""
+    from vae_amd import _lib as L
+    torch.manual_seed(15)
+    x = _bf(torch.randn(n, cin, 16, 16))
+    w = _bf(torch.randn(cout, cin, 1, 1) * (1.0 / cin ** 0.5))
+    b = torch.randn(cout) * 0.1 if bias else None
+    r = _bf(torch.randn(n, cout, 16, 16)) if res else None
+    ref = F.conv2d(F.relu(x) if act else x, w, b)
+    if res:
+        ref = ref + (F.leaky_relu(r, 0.01) if res_act else r)
+    xd, out = nhwc(x, torch.bfloat16), torch.empty(n, 16, 16, cout, device="cuda", dtype=torch.bfloat16)
+    wd = w.permute(0, 2, 3, 1).contiguous().to("cuda", torch.bfloat16)
+    a = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=cin, k=cout, p=16, q=16, r=1, stride=1, pad=0)
+    a.x, a.wt, a.y = xd.data_ptr(), wd.data_ptr(), out.data_ptr()
+    keep = []
+    if act:
+        a.x_xf = L.Xform(kind=L.X_ACT, channels=cin, slope=0.0)
+    if bias:
+        bd = b.cuda()
+        keep.append(bd)
+        a.bias = bd.data_ptr()
+    if res:
+        rd = nhwc(r, torch.bfloat16)
+        keep.append(rd)
+        a.residual = rd.data_ptr()
+        if res_act:
+            a.residual_xf = L.Xform(kind=L.X_ACT, channels=cout, slope=0.01)
+    L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel(to_nchw(out), ref) < TOL
+
+
+def test_p1_backward_data():
+    """1x1 conv data gradient on the pixel-tile kernel: (dy @ W) * relu'(t)."""
+    from vae_amd import _lib as L
+    torch.manual_seed(16)
+    n, cin, cout = 4, 256, 256
+    w = _bf(torch.randn(cout, cin, 1, 1) * (1.0 / cin ** 0.5))
+    gy = _bf(torch.randn(n, cout, 16, 16))
+    t = _bf(torch.randn(n, cin, 16, 16))
+    ref = F.conv_transpose2d(gy, w)
+    ref = torch.where(t > 0, ref, ref * 0.0)
+    gyd, td = nhwc(gy, torch.bfloat16), nhwc(t, torch.bfloat16)
+    wt = w.permute(1, 2, 3, 0).contiguous().to("cuda", torch.bfloat16)
+    wd = w.permute(0, 2, 3, 1).contiguous().to("cuda", torch.bfloat16)
+    dx = torch.empty(n, 16, 16, cin, device="cuda", dtype=torch.bfloat16)
+    a = L.ConvArgs(dtype=L.BF16, n=n, h=16, w=16, c=cin, k=cout, p=16, q=16, r=1, stride=1, pad=0)
+    a.dy, a.wt, a.wt_t, a.dx = gyd.data_ptr(), wd.data_ptr(), wt.data_ptr(), dx.data_ptr()
+    a.dx_epi = L.Xform(kind=L.X_ACT, channels=cin, slope=0.0, aux=td.data_ptr())
+    L.call("vae_conv2d_bwd_data", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert rel(to_nchw(dx), ref) < TOL
