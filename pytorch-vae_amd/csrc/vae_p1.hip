@@ -9,13 +9,16 @@
 // Why not the conv-GEMM: at K = 256 its 128 x 128 tile runs 4 K-steps of 64 behind a 2-stage
 // register ring with the per-element phase/tap addressing of a general conv (19.5 us forward,
 // 30.2 us data gradient at B=128, profiles/r3_v5_vq_bench_kernel_stats.csv) for 50 MB of traffic.
-// Here one workgroup owns 256 pixels x 128 channels and stages K in 128-channel chunks (A 64 KB +
-// B 32 KB), the next chunk's loads issued before the current chunk's MFMAs.
+// Here one workgroup (4 waves of 64 x 64) owns 128 pixels x 128 channels and stages K in 64-channel
+// chunks (A + B 32 KB), the next chunk's loads issued before the current chunk's MFMAs; 66 KB of
+// LDS, two workgroups per CU.  (A 256-pixel tile with 128-channel chunks, one workgroup per CU,
+// measured the same: 15.7 us forward / 14.9 us data gradient per call at B=128 — the kernel moves
+// ~50 MB, so it runs at ~3.3 TB/s either way.)
 //
-// LDS rows are 256 B (128 channels) with 16-byte chunk c of row P at slot c ^ (P & 15): the lane
-// groups of ds_read_b128 ({0-3,12-15,20-27}, ... — MI355X_MICROARCH.md LDS table) read rows
+// LDS rows are 128 B (64 channels) with 16-byte chunk c of row P at slot c ^ ((P >> 1) & 7): the
+// lane groups of ds_read_b128 ({0-3,12-15,20-27}, ... — MI355X_MICROARCH.md LDS table) read rows
 // P0..P0+15 (P0 % 16 == 0) at chunks c0 / c0+1 and land on 16 distinct 4-bank groups, and 8
-// consecutive lanes of ds_write_b128 store 8 distinct slots of one row.
+// consecutive lanes of ds_write_b128 store the 8 slots of one row.
 #include "vae_c3.hpp"
 #include "vae_igemm.hpp"
 #include <stdlib.h>
@@ -23,14 +26,15 @@
 namespace vae {
 namespace {
 
-constexpr int P1_NT = 512;
-constexpr int P1_BM = 256, P1_BN = 128, P1_KC = 128;      // pixels, channels, K chunk
+constexpr int P1_NT = 256;
+constexpr int P1_BM = 128, P1_BN = 128, P1_KC = 64;       // pixels, channels, K chunk
 constexpr int P1_ROW = P1_KC * 2;                          // LDS row bytes
-constexpr int P1_AI = P1_BM * (P1_KC / 8) / P1_NT;         // 16-B A loads per thread per chunk (8)
+constexpr int P1_AI = P1_BM * (P1_KC / 8) / P1_NT;         // 16-B A loads per thread per chunk (4)
 constexpr int P1_BI = P1_BN * (P1_KC / 8) / P1_NT;         // B (4)
+constexpr int P1_CPR = P1_KC / 8;                          // 16-B chunks per LDS row (8)
 constexpr int P1_LDC = P1_BN + 4;
-constexpr int P1_OPER = (P1_BM + P1_BN) * P1_ROW;          // 98304
-constexpr int P1_EPI = P1_BM * P1_LDC * 4;                 // 135168
+constexpr int P1_OPER = (P1_BM + P1_BN) * P1_ROW;          // 32768
+constexpr int P1_EPI = P1_BM * P1_LDC * 4;                 // 67584
 constexpr int P1_LDS = P1_OPER > P1_EPI ? P1_OPER : P1_EPI;
 
 struct P1Params {
@@ -45,7 +49,7 @@ struct P1Params {
   int a_act, res_act, M, C, N;
 };
 
-__device__ __forceinline__ int p1_sw(int P, int c) { return P * P1_ROW + ((c ^ (P & 15)) << 4); }
+__device__ __forceinline__ int p1_sw(int P, int c) { return P * P1_ROW + ((c ^ ((P >> 1) & 7)) << 4); }
 
 __device__ __forceinline__ uint32_t p1_lrelu(uint32_t w, float slope) {
   f32x2 v = f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
@@ -79,12 +83,12 @@ __global__ void __launch_bounds__(P1_NT) p1_kernel(const P1Params p) {
 #pragma unroll
     for (int k = 0; k < P1_AI; ++k) {
       const int it = tid + P1_NT * k;
-      bload<16>(ra, (uint32_t)(((m0 + (it >> 4)) * p.C + c0 + (it & 15) * 8) * 2), ar[k]);
+      bload<16>(ra, (uint32_t)(((m0 + it / P1_CPR) * p.C + c0 + (it % P1_CPR) * 8) * 2), ar[k]);
     }
 #pragma unroll
     for (int k = 0; k < P1_BI; ++k) {
       const int it = tid + P1_NT * k;
-      bload<16>(rb, (uint32_t)(((n0 + (it >> 4)) * p.C + c0 + (it & 15) * 8) * 2), br[k]);
+      bload<16>(rb, (uint32_t)(((n0 + it / P1_CPR) * p.C + c0 + (it % P1_CPR) * 8) * 2), br[k]);
     }
   };
   auto store = [&]() {
@@ -96,12 +100,12 @@ __global__ void __launch_bounds__(P1_NT) p1_kernel(const P1Params p) {
         v.x = p1_lrelu(v.x, p.a_slope); v.y = p1_lrelu(v.y, p.a_slope);
         v.z = p1_lrelu(v.z, p.a_slope); v.w = p1_lrelu(v.w, p.a_slope);
       }
-      *reinterpret_cast<uint4*>(As + p1_sw(it >> 4, it & 15)) = v;
+      *reinterpret_cast<uint4*>(As + p1_sw(it / P1_CPR, it % P1_CPR)) = v;
     }
 #pragma unroll
     for (int k = 0; k < P1_BI; ++k) {
       const int it = tid + P1_NT * k;
-      *reinterpret_cast<uint4*>(Bs + p1_sw(it >> 4, it & 15)) = uint4{br[k][0], br[k][1], br[k][2], br[k][3]};
+      *reinterpret_cast<uint4*>(Bs + p1_sw(it / P1_CPR, it % P1_CPR)) = uint4{br[k][0], br[k][1], br[k][2], br[k][3]};
     }
   };
   f32x4 acc[4][4];
@@ -139,7 +143,7 @@ __global__ void __launch_bounds__(P1_NT) p1_kernel(const P1Params p) {
       __syncthreads();
     }
   }
-  // epilogue through LDS (fp32 [256][128 + 4]), then 16-byte rows of 8 channels
+  // epilogue through LDS (fp32 [128][128 + 4]), then 16-byte rows of 8 channels
   float* Cs = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
