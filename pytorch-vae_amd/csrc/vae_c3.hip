@@ -171,8 +171,11 @@ __global__ void __launch_bounds__(BN * 4) c3_kernel(const C3Params p) {
     frags(0, af[0], bfr[0]);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      // this tap's fragments (read during the previous tap) have landed: one wait here, so the
-      // next tap's reads issued between the MFMAs below need none (lgkmcnt counts in order)
+      // this tap's fragments (read during the previous tap) have landed: one wait here, fenced
+      // by scheduling barriers on both sides (the scheduler otherwise floats it above the
+      // previous tap's last MFMAs, or waits after every read), so the next tap's reads issued
+      // between the MFMAs below need none (lgkmcnt counts in order)
+      __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0)
       __builtin_amdgcn_sched_barrier(0);
       if (t + 1 < 9) frags(t + 1, af[(t + 1) & 1], bfr[(t + 1) & 1]);
@@ -419,6 +422,7 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
       afrag(kb, af);                                       // (one exposed read per K block)
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
+        __builtin_amdgcn_sched_barrier(0);                 // (the wait stays between the steps)
         __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0)
         __builtin_amdgcn_sched_barrier(0);
         // next step's B: (kb, s+1), or (kb+1, 0) — past the end a harmless re-read of block 7
