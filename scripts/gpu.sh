@@ -18,6 +18,10 @@
 #   pmc:A:B          the same for --arch A --batch B
 #   kprobe           per-block phase probe (needs `make probe`)
 #   kbench[:ARGS]    per-launch microbench under a kernel trace (tools/kbench.py, ARGS comma-separated)
+#   c3bench[:ENV]    the VQ-VAE image-tile kernels back to back (tools/c3bench.py), ENV e.g.
+#                    VAE_C3_DBG=5 (phase ablation: 1 no chunk loads, 2 no MFMAs, 4 no LDS stores)
+#   c3trace          tools/c3bench.py under rocprofv3 --kernel-trace --stats
+#   c3pmc            tools/c3bench.py under two PMC passes (MFMA busy, LDS bank conflicts, waits)
 set -o pipefail
 TAG=${1:?tag}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -67,6 +71,14 @@ for step in "$@"; do
     kbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
                -d $O/${TAG}_kb -o kb -- python3 $R/tools/kbench.py --out $O/${TAG}_kb_groups.json ${a1//,/ }) \
                > $O/${TAG}_kbench.log 2>&1 ;;
+    c3bench) run c3bench_${a1//[=,]/_} 200 env ${a1//,/ } python3 -u tools/c3bench.py ;;
+    c3trace) (cd /tmp && export TMPDIR=/tmp && REPS=10 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv \
+               -d $O/${TAG}_c3trace -o run -- python3 $R/tools/c3bench.py) > $O/${TAG}_c3trace.log 2>&1 ;;
+    c3pmc) (cd /tmp && export TMPDIR=/tmp && \
+            REPS=5 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY \
+              --output-format csv -d $O/${TAG}_c3pmc_a -o run -- python3 $R/tools/c3bench.py > $O/${TAG}_c3pmc_a.log 2>&1 && \
+            REPS=5 timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+              --output-format csv -d $O/${TAG}_c3pmc_b -o run -- python3 $R/tools/c3bench.py > $O/${TAG}_c3pmc_b.log 2>&1) ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   rc=$?
