@@ -208,15 +208,36 @@ def time_kernels(plan, reps=20):
     return res
 
 
-# device kernels each ABI call of the VanillaVAE step launches (profiles/*pmc*.json and the
-# rocprofv3 kernel_stats CSVs are keyed by kernel symbol; a call is timed as a whole)
-KERNEL_SYMBOLS = {"vae_head_bwd": ["head_bwd_mfma", "reduce_rows_kernel"], "vae_head_fwd": ["head_fwd_mfma"],
-                  "vae_elbo_fwd": ["elbo_kernel"],
-                  "vae_convT2d_bwd": ["hires_convT_bwd_kernel", "hires_slab_reduce"],
-                  "vae_conv_bwd_filter_batch": ["wg_group_kernel", "wg_slab_reduce"],
-                  "vae_convT2d_fwd": ["hires_convT_fwd_kernel", "cgemm_kernel"],
-                  "vae_conv2d_fwd": ["cgemm_kernel"], "vae_conv2d_bwd_data": ["cgemm_kernel"],
-                  "vae_convT2d_bwd_data": ["cgemm_kernel"]}
+def call_kernels(fn, ref):
+    """The device kernels one call of the step launches, as (mangled, demangled) names: the call
+    is run once more with the library's launch log on (vaehip.h vae_launch_log) — what rocprofv3
+    and the PMC summaries key their rows by.  (Runs after the timed region, like time_kernels.)"""
+    import ctypes
+    from vae_amd import _lib as L
+    from vae_amd.net import call_one
+    lib = L.load()
+    lib.vae_launch_log(1)
+    try:
+        call_one(fn, ref, torch.cuda.current_stream().cuda_stream)
+    finally:
+        lib.vae_launch_log(0)
+    need = lib.vae_launch_log_names(None, 0)
+    buf = ctypes.create_string_buffer(int(need))
+    lib.vae_launch_log_names(buf, need)
+    out = []
+    for line in buf.value.decode(errors="replace").splitlines():
+        m, _, d = line.partition("\t")
+        out.append((m, d or m))
+    return out
+
+
+def _row_of(kernel, names):
+    """The row of `names` (profile keys) that is this kernel (mangled or demangled form), or None."""
+    m, d = kernel
+    for k in names:
+        if k in (m, d):
+            return k
+    return None
 
 
 def _profiles(pattern, arch):
@@ -231,36 +252,50 @@ def _profiles(pattern, arch):
     return sorted(paths, key=key, reverse=True)
 
 
-def pmc_traffic(symbols, arch="vanilla"):
-    """HBM bytes per launch of a call's kernels from the newest profiles/*pmc*.json holding them
-    (tools/pmc_summary.py; FETCH_SIZE x2 per MI355X_MICROARCH.md §HBM), with the file and the git
-    HEAD it was measured at.  None when not collected for these kernels."""
-    for path in _profiles("*pmc*.json", arch):
+def _matching_profile(pattern, arch, kernels, digest):
+    """Newest profiles/ summary measured on THIS build (its `digest` equals the loaded library's
+    vae_build_digest, i.e. the same csrc sources) that holds EVERY kernel of the call; else None
+    with the reason."""
+    why = "no profiles/%s summary" % pattern
+    for path in _profiles(pattern, arch):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        got = {k: v.get("hbm_bytes_per_launch") for k, v in d.get("kernels", {}).items()
-               if any(sym in k for sym in symbols)}
-        if got:
-            return {"bytes_per_launch": got, "file": os.path.relpath(path, REPO), "head": d.get("head")}
-    return None
-
-
-def rocprof_times(symbols, arch="vanilla"):
-    """Average duration (us) of a call's kernels in the newest committed rocprofv3 kernel_stats CSV
-    that holds them (file named in the result): the kernels' own time next to the call's."""
-    import csv
-    for path in _profiles("*kernel_stats.csv", arch):
-        try:
-            rows = list(csv.DictReader(open(path)))
-        except Exception:
+        if d.get("digest") != digest:
+            why = f"no {pattern} summary of this build (digest {digest})"
             continue
-        got = {r["Name"][:120]: round(float(r["AverageNs"]) / 1e3, 2) for r in rows
-               if any(sym in r["Name"] for sym in symbols)}
-        if got:
-            return {"avg_us": got, "file": os.path.relpath(path, REPO)}
-    return None
+        rows = {k: _row_of(k_, d.get("kernels", {})) for k_ in kernels for k in [k_[1]]}
+        if any(v is None for v in rows.values()):
+            why = f"{os.path.relpath(path, REPO)} lacks " + ", ".join(k for k, v in rows.items() if v is None)
+            continue
+        return path, d, rows
+    return None, None, why
+
+
+def pmc_traffic(kernels, digest, arch="vanilla"):
+    """HBM bytes per launch of a call = the sum over ITS kernels (tools/pmc_summary.py: 2 x
+    FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM) from a PMC summary of this very build that
+    holds all of them; otherwise None (with the reason)."""
+    path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest)
+    if path is None:
+        return None, rows
+    per = {k: d["kernels"][r].get("hbm_bytes_per_launch") for k, r in rows.items()}
+    if any(v is None for v in per.values()):
+        return None, f"{os.path.relpath(path, REPO)}: no FETCH_SIZE/WRITE_SIZE for every kernel"
+    return {"bytes": sum(per.values()), "bytes_per_kernel": per, "file": os.path.relpath(path, REPO),
+            "digest": d.get("digest"), "head": d.get("head")}, None
+
+
+def rocprof_times(kernels, digest, arch="vanilla"):
+    """Average duration (us) of a call's kernels in a rocprofv3 --kernel-trace --stats summary of
+    this build (tools/prof_summary.py), or None (with the reason)."""
+    path, d, rows = _matching_profile("*kstats*.json", arch, kernels, digest)
+    if path is None:
+        return None, rows
+    per = {k: d["kernels"][r]["avg_us"] for k, r in rows.items()}
+    return {"avg_us": per, "sum_avg_us": round(sum(per.values()), 2), "file": os.path.relpath(path, REPO),
+            "head": d.get("head")}, None
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -503,31 +538,37 @@ def main():
     # ---- dominant kernel: per-launch time with HIP events on the step's stream
     times = time_kernels(plan)
     costs = kernel_costs(plan, dsz)
-    rows = []
+    rows, rows_ref = [], []
     for (fn, ref, us), (_, _, fl, by) in zip(times, costs):
         rows.append((us, fn, fl, by))
+        rows_ref.append(ref)
     if args.kernel_breakdown:
         for us, fn, fl, by in rows:
             print(f"{fn:28s} {us:9.2f} us  {fl / 1e9:8.3f} GF  {by / 1e6:8.2f} MB  "
                   f"{(fl / us / 1e6) if us else 0:8.1f} TF/s  {(by / us / 1e3) if us else 0:8.1f} GB/s",
                   file=sys.stderr)
-    us, fn, fl, by = max(rows, key=lambda r: r[0])
+    idx = max(range(len(rows)), key=lambda i: rows[i][0])
+    us, fn, fl, by = rows[idx]
     ai = fl / by if by else 0.0
     peak_tf = MFMA_PEAK_TFLOPS[args.dtype]
     ridge = peak_tf * 1e12 / (HBM_PEAK_GBS * 1e9)
-    idx = [r[1] for r in rows].index(fn)
     if ai >= ridge:
         roof = {"bound": "mfma", "achieved": round(fl / (us * 1e-6) / 1e12, 3), "peak": peak_tf, "unit": "TFLOP/s"}
     else:
         roof = {"bound": "hbm", "achieved": round(by / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
-    syms = KERNEL_SYMBOLS.get(fn, [])
-    tr = pmc_traffic(syms, args.arch) if syms else None
-    roof["traffic"] = (sum(v for v in tr["bytes_per_launch"].values() if v) if tr else None)
-    roof["traffic_source"] = tr
-    roof["kernel"] = f"{fn} (call #{idx} of the step; its kernels: {', '.join(syms) or 'n/a'})"
+    from vae_amd import _lib as L
+    digest = L.load().vae_build_digest().decode()
+    kernels = call_kernels(fn, rows_ref[idx])
+    tr, why_tr = pmc_traffic(kernels, digest, args.arch)
+    roof["traffic"] = tr["bytes"] if tr else None
+    roof["traffic_ratio"] = round(tr["bytes"] / by, 3) if tr and by else None
+    roof["traffic_source"] = tr if tr else {"missing": why_tr}
+    roof["kernel"] = f"{fn} (call #{idx} of the step; its kernels: {', '.join(k[1] for k in kernels) or 'n/a'})"
     roof["us_per_launch"] = round(us, 2)
-    roof["rocprof"] = rocprof_times(syms, args.arch) if syms else None
+    rp, why_rp = rocprof_times(kernels, digest, args.arch)
+    roof["rocprof"] = rp if rp else {"missing": why_rp}
+    roof["build_digest"] = digest
     roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}
     step_kernel_us = sum(r[0] for r in rows)
     # the step-level attainable time — every kernel at its own roofline bound,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 14
+#define VAE_ABI_VERSION 15
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -301,6 +301,16 @@ typedef struct vae_recon_args {
 
 int vae_abi_version(void);
 const char* vae_last_error(void);
+/* Build identity and launch introspection (measurement tooling; no GPU work).
+ * vae_build_digest: a digest of the sources this library was compiled from (csrc + this header),
+ *   written into profiles so a counter summary is only ever matched with the code it measured.
+ * vae_launch_log(1) starts recording (per host thread) the device kernels every later entry point
+ *   launches, vae_launch_log(0) stops; vae_launch_log_names writes the recorded kernels as lines
+ *   "<mangled>\t<demangled>\n" into buf (NUL-terminated, truncated to cap) and returns the bytes
+ *   the full text needs. */
+const char* vae_build_digest(void);
+int vae_launch_log(int32_t on);
+int64_t vae_launch_log_names(char* buf, int64_t cap);
 
 /* --- Conv2d (encoder block, vanilla_vae.py:28-29 run at :84) ----------------------- */
 int vae_conv2d_fwd(const vae_conv_args* a, void* stream);

@@ -61,10 +61,32 @@ inline int with_ws_tail(long tail, F&& f) {
   q.need = outer > inner ? outer : inner;
   return rc;
 }
+// Launch log (host, per thread): while on, every VAE_LAUNCH records its kernel's host stub, so a
+// measurement tool can ask which device kernels one ABI call launched (vae_launch_log /
+// vae_launch_log_names) and match them against rocprofv3 rows instead of a hand-kept table.
+struct LaunchLog {
+  int on;
+  int n;
+  const void* k[64];
+};
+inline LaunchLog& launch_log() {
+  static thread_local LaunchLog l = {0, 0, {}};
+  return l;
+}
+inline void log_launch(const void* k) {
+  LaunchLog& l = launch_log();
+  if (!l.on) return;
+  for (int i = 0; i < l.n; ++i)
+    if (l.k[i] == k) return;
+  if (l.n < 64) l.k[l.n++] = k;
+}
 }  // namespace vae
-#define VAE_LAUNCH(...)                                         \
+#define VAE_LAUNCH(K, ...)                                      \
   do {                                                          \
-    if (!::vae::querying()) hipLaunchKernelGGL(__VA_ARGS__);    \
+    if (!::vae::querying()) {                                   \
+      ::vae::log_launch((const void*)(K));                      \
+      hipLaunchKernelGGL(K, __VA_ARGS__);                       \
+    }                                                           \
   } while (0)
 namespace vae {
 

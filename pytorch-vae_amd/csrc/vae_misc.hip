@@ -1,8 +1,10 @@
 // Non-GEMM kernels of the VAE step: the decoder head (final Conv2d(C->3)+Tanh+SSE, a thin-N
 // layer that would waste 13/16 of an MFMA tile, so it runs on the VALU with its input tile
 // staged once in LDS), the reparameterization, the ELBO reductions, Adam, and utilities.
+#include <cxxabi.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <math.h>
 
@@ -624,6 +626,30 @@ int grid_for(long n, int per_block = 256, int max_blocks = 2048) {
 using namespace vae;
 
 extern "C" int vae_abi_version(void) { return VAE_ABI_VERSION; }
+
+extern "C" int vae_launch_log(int32_t on) {
+  LaunchLog& l = launch_log();
+  if (on) l.n = 0;
+  l.on = on ? 1 : 0;
+  return VAE_OK;
+}
+
+extern "C" int64_t vae_launch_log_names(char* buf, int64_t cap) {
+  const LaunchLog& l = launch_log();
+  int64_t need = 0;
+  for (int i = 0; i < l.n; ++i) {
+    const char* m = hipKernelNameRefByPtr(l.k[i], nullptr);
+    if (!m) m = "?";
+    int st = 0;
+    char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+    const int w = snprintf(buf && need < cap ? buf + need : nullptr, buf && need < cap ? (size_t)(cap - need) : 0,
+                           "%s\t%s\n", m, (st == 0 && d) ? d : m);
+    free(d);
+    need += w > 0 ? w : 0;
+  }
+  if (buf && cap > 0 && need >= cap) buf[cap - 1] = '\0';
+  return need + 1;
+}
 extern "C" const char* vae_last_error(void) { return g_err; }
 
 #ifdef VAE_PROBE

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -139,6 +139,9 @@ class LatentArgs(ctypes.Structure):
 _SIGS = {
     "vae_abi_version": [],
     "vae_last_error": [],
+    "vae_build_digest": [],
+    "vae_launch_log": [c_int32],
+    "vae_launch_log_names": [ctypes.c_char_p, c_int64],
     "vae_conv2d_fwd": [POINTER(ConvArgs), c_void_p],
     "vae_conv2d_bwd_data": [POINTER(ConvArgs), c_void_p],
     "vae_conv2d_bwd_filter": [POINTER(ConvArgs), c_void_p],
@@ -198,7 +201,8 @@ def load(path: str = LIB_PATH):
     for name, argtypes in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = ctypes.c_char_p if name == "vae_last_error" else c_int32
+        fn.restype = (ctypes.c_char_p if name in ("vae_last_error", "vae_build_digest") else
+                      c_int64 if name == "vae_launch_log_names" else c_int32)
     if lib.vae_abi_version() != ABI_VERSION:
         raise VaeHipError(f"libvaehip ABI {lib.vae_abi_version()} != expected {ABI_VERSION}")
     _lib = lib
@@ -277,6 +281,9 @@ class FilterBatch:
         self.items = (c_void_p * n)(*[ctypes.addressof(ref._obj) for _, ref in self.calls])
         self.workspace, self.workspace_bytes = None, 0
         self.side = False            # run on the plan's side stream (net.run_calls)
+        # scalar-argument calls that read this batch's output (vae_unpad_accumulate of a padded
+        # gradient): run right behind it on the same stream, whichever stream that is
+        self.after = []
 
     @property
     def args(self):
@@ -290,3 +297,5 @@ class FilterBatch:
     def __call__(self, stream):
         call("vae_conv_bwd_filter_batch", len(self.calls), self.kinds, self.items, self.workspace,
              self.workspace_bytes, stream)
+        for fn, args in self.after:
+            call(fn, *args, stream)

@@ -100,17 +100,34 @@ class ImgDifficultySampler:
         self.img_weights = np.maximum(self.img_weights, floor)
 
 
+def resized_size(w: int, h: int, size: int):
+    """torchvision transforms.Resize(int) output (w, h): the SHORTER edge becomes `size`, the longer
+    one int(size * long / short) (torchvision _compute_resized_output_size; dataset.py:78)."""
+    short, long_ = (w, h) if w <= h else (h, w)
+    if short == size:
+        return w, h
+    new_long = int(size * long_ / short)
+    return (size, new_long) if w <= h else (new_long, size)
+
+
 def load_images(paths: Sequence[str], size: int, device=None) -> torch.Tensor:
-    """default_loader (RGB) + Resize(size) + ToTensor, kept as uint8 [N, 3, size, size] (the
-    ToTensor scale 1/255 is applied per batch on the device).  Resize of a square image to
-    (size, size) with PIL's bilinear filter, torchvision's default for PIL inputs."""
+    """default_loader (RGB) + Resize(size) + ToTensor (dataset.py:78-79), kept as uint8
+    [N, 3, size, size] (the ToTensor scale 1/255 is applied per batch on the device).  Resize(int)
+    scales the shorter edge to `size` with PIL's bilinear filter (torchvision's default for PIL
+    inputs) and keeps the aspect ratio; a non-square image therefore comes out non-square, which the
+    reference's models cannot take (their flatten sizes assume size x size, vanilla_vae.py:36) — such
+    an image is rejected here with its name instead of failing later inside the model."""
     from PIL import Image
     out = torch.empty(len(paths), 3, size, size, dtype=torch.uint8)
     for i, p in enumerate(paths):
         with Image.open(p) as im:
             im = im.convert("RGB")
-            if im.size != (size, size):
-                im = im.resize((size, size), Image.BILINEAR)
+            tgt = resized_size(im.size[0], im.size[1], size)
+            if tgt != (size, size):
+                raise ValueError(f"{p}: {im.size[0]}x{im.size[1]} resizes to {tgt[0]}x{tgt[1]} under "
+                                 f"Resize({size}) (shorter edge to {size}); the models take {size}x{size} images")
+            if im.size != tgt:
+                im = im.resize(tgt, Image.BILINEAR)
             a = np.asarray(im, dtype=np.uint8)
         out[i] = torch.from_numpy(a.copy()).permute(2, 0, 1)
     return out.to(device) if device is not None else out
@@ -181,7 +198,8 @@ class VAEDataset:
             return
         per = -(-n // self.world)
         order = list(range(n))
-        order += order[:per * self.world - n] if n else []
+        if n:   # DistributedSampler: repeat the list as often as needed (the pad may exceed n)
+            order = (order * -(-(per * self.world) // n))[:per * self.world]
         mine = order[self.rank::self.world]
         for i in range(0, len(mine), bs):
             yield s.batch(mine[i:i + bs])

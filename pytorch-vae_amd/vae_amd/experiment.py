@@ -349,6 +349,13 @@ def _fusable(model) -> bool:
     return getattr(model, "center_focus_sigma", None) is None and getattr(model, "mssim", None) is None
 
 
+def _owns_flat(opt, model) -> bool:
+    """A torch.optim.Adam with one parameter group holding model.flat (what GraphedSteps can share)."""
+    flat = getattr(model, "flat", None)
+    return (flat is not None and type(opt) is torch.optim.Adam and len(opt.param_groups) == 1
+            and any(q is flat for q in opt.param_groups[0]["params"]))
+
+
 def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=None,
         engine: str = "graph") -> List[Dict[str, float]]:
     """Minimal Trainer loop over an iterable of (imgs, labels, names) batches: the reference's
@@ -368,7 +375,10 @@ def fit(experiment: VAEXperiment, train_batches, epochs: int = 1, val_batches=No
         optims = opt_cfg
     graphed = None
     if engine == "graph":
-        if hasattr(experiment.model, "fused_train_step") and len(optims) == 1 and _fusable(experiment.model):
+        # the fused step shares the torch optimizer's state: only a plain Adam over model.flat
+        # (configure_optimizers' own); any other setup keeps the eager path instead of raising
+        if (hasattr(experiment.model, "fused_train_step") and len(optims) == 1 and _fusable(experiment.model)
+                and _owns_flat(optims[0], experiment.model)):
             graphed = GraphedSteps(experiment, optims[0])
     elif engine != "eager":
         raise ValueError(f"engine {engine!r}")

@@ -203,6 +203,7 @@ class StepPlan:
             self.y8 = torch.zeros(BS, img, img, 8, dtype=T, device=dev)
             self.g8 = torch.zeros(BS, img, img, 8, dtype=T, device=dev)
             self.w8h = torch.zeros(8 * 9 * r[-1], dtype=T, device=dev)
+            self.b8h = torch.zeros(8, dtype=torch.float32, device=dev)   # bias padded alike (lanes 3..7 stay 0)
         self.recon = torch.empty(BS, 3, img, img, **f32)
         self.grad_recon = None if fused_loss else torch.zeros(BS, 3, img, img, **f32)
         self.out = torch.zeros(4, **f32)                                  # loss, recon, KLD(report), kld
@@ -435,6 +436,8 @@ class StepPlan:
         if self.wide_head:          # head weights [3][3][3][C] -> [8][3][3][C] (one row of 27C -> 72C)
             F.append(("vae_pad_channels", (T, 1, 27 * r[-1], 72 * r[-1], net.w("final_layer.3.weight"),
                                            self.w8h.data_ptr())))
+            # the GEMM epilogue reads 8 bias values (its N): pad the 3-element bias too
+            F.append(("vae_pad_channels", (L.F32, 1, 3, 8, net.p("final_layer.3.bias"), self.b8h.data_ptr())))
         # ---------------------------------------------------------------- encoder
         sp = img
         for i in range(nenc):
@@ -697,7 +700,7 @@ class StepPlan:
         a.x = self.fin.data_ptr()
         a.x_xf = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin), running=True)
         a.wt = self.w8h.data_ptr()
-        a.bias = net.p("final_layer.3.bias")     # (channels 3..7 of y8 are never read)
+        a.bias = self.b8h.data_ptr()              # (channels 3..7 of y8 are never read)
         a.y = self.y8.data_ptr()
         self._add(F, "vae_conv2d_fwd", a)
         rc = L.ReconArgs(dtype=T, n=BS, h=img, w=img, c=3, ld=8)
@@ -841,7 +844,12 @@ def batch_filter_calls(calls, ends, splits=()):
             b = L.FilterBatch(wg)
             b.side = side
             out.append((BATCH_FN, b))
-            out.extend((fn, ref) for fn, ref in deferred if fn == "vae_unpad_accumulate")
+            unpads = [(fn, ref) for fn, ref in deferred if fn == "vae_unpad_accumulate"]
+            if side:
+                # they read the batch's padded gradients: same (side) stream, right behind it
+                b.after = unpads
+            else:
+                out.extend(unpads)
         else:
             out.extend(deferred)
 

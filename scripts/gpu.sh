@@ -12,9 +12,11 @@
 #   quick            VanillaVAE bench, 200 steps, no CPU baseline, per-call breakdown
 #   qenv:V=x,W=y     the quick bench with environment overrides (tunable sweeps)
 #   arch:A:B         bench --arch A --batch B (betaH, iwae, vq, ae_big ...), no CPU baseline
+#   archcpu:A:B      the same with the CPU baseline legs (the oracle on the host cores)
 #   prof             rocprofv3 --kernel-trace --stats over a short VanillaVAE bench
 #   prof:A:B         the same for --arch A --batch B
-#   pmc              PMC passes (SQ / MFMA / FETCH / WRITE) of the VanillaVAE step, one run each
+#   pmc              PMC passes (SQ / MFMA / FETCH / WRITE) of the graph-replayed VanillaVAE step, one
+#                    run each; summary stamped with the build digest and GIT_HEAD (pass GIT_HEAD=...)
 #   pmc:A:B          the same for --arch A --batch B
 #   kprobe           per-block phase probe (needs `make probe`)
 #   kbench[:ARGS]    per-launch microbench under a kernel trace (tools/kbench.py, ARGS comma-separated)
@@ -42,12 +44,15 @@ prof() {  # name bench-args...
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
      -d $O/${TAG}_${name} -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-dropin "$@") \
-     > $O/${TAG}_${name}.log 2>&1
+     > $O/${TAG}_${name}.log 2>&1 || return $?
+  cd $R && python3 tools/prof_summary.py --dir $O/${TAG}_${name} --out $O/${TAG}_${name}_kstats.json \
+     --config "bench.py --steps 20 --warmup 5 $*" >> $O/${TAG}_${name}.log 2>&1
 }
 
 pmc() {   # name bench-args...   (one counter group per run: rocprofv3 does not split passes)
+  # the graph-replayed step (the timed one); PMCNOGRAPH=1 profiles the eager launch sequence
   local name=$1; shift
-  local B="python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-graph --no-dropin $*"
+  local B="python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-dropin ${PMCNOGRAPH:+--no-graph} $*"
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES --output-format csv -d $O/${TAG}_${name}_pa -o run -- $B > $O/${TAG}_${name}_pa.log 2>&1 || return $?
   timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU_MFMA_MOPS_BF16 FETCH_SIZE --output-format csv -d $O/${TAG}_${name}_pb -o run -- $B > $O/${TAG}_${name}_pb.log 2>&1 || return $?
@@ -65,6 +70,7 @@ for step in "$@"; do
     quick) run quick 300 python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --kernel-breakdown ;;
     qenv) run qenv_${a1//[=,]/_} 300 env ${a1//,/ } python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-dropin ;;
     arch) run arch_${a1}_${a2} 300 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --no-cpu-baseline --kernel-breakdown ;;
+    archcpu) run archcpu_${a1}_${a2} 400 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --kernel-breakdown ;;
     prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;
     pmc) if [ -n "$a1" ]; then pmc pmc_$a1 --arch $a1 --batch $a2; else pmc pmc; fi ;;
     kprobe) run kprobe 200 env VAE_HIP_LIB=probe python3 -u tools/kprobe.py --out $O/${TAG}_kp.json ;;

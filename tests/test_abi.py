@@ -10,7 +10,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(vae_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(vae_\w+)\(", src, flags=re.M)))
 
 
 def test_library_loads_and_abi_version():
@@ -51,3 +51,29 @@ def test_activation_backward_epilogue_without_aux_is_rejected():
     a.dx_epi = L.Xform(kind=L.X_ACT, channels=8, slope=0.01)
     rc = lib.vae_conv2d_bwd_data(ctypes.byref(a), None)
     assert rc == -1 and b"aux" in lib.vae_last_error()
+
+
+def test_build_digest_names_the_sources():
+    """vae_build_digest() = sha256 (16 hex) of the csrc sources + vaehip.h the library was built
+    from (Makefile); profiles/ summaries carry it and bench.py pairs them by it."""
+    import glob
+    import hashlib
+    lib = L.load()
+    d = lib.vae_build_digest().decode()
+    assert re.fullmatch(r"[0-9a-f]{16}", d)
+    csrc = os.path.join(os.path.dirname(HEADER), "..", "pytorch-vae_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")),
+                   key=lambda p: os.path.basename(p)) + [HEADER]
+    h = hashlib.sha256(b"".join(open(f, "rb").read() for f in files)).hexdigest()[:16]
+    assert d == h, "libvaehip.so is stale: rebuild (make -C pytorch-vae_amd/csrc)"
+
+
+def test_launch_log_without_gpu():
+    """The launch log records nothing for a call rejected before launching, and reports the
+    size of an empty listing."""
+    lib = L.load()
+    assert lib.vae_launch_log(1) == 0
+    a = L.ConvArgs()
+    assert lib.vae_conv2d_fwd(ctypes.byref(a), None) != 0
+    assert lib.vae_launch_log(0) == 0
+    assert lib.vae_launch_log_names(None, 0) == 1

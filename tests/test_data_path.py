@@ -89,7 +89,7 @@ def test_data_module_batches_and_loss_recording(tmp_path):
     assert [b[0].shape[0] for b in vb] == [2]
 
 
-@pytest.mark.parametrize("world,n,bs", [(2, 9, 4), (3, 10, 2), (4, 3, 8), (2, 8, 4)])
+@pytest.mark.parametrize("world,n,bs", [(2, 9, 4), (3, 10, 2), (4, 3, 8), (2, 8, 4), (8, 2, 4), (8, 3, 1)])
 def test_eval_loaders_cover_every_image_on_every_rank_count(world, n, bs):
     """val / test loaders with several ranks evaluate every image (DistributedSampler
     padding: wrap-around to a multiple of world, rank r takes r, r+world, ...) and every rank
@@ -109,3 +109,21 @@ def test_eval_loaders_cover_every_image_on_every_rank_count(world, n, bs):
     assert len(set(counts)) == 1
     assert set(seen) == set(names)
     assert len(seen) == -(-n // world) * world
+
+
+@pytest.mark.parametrize("w,h,want", [(64, 64, (64, 64)), (128, 128, (64, 64)), (128, 96, (85, 64)),
+                                      (96, 128, (64, 85)), (50, 200, (64, 256))])
+def test_resize_follows_torchvision_shorter_edge(w, h, want):
+    """transforms.Resize(int) (dataset.py:78) scales the shorter edge (torchvision
+    _compute_resized_output_size: int(size * long / short) for the other one)."""
+    assert V.resized_size(w, h, 64) == want
+
+
+def test_load_images_rejects_non_square(tmp_path):
+    from PIL import Image
+    Image.new("RGB", (96, 128), (10, 20, 30)).save(tmp_path / "a.png")
+    Image.new("RGB", (128, 128), (10, 20, 30)).save(tmp_path / "b.png")
+    x = V.load_images([str(tmp_path / "b.png")], 64)
+    assert x.shape == (1, 3, 64, 64) and int(x[0, 1, 5, 5]) == 20
+    with pytest.raises(ValueError, match="64x85"):
+        V.load_images([str(tmp_path / "a.png")], 64)

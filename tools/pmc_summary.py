@@ -37,6 +37,30 @@ def load(dirs):
     return per, dur
 
 
+def build_identity():
+    """(digest, head) of the measured build: vae_build_digest() of the in-tree libvaehip.so (the
+    digest of the csrc sources it was compiled from; bench.py only pairs a summary with a library of
+    the same digest) and the git HEAD the tree was sent from (GIT_HEAD, set by the caller — the GPU
+    box's copy of the tree has no .git; `git rev-parse` where it does)."""
+    import ctypes
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        lib = ctypes.CDLL(os.path.join(repo, "pytorch-vae_amd", "vae_amd", "libvaehip.so"))
+        lib.vae_build_digest.restype = ctypes.c_char_p
+        digest = lib.vae_build_digest().decode()
+    except Exception:
+        digest = None
+    head = os.environ.get("GIT_HEAD") or None
+    if head is None:
+        try:
+            head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
+                                  cwd=repo).stdout.strip() or None
+        except Exception:
+            head = None
+    return digest, head
+
+
 def mean(v):
     return sum(v) / len(v) if v else None
 
@@ -75,13 +99,8 @@ def main():
         for name in ("GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"):
             if name in c:
                 tot[name] += sum(c[name])
-    import subprocess
-    try:
-        head = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
-                              cwd=os.path.dirname(os.path.abspath(__file__))).stdout.strip() or None
-    except Exception:
-        head = None
-    summary = {"config": args.config, "sources": args.dirs, "head": head,
+    digest, head = build_identity()
+    summary = {"config": args.config, "sources": args.dirs, "digest": digest, "head": head,
                "all_vae_dispatches_mfma_busy": (round(tot["SQ_VALU_MFMA_BUSY_CYCLES"] /
                                                      (tot["GRBM_GUI_ACTIVE"] / 8 * 1024), 4)
                                                if tot["GRBM_GUI_ACTIVE"] else None),
