@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 15
+#define VAE_ABI_VERSION 16
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -498,6 +498,14 @@ typedef struct vae_latent_args {
   float* dx_dgamma; float* dx_dbeta;
   int32_t sum_reps, sum_rstride;
   float* dw1; float* db1;            /* fp32, accumulated */
+  /* eps_gen = 1: vae_latent_dec_fwd DRAWS eps ~ N(0,1) itself (torch.randn_like(std) of
+   * reparameterize, vanilla_vae.py:116, every step) and writes it to `eps` (an output then) for the
+   * backward: Philox4x32-10 keyed by eps_seed, counter (element/4, *eps_step, 0x5EED, 0), then
+   * Box-Muller on each pair of words.  *eps_step is the device step counter vae_step_begin_ex
+   * advances, so every replay of a captured step draws fresh noise.  eps_gen = 0: eps is read. */
+  const int32_t* eps_step;
+  uint64_t eps_seed;
+  int32_t eps_gen;
 } vae_latent_args;
 int vae_latent_fc_fwd(const vae_latent_args* a, void* stream);
 int vae_latent_dec_fwd(const vae_latent_args* a, void* stream);

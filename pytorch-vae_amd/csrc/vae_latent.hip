@@ -46,6 +46,31 @@ __device__ __forceinline__ uint4 ld16(const void* p) { return *reinterpret_cast<
 __device__ __forceinline__ f32x4 ld4f(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 constexpr uint4 kZero4 = {0u, 0u, 0u, 0u};
 
+// Philox4x32-10 (Salmon et al., SC'11): 4 x 32 random bits per (counter, key)
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = uint4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+// four N(0,1) draws for eps elements 4q..4q+3 of step `step` (Box-Muller on word pairs; u in (0, 1])
+__device__ __forceinline__ f32x4 normal4(uint32_t q, uint32_t step, uint64_t seed) {
+  const uint4 w = philox4x32_10(uint4{q, step, 0x5EEDu, 0u}, (uint32_t)seed, (uint32_t)(seed >> 32));
+  constexpr float kInv = 2.3283064365386963e-10f;               // 2^-32
+  const float u0 = ((float)w.x + 0.5f) * kInv, v0 = (float)w.y * kInv;
+  const float u1 = ((float)w.z + 0.5f) * kInv, v1 = (float)w.w * kInv;
+  const float r0 = sqrtf(-2.f * logf(u0)), r1 = sqrtf(-2.f * logf(u1));
+  float s0, c0, s1, c1;
+  sincosf(6.283185307179586f * v0, &s0, &c0);
+  sincosf(6.283185307179586f * v1, &s1, &c1);
+  return f32x4{r0 * c0, r0 * s0, r1 * c1, r1 * s1};
+}
+
 // One wave's 16-row x (16*TN)-column block of a tile, ksteps of 32, from k-contiguous LDS rows:
 // A rows ar0.., B rows bc0.. (lda / ldb elements apart).
 template <int TN>
@@ -195,6 +220,8 @@ __global__ void __launch_bounds__(256) latent_dec_fwd_kernel(const vae_latent_ar
     bv[i] = ld16(w2 + (long)(n0 + r) * D + 8 * kc);
   }
   const bool rep = a.eps != nullptr;
+  const bool gen = a.eps_gen != 0;                 // draw eps here (host-checked: eps, eps_step set)
+  const uint32_t step = gen ? (uint32_t)*a.eps_step : 0u;
   f32x4 mu[NA][2], lv[NA][2], ep[NA][2];
   uint4 zv[NA];
 #pragma unroll
@@ -208,7 +235,7 @@ __global__ void __launch_bounds__(256) latent_dec_fwd_kernel(const vae_latent_ar
       for (int h = 0; h < 2; ++h) {
         mu[i][h] = ld4f(a.mulv + mb + d0 + 4 * h);
         lv[i][h] = ld4f(a.mulv + mb + D + d0 + 4 * h);
-        ep[i][h] = ld4f(a.eps + eb + d0 + 4 * h);
+        ep[i][h] = gen ? normal4((uint32_t)((eb + d0) / 4 + h), step, a.eps_seed) : ld4f(a.eps + eb + d0 + 4 * h);
       }
     } else {
       zv[i] = ok ? ld16(z + eb + d0) : kZero4;
@@ -234,7 +261,14 @@ __global__ void __launch_bounds__(256) latent_dec_fwd_kernel(const vae_latent_ar
         zz[e] = row < BS ? fmaf(ep[i][h][q], expf(0.5f * lv[i][h][q]), mu[i][h][q]) : 0.f;   // = vae_reparam_fwd
       }
       o = to_bf16x8(zz);
-      if (blockIdx.x == 0 && row < BS) *reinterpret_cast<bf16x8*>(z + (long)row * D + d0) = o;
+      if (blockIdx.x == 0 && row < BS) {
+        *reinterpret_cast<bf16x8*>(z + (long)row * D + d0) = o;
+        if (gen) {                                 // the drawn noise, for the backward (dlogvar)
+          float* e = const_cast<float*>(a.eps) + (long)row * D + d0;
+          *reinterpret_cast<f32x4*>(e) = ep[i][0];
+          *reinterpret_cast<f32x4*>(e + 4) = ep[i][1];
+        }
+      }
     } else {
       o = *reinterpret_cast<const bf16x8*>(&zv[i]);
     }
@@ -608,6 +642,7 @@ extern "C" int vae_latent_dec_fwd(const vae_latent_args* a, void* stream) {
   if (int rc = latent_check(a, "latent_dec_fwd")) return rc;
   if (!a->w2 || !al16(a->w2) || !a->h || !a->z || !al16(a->z)) return fail(VAE_E_BADARG, "latent_dec_fwd: w2 / h / z");
   if (a->eps && (!a->mulv || !al16(a->mulv) || !al16(a->eps))) return fail(VAE_E_BADARG, "latent_dec_fwd: mulv / eps");
+  if (a->eps_gen && (!a->eps || !a->eps_step)) return fail(VAE_E_BADARG, "latent_dec_fwd: eps_gen needs eps and eps_step");
   const int BS = a->batch * a->samples;
   const dim3 grid((unsigned)(a->out_features / 64), (unsigned)((BS + 31) / 32));
   if (a->latent == 128) VAE_LAUNCH(latent_dec_fwd_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, *a);

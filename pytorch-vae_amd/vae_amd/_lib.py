@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -133,7 +133,8 @@ class LatentArgs(ctypes.Structure):
                 ("eps", c_void_p), ("z", c_void_p), ("w2", c_void_p), ("b2", c_void_p), ("h", c_void_p),
                 ("dh", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p), ("dw2", c_void_p), ("db2", c_void_p),
                 ("dx", c_void_p), ("dx_epi", Xform), ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p),
-                ("sum_reps", c_int32), ("sum_rstride", c_int32), ("dw1", c_void_p), ("db1", c_void_p)]
+                ("sum_reps", c_int32), ("sum_rstride", c_int32), ("dw1", c_void_p), ("db1", c_void_p),
+                ("eps_step", c_void_p), ("eps_seed", ctypes.c_uint64), ("eps_gen", c_int32)]
 
 # name -> (argtypes)
 _SIGS = {

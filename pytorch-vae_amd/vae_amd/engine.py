@@ -77,14 +77,19 @@ class TrainStep:
     on fixed-shape device buffers.
 
     Inputs live in `plan.x` (NCHW fp32 images) and `plan.eps` (N(0,1) noise, the reference's
-    torch.randn_like at vanilla_vae.py:116); write them before calling, or pass tensors.
+    torch.randn_like at vanilla_vae.py:116); write them before calling, or pass tensors — or let the
+    step draw eps on the device (device_eps=seed: Philox in the fused bottleneck kernel).
     With more than one rank the backward is cut into segments at gradient-bucket boundaries
     (dp.plan_buckets); each bucket's RCCL all-reduce is launched as soon as its segment is
     queued, so it runs on the communication stream while the rest of the backward computes."""
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
-                 nbuckets: int = 4):
+                 nbuckets: int = 4, device_eps: Optional[int] = None):
         self.net, self.plan, self.opt = net, plan, opt
+        # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
+        # by the optimizer's step counter) — the reference's per-step randn_like inside the step
+        self.device_eps = (device_eps is not None and hasattr(plan, "use_device_eps")
+                           and plan.use_device_eps(opt.step, device_eps))
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.use_graph = graph
@@ -179,6 +184,8 @@ class TrainStep:
         if x is not None:
             self.plan.x.copy_(x)
         if eps is not None:
+            if self.device_eps:
+                raise ValueError("this step draws eps on the device (device_eps); do not pass eps")
             self.plan.eps.copy_(eps.reshape(self.plan.eps.shape))
         if self.use_graph and not self.graphs:
             self._capture()

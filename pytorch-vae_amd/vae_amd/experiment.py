@@ -258,6 +258,10 @@ class GraphedSteps:
             if self.fused is None:
                 self.fused = self._shared_adam()
             step = self.steps[B] = model.fused_train_step(B, opt=self.fused, **self.kw)
+            # eps drawn inside the step on the device (Philox keyed by a seed from torch's generator,
+            # so manual_seed still fixes the run) where the fused bottleneck can; else plan.eps below
+            if hasattr(step.plan, "use_device_eps") and not getattr(step, "zero_eps", False):
+                step.device_eps = step.plan.use_device_eps(self.fused.step, int(torch.randint(0, 2 ** 62, (1,))))
         lr = self.opt.param_groups[0]['lr']
         if lr != self._lr:                            # (a device scalar: written only on change)
             self.fused.set_lr(lr)
@@ -265,7 +269,7 @@ class GraphedSteps:
         self._img_shape = tuple(imgs.shape[1:])
         exp.curr_device = imgs.device
         plan = step.plan
-        if hasattr(plan, "eps") and not getattr(step, "zero_eps", False):
+        if hasattr(plan, "eps") and not getattr(step, "zero_eps", False) and not getattr(step, "device_eps", False):
             plan.eps.normal_()                        # torch.randn_like(std), vanilla_vae.py:116
         step(imgs)
         self.nstep += 1

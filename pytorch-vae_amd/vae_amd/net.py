@@ -736,6 +736,19 @@ class StepPlan:
         Bw.append(("vae_unpad_accumulate", (1, 72 * C, 27 * C, self.dw8h.data_ptr(), self.g("final_layer.3.weight"))))
         Bw.append(("vae_unpad_accumulate", (1, 8, 3, self.db8h.data_ptr(), self.g("final_layer.3.bias"))))
 
+    def use_device_eps(self, step: torch.Tensor, seed: int = 1265) -> bool:
+        """Draw eps ~ N(0,1) on the device inside the forward, every step (the reference's
+        torch.randn_like(std), vanilla_vae.py:116): vae_latent_dec_fwd runs Philox4x32-10 keyed by
+        `seed` with the device step counter `step` (int32, advanced by vae_step_begin[_ex]) and writes
+        the draw to self.eps for the backward.  Only the fused bf16 bottleneck (latent_fused) draws;
+        returns False (eps stays an input) otherwise."""
+        if not self.latent_fused:
+            return False
+        la = self._latent
+        la.eps_gen, la.eps_step, la.eps_seed = 1, step.data_ptr(), seed & 0xFFFFFFFFFFFFFFFF
+        self._eps_step = step                       # keep the counter alive with the plan
+        return True
+
     # ------------------------------------------------------------------ execution
     def _run(self, calls, stream):
         run_calls(self, calls, stream)
