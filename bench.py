@@ -66,9 +66,10 @@ def parse():
                          "patient_vvbig_ae.yaml (MSE, no KL)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--concurrent", choices=["auto", "on", "off"], default="auto",
-                    help="weight gradients on a side stream beside the data-gradient chain; auto = on for "
-                         "VQ-VAE (r1: 9.96 -> 8.51 ms), off for the VanillaVAE family (measured 0.88 vs 0.77 ms: "
-                         "the graph's per-call fork/join edges cost more than the overlap gains)")
+                    help="weight gradients on a side stream beside the data-gradient chain; auto = off: the "
+                         "VanillaVAE family measured 0.88 vs 0.77 ms (r1: the graph's per-call fork/join edges cost "
+                         "more than the overlap gains), VQ-VAE 3.436 on vs 3.330 off at r4 (it was 9.96 -> 8.51 ms "
+                         "in r1, before the image-tile kernels filled the chip on their own)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernel-breakdown", action="store_true", help="print per-kernel times to stderr")
@@ -499,7 +500,7 @@ def main():
     if args.arch == "vq":
         from vae_amd.vq import VQNet, VQStepPlan
         net = VQNet(dtype=dtype, device="cuda", generator=gen)
-        plan = VQStepPlan(net, args.batch, concurrent=args.concurrent != "off")
+        plan = VQStepPlan(net, args.batch, concurrent=args.concurrent == "on")
         opt = FusedAdam(net, lr=0.005)                             # configs/vae/vq_vae.yaml LR
     elif args.arch in AE_WIDTHS:
         # models.Autoencoder's fused step: the VanillaVAE plan with the fc_var half pinned at zero and

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 16
+#define VAE_ABI_VERSION 18
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -326,6 +326,15 @@ int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream);
  * take vae_convT2d_workspace_size(a, VAE_OP_BWD) bytes of workspace; any other layer runs
  * vae_convT2d_bwd_data then vae_convT2d_bwd_filter. */
 int vae_convT2d_bwd(const vae_conv_args* a, void* stream);
+/* The output ConvTranspose2d of the VQ-VAE fused with its Tanh + reconstruction + SSE (+ backward
+ * seed) (vq_vae.py:160-164, :203; what vae_convT2d_fwd followed by vae_recon_fwd(rc) computes,
+ * without storing the pre-tanh output): bf16, wide side [n][32][32][128] (LeakyReLU or none on
+ * load), RGB side packed to 8 channels (k = 8, 3 real; rc->ld = 8).  Other shapes run the two calls
+ * (a->y must then be set).  vae_convT2d_bwd of that layer with dw_inner = 3 runs its data, weight
+ * and bias gradients in one pass (workspace: vae_convT2d_workspace_size(a, VAE_OP_BWD)); the input
+ * Conv2d(3 -> 128, k4 s2) weight gradient of the same network (vae_conv2d_bwd_filter, c = 8 packed,
+ * dw_inner = 3) likewise has its own kernel. */
+int vae_convT2d_fwd_recon(const vae_conv_args* a, const vae_recon_args* rc, void* stream);
 /* --- Linear (fc_mu/fc_var vanilla_vae.py:36-37,89-90; decoder_input :43,101) -------- */
 int vae_linear_fwd(const vae_linear_args* a, void* stream);
 int vae_linear_bwd_data(const vae_linear_args* a, void* stream);
@@ -511,6 +520,41 @@ int vae_latent_fc_fwd(const vae_latent_args* a, void* stream);
 int vae_latent_dec_fwd(const vae_latent_args* a, void* stream);
 int vae_latent_dec_bwd(const vae_latent_args* a, void* stream);
 int vae_latent_fc_bwd(const vae_latent_args* a, void* stream);
+
+/* --- The Autoencoder's other reconstruction losses (forward + backward seed) ----------------------
+ * VAE_RLOSS_CENTER: mean(mask * (recon - target)^2) over n*c*h*w (models/autoencoder.py:95-146,
+ *   :259-265; mask = create_center_weight_mask, [h][w]).
+ * VAE_RLOSS_MSSIM: 1 - prod_{l < L-1} cs_l^w_l * ssim_{L-1}^w_{L-1} over `levels` avg-pooled levels,
+ *   depthwise window = outer(window, window) with zero padding window_size/2, C1 = 1e-4, C2 = 9e-4,
+ *   size_average, (s + 1) / 2 when normalize (models/mssim_vae.py:182-282, autoencoder.py:266-267).
+ *   window[] is the reference's normalised 1-D window (its Gaussian with a POSITIVE exponent).
+ * Writes out[0] = loss, out[1] = Reconstruction_Loss (= loss), out[2] = 0; grad (if set) =
+ * grad_scale * dL/drecon (NCHW fp32), the seed of the fused backward (vae_head_args.grad_recon /
+ * vae_recon_args.grad_recon); per_img (if set with sse) = sse / (c*h*w), the per-image MSE of
+ * experiment.py:60-62.  Planes of up to 64 x 64; workspace: vae_recon_loss_workspace_size. */
+enum vae_recon_loss_kind { VAE_RLOSS_CENTER = 0, VAE_RLOSS_MSSIM = 1 };
+typedef struct vae_recon_loss_args {
+  int32_t kind;
+  int32_t n, c, h, w;
+  const float* recon;        /* NCHW fp32 (img1) */
+  const float* target;       /* NCHW fp32 (img2) */
+  const float* mask;         /* CENTER: [h][w] */
+  float window[16];          /* MSSIM: 1-D window (window_size <= 15, odd) */
+  int32_t window_size;
+  int32_t levels;            /* MSSIM: 5 */
+  float level_weights[8];    /* MSSIM: 0.0448, 0.2856, 0.3001, 0.2363, 0.1333 */
+  int32_t normalize;
+  int32_t size_average;      /* must be 1 (the reference's default) */
+  float* grad;
+  float grad_scale;
+  float* out;                /* [3] */
+  const float* sse;          /* optional [n] */
+  float* per_img;            /* optional [n] */
+  float* workspace;
+  int64_t workspace_bytes;
+} vae_recon_loss_args;
+int vae_recon_loss(const vae_recon_loss_args* a, void* stream);
+int vae_recon_loss_workspace_size(const vae_recon_loss_args* a, size_t* bytes);
 
 #ifdef __cplusplus
 }

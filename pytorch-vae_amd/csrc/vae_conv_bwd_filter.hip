@@ -3,6 +3,7 @@
 #include "vae_wgrad.hpp"
 #include "vae_wgemm.hpp"
 #include "vae_c3.hpp"
+#include "vae_rgb.hpp"
 
 using namespace vae;
 
@@ -11,6 +12,10 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "conv2d_bwd_filter") || !a->dy || !a->x || !a->dw) return fail(VAE_E_BADARG, "conv2d_bwd_filter: null tensor");
   if (!xf_ok(a->dy_xf, "conv2d_bwd_filter.dy") || !xf_ok(a->x_xf, "conv2d_bwd_filter.x")) return VAE_E_BADARG;
   const bool closed = a->db && a->dy_xf.kind == VAE_X_BN_DY;   // Σdy from the BN sums
+  if (a->dtype == VAE_BF16) {                                   // the VQ-VAE's input Conv2d(3 -> C, k4 s2)
+    const int rc = rgb_in_wgrad_launch(a, (hipStream_t)stream);
+    if (rc != kHeadFallback) return rc;
+  }
   // 3x3 stride-1 on a 16 x 16 grid (the VQ-VAE's residual stacks): image-group tiles with the
   // halo patch staged once per image (vae_c3.hip); needs a workspace for the partial slabs
   if (a->dtype == VAE_BF16 && !a->x_nchw_f32 && c3_enabled() && (a->workspace || querying()) &&

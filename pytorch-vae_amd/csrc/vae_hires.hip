@@ -16,6 +16,7 @@
 //     accumulators (the producer contract of vaehip.h y_sum), and stores the rows through LDS as
 //     whole 4 KB rows (16 B per lane).
 #include "vae_launch.hpp"
+#include "vae_rgb.hpp"
 
 namespace vae {
 namespace {
@@ -550,7 +551,9 @@ extern "C" int vae_convT2d_bwd(const vae_conv_args* a, void* stream) {
   if (!vae::geom_ok(a, "convT2d_bwd")) return VAE_E_BADARG;
   if (!a->dy || !a->x || !a->dw || !a->dx || !a->wt) return vae::fail(VAE_E_BADARG, "convT2d_bwd: null tensor");
   if (a->dtype == VAE_BF16) {
-    const int rc = vae::hires_convT_bwd_launch(a, (hipStream_t)stream);
+    int rc = vae::rgb_out_bwd_launch(a, (hipStream_t)stream);     // the VQ-VAE's output ConvT(C -> 3)
+    if (rc != vae::kHeadFallback) return rc;
+    rc = vae::hires_convT_bwd_launch(a, (hipStream_t)stream);
     if (rc != vae::kHeadFallback) return rc;
   }
   if (int rc = vae_convT2d_bwd_data(a, stream)) return rc;

@@ -1,20 +1,10 @@
 // C-ABI entry points of the Linear layers: fc_mu|fc_var fused as one N=2D layer
-// (models/vanilla_vae.py:36-37, :89-90) and decoder_input (:43, :101).
+// (models/vanilla_vae.py:36-37, :89-90) and decoder_input (:43, :101).  One entry point per
+// translation unit: each instantiates its own family of generic GEMM kernels, and one file with all
+// three was the build's longest compile (~10 min); apart they build in parallel.
 #include "vae_launch.hpp"
 
 using namespace vae;
-
-extern "C" int vae_linear_fwd(const vae_linear_args* a, void* stream) {
-  if (!a || !a->x || !a->wt || !a->y || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_fwd: args");
-  if (!xf_ok(a->x_xf, "linear_fwd.x")) return VAE_E_BADARG;
-  GemmParams p = base_params();
-  p.M = a->m; p.N = a->n; p.K = a->k;
-  p.a_ptr = a->x; p.a_ld = a->k; p.a_xf = sanitize(a->x_xf);
-  p.b_ptr = a->wt; p.b_ld = a->k;
-  p.out = a->y; p.out_ld = a->n; p.bias = a->bias; p.out_f32 = a->y_f32;
-  return launch<A_DENSE, B_NK, E_STORE, false, false>(a->dtype, false, false, p, 0, a->workspace, a->workspace_bytes,
-                                        (hipStream_t)stream);
-}
 
 // dx[m][k] = Σ_n dy[m][n] · W[n][k];  epilogue: activation backward (dx_epi) or, when
 // mulv is set, the reparameterization + KL backward into dmulv
@@ -40,17 +30,4 @@ extern "C" int vae_linear_bwd_data(const vae_linear_args* a, void* stream) {
   if (int rc = check_finalize(a->bn_finalize, a->bn_counter, "linear_bwd_data")) return rc;
   return then_finalize(launch<A_DENSE, B_KN, E_BNBWD, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, a->workspace, a->workspace_bytes,
                                               (hipStream_t)stream), a->bn_finalize, (hipStream_t)stream);
-}
-
-// dW[n][k] += Σ_m dy[m][n] · xf(x)[m][k];  db[n] += Σ_m dy[m][n]  (ones column)
-extern "C" int vae_linear_bwd_filter(const vae_linear_args* a, void* stream) {
-  if (!a || !a->dy || !a->x || !a->dw || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_bwd_filter: args");
-  if (!xf_ok(a->x_xf, "linear_bwd_filter.x")) return VAE_E_BADARG;
-  GemmParams p = base_params();
-  p.M = a->n; p.N = a->k + (a->db ? 1 : 0); p.K = a->m;
-  p.ones_col = a->db ? a->k : -1; p.bias_grad = a->db;
-  p.a_ptr = a->dy; p.a_ld = a->n;
-  p.b_ptr = a->x; p.b_ld = a->k; p.b_xf = sanitize(a->x_xf);
-  p.out = a->dw; p.out_ld = a->k;
-  return launch<A_KM, B_KN, E_ACC, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, nullptr, 0, (hipStream_t)stream);
 }

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 16
+ABI_VERSION = 18
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -101,6 +101,19 @@ class ReconArgs(ctypes.Structure):
                 ("grad_scale", c_float), ("grad_recon", c_void_p), ("ld", c_int32)]
 
 
+class ReconLossArgs(ctypes.Structure):
+    """vaehip.h vae_recon_loss_args (the Autoencoder's centre-weighted MSE / MS-SSIM)."""
+    _fields_ = [("kind", c_int32), ("n", c_int32), ("c", c_int32), ("h", c_int32), ("w", c_int32),
+                ("recon", c_void_p), ("target", c_void_p), ("mask", c_void_p), ("window", c_float * 16),
+                ("window_size", c_int32), ("levels", c_int32), ("level_weights", c_float * 8),
+                ("normalize", c_int32), ("size_average", c_int32), ("grad", c_void_p), ("grad_scale", c_float),
+                ("out", c_void_p), ("sse", c_void_p), ("per_img", c_void_p), ("workspace", c_void_p),
+                ("workspace_bytes", c_int64)]
+
+
+RLOSS_CENTER, RLOSS_MSSIM = 0, 1
+
+
 class RecordArgs(ctypes.Structure):
     _fields_ = [("batch", c_int32), ("samples", c_int32), ("img_elems", c_int32), ("nterms", c_int32),
                 ("step", c_int32), ("src_terms", c_void_p), ("terms", c_void_p), ("per_img", c_void_p),
@@ -150,6 +163,7 @@ _SIGS = {
     "vae_convT2d_bwd_data": [POINTER(ConvArgs), c_void_p],
     "vae_convT2d_bwd_filter": [POINTER(ConvArgs), c_void_p],
     "vae_convT2d_bwd": [POINTER(ConvArgs), c_void_p],
+    "vae_convT2d_fwd_recon": [POINTER(ConvArgs), POINTER(ReconArgs), c_void_p],
     "vae_linear_fwd": [POINTER(LinearArgs), c_void_p],
     "vae_linear_bwd_data": [POINTER(LinearArgs), c_void_p],
     "vae_linear_bwd_filter": [POINTER(LinearArgs), c_void_p],
@@ -184,6 +198,8 @@ _SIGS = {
     "vae_latent_dec_fwd": [POINTER(LatentArgs), c_void_p],
     "vae_latent_dec_bwd": [POINTER(LatentArgs), c_void_p],
     "vae_latent_fc_bwd": [POINTER(LatentArgs), c_void_p],
+    "vae_recon_loss": [POINTER(ReconLossArgs), c_void_p],
+    "vae_recon_loss_workspace_size": [POINTER(ReconLossArgs), POINTER(ctypes.c_size_t)],
 }
 EXPORTED = tuple(_SIGS)
 
@@ -300,3 +316,29 @@ class FilterBatch:
              self.workspace_bytes, stream)
         for fn, args in self.after:
             call(fn, *args, stream)
+
+
+def recon_loss_args(kind: int, n: int, c: int, h: int, w: int, *, mask=None, window=None, levels: int = 5,
+                    level_weights=(0.0448, 0.2856, 0.3001, 0.2363, 0.1333), normalize: bool = True) -> "ReconLossArgs":
+    """A vae_recon_loss argument block with the loss's constants filled in (pointers left to the caller):
+    kind RLOSS_CENTER with `mask` ([h][w] device tensor), or RLOSS_MSSIM with the 1-D `window`
+    (models.MSSIM's normalised window, host floats)."""
+    a = ReconLossArgs(kind=kind, n=n, c=c, h=h, w=w, size_average=1, grad_scale=1.0)
+    if kind == RLOSS_CENTER:
+        a.mask = mask.data_ptr()
+    else:
+        win = [float(v) for v in window]
+        a.window_size = len(win)
+        for i, v in enumerate(win):
+            a.window[i] = v
+        a.levels = levels
+        for i, v in enumerate(level_weights):
+            a.level_weights[i] = float(v)
+        a.normalize = int(normalize)
+    return a
+
+
+def recon_loss_workspace(a: "ReconLossArgs") -> int:
+    out = ctypes.c_size_t(0)
+    call("vae_recon_loss_workspace_size", ctypes.byref(a), ctypes.byref(out))
+    return int(out.value)

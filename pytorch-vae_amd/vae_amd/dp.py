@@ -102,14 +102,32 @@ def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4
     return merged
 
 
+class _MeanWork:
+    """A gloo SUM all-reduce still in flight, whose wait() also applies the 1/world scale (gloo has
+    no AVG): the caller keeps queueing work (the next backward segments) until it waits, as with
+    RCCL's AVG handle."""
+
+    def __init__(self, work, t: torch.Tensor, world: int):
+        self.work, self.t, self.world = work, t, world
+
+    def wait(self):
+        self.work.wait()
+        self.t.div_(self.world)
+        return True
+
+    def is_completed(self):
+        return self.work.is_completed()
+
+
 def allreduce_mean(t: torch.Tensor, group=None, async_op: bool = False):
-    """DDP gradient averaging of one bucket (RCCL AVG on GPU; SUM then scale on gloo)."""
+    """DDP gradient averaging of one bucket: RCCL AVG on GPU, gloo SUM then 1/world.  async_op:
+    returns a handle to wait on (for gloo the scaling happens in its wait()), None otherwise."""
     world = dist.get_world_size(group)
     if dist.get_backend(group) == "nccl":
         return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
     work = dist.all_reduce(t, group=group, async_op=async_op)
     if async_op:
-        work.wait()
+        return _MeanWork(work, t, world)
     t.div_(world)
     return None
 

@@ -348,9 +348,11 @@ class GraphedSteps:
 
 
 def _fusable(model) -> bool:
-    """Models whose whole step the fused engine computes (the centre-weighted and MSSIM
-    Autoencoder losses run through loss_function instead)."""
-    return getattr(model, "center_focus_sigma", None) is None and getattr(model, "mssim", None) is None
+    """Models whose whole step the fused engine computes: every model with fused_train_step — the
+    Autoencoder's centre-weighted MSE and MS-SSIM included (vae_recon_loss inside the step), except
+    an MS-SSIM configured outside the kernel's range (size_average=False, windows > 15)."""
+    m = getattr(model, "mssim", None)
+    return m is None or (m.size_average and m.window_size <= 15)
 
 
 def _owns_flat(opt, model) -> bool:

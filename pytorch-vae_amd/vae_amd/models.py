@@ -175,6 +175,35 @@ class _HipELBO(torch.autograd.Function):
         return plan.grads.clone(), None, None, None, None, None
 
 
+class _HipReconLoss(torch.autograd.Function):
+    """The Autoencoder's centre-weighted MSE / MS-SSIM on the GPU (vaehip.h vae_recon_loss): forward
+    evaluates the loss and dL/drecons in one call; backward scales that seed by dL/dloss.  `cfg` is a
+    StepPlan recon_loss dict."""
+
+    @staticmethod
+    def forward(ctx, recons: Tensor, target: Tensor, cfg: dict):
+        n, c, h, w = recons.shape
+        recons, target = recons.detach().float().contiguous(), target.detach().float().contiguous()
+        if cfg["kind"] == "center":
+            mask = cfg["mask"].to(recons.device, torch.float32).contiguous()
+            a = L.recon_loss_args(L.RLOSS_CENTER, n, c, h, w, mask=mask)
+        else:
+            a = L.recon_loss_args(L.RLOSS_MSSIM, n, c, h, w, window=cfg["window"])
+        grad = torch.empty_like(recons)
+        out = torch.zeros(3, dtype=torch.float32, device=recons.device)
+        ws = torch.empty(max(1, L.recon_loss_workspace(a) // 4), dtype=torch.float32, device=recons.device)
+        a.recon, a.target, a.grad, a.out = recons.data_ptr(), target.data_ptr(), grad.data_ptr(), out.data_ptr()
+        a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel() * 4
+        L.call("vae_recon_loss", a, L.stream_ptr())
+        ctx.save_for_backward(grad)
+        return out[0].clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g, None, None
+
+
 class _HipVAE(BaseVAE):
     """Shared machinery of the VanillaVAE-family models on libvaehip."""
 
@@ -438,7 +467,9 @@ class MSSIM(nn.Module):
         self.in_channels, self.window_size = in_channels, window_size
         self.normalize, self.size_average = normalize, size_average
         k = torch.tensor([math.exp((i - window_size // 2) ** 2 / (2 * 1.5 ** 2)) for i in range(window_size)])
-        k = (k / k.sum()).unsqueeze(1)
+        k = k / k.sum()
+        self.window_1d = k.tolist()             # the separable factor the HIP kernel takes (vae_recon_loss)
+        k = k.unsqueeze(1)
         self._window = k.mm(k.t()).float().unsqueeze(0).unsqueeze(0).expand(
             in_channels, 1, window_size, window_size).contiguous()
 
@@ -556,14 +587,26 @@ class Autoencoder(_HipVAE):
         with torch.no_grad():
             self.net.load_reference_state_dict(full)
 
+    def _recon_loss_cfg(self, device) -> Optional[dict]:
+        """StepPlan / vae_recon_loss configuration of this model's reconstruction loss (None: MSE)."""
+        if self.center_focus_sigma is not None:
+            if self.center_weight_mask is None:
+                self.center_weight_mask = self.create_center_weight_mask(self.net.img_size, self.net.img_size, device)
+            return {"kind": "center", "mask": self.center_weight_mask.view(self.net.img_size, self.net.img_size)}
+        if self.mssim is not None:
+            if not (self.mssim.size_average and self.mssim.window_size <= 15):
+                return None
+            return {"kind": "mssim", "window": self.mssim.window_1d, "normalize": self.mssim.normalize}
+        return None
+
     def _loss_config(self) -> dict:
-        return dict(loss="vanilla", samples=1)
+        return dict(loss="vanilla", samples=1, recon_loss=self._recon_loss_cfg(self.net.device))
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
                          betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
-        if self.center_focus_sigma is not None or self.mssim is not None:
-            raise NotImplementedError("the fused step computes the plain MSE; the centre-weighted and MSSIM "
-                                      "losses run through loss_function (torch loss, HIP backward)")
+        """The whole Autoencoder step in one graph, whichever reconstruction loss the model has: the
+        plain MSE on the ELBO kernel (M_N = 0), or the centre-weighted MSE / MS-SSIM on vae_recon_loss
+        (loss terms, per-image MSE and the dL/drecon seed of the fused backward)."""
         step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group, opt)
         step.plan.eps.zero_()
         step.zero_eps = True
@@ -594,7 +637,11 @@ class Autoencoder(_HipVAE):
                 and torch.is_grad_enabled() and recons is last[2] and input is last[1]):
             g = _HipELBO.apply(self.flat, last[2], last[3], last[4], last[0], dict(loss="vanilla", kld_weight=0.0))
             return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': zero, 'feature_loss': zero}
-        if self.center_focus_sigma is not None:
+        cfg = (self._recon_loss_cfg(recons.device) if recons.is_cuda and recons.dim() == 4
+               and recons.shape[2] * recons.shape[3] <= 4096 and recons.shape[2:] == input.shape[2:] else None)
+        if cfg is not None and (cfg["kind"] != "center" or tuple(cfg["mask"].shape) == tuple(recons.shape[2:])):
+            recons_loss = _HipReconLoss.apply(recons, input, cfg)  # vae_recon_loss (HIP forward + seed)
+        elif self.center_focus_sigma is not None:
             if self.center_weight_mask is None:
                 self.center_weight_mask = self.create_center_weight_mask(input.shape[2], input.shape[3], input.device)
             recons_loss = self.weighted_mse_loss(recons, input, self.center_weight_mask)

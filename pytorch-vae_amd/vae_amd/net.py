@@ -131,8 +131,14 @@ class StepPlan:
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
                  capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
                  concurrent: bool = False, fuse_bn: bool = False, bn_in_consumer: bool = True,
-                 wg_overlap: bool = False):
+                 wg_overlap: bool = False, recon_loss: Optional[dict] = None):
         self.net = net
+        # recon_loss (the Autoencoder's other reconstruction losses, vaehip.h vae_recon_loss):
+        # {"kind": "center", "mask": [H][W] device tensor} or {"kind": "mssim", "window": 1-D window}.
+        # The loss runs inside the step in place of the ELBO and seeds the backward with its
+        # dL/drecon (grad_recon), as the drop-in path does with autograd's.
+        self.recon_loss = recon_loss if training else None
+        self.seed_recon = (not fused_loss) or self.recon_loss is not None
         self.B = batch
         # training=False: eval-mode BatchNorm (running statistics, nothing updated; the
         # reference's validation_step / sample / generate under model.eval()) — forward only
@@ -205,7 +211,7 @@ class StepPlan:
             self.w8h = torch.zeros(8 * 9 * r[-1], dtype=T, device=dev)
             self.b8h = torch.zeros(8, dtype=torch.float32, device=dev)   # bias padded alike (lanes 3..7 stay 0)
         self.recon = torch.empty(BS, 3, img, img, **f32)
-        self.grad_recon = None if fused_loss else torch.zeros(BS, 3, img, img, **f32)
+        self.grad_recon = torch.zeros(BS, 3, img, img, **f32) if self.seed_recon else None
         self.out = torch.zeros(4, **f32)                                  # loss, recon, KLD(report), kld
         self.per_img = torch.zeros(BS, **f32)
         self.head_coef = torch.zeros(BS, **f32)
@@ -539,7 +545,9 @@ class StepPlan:
         e.kl_coef = self.kl_coef.data_ptr()
         self.n_decode1 = len(F)
         self.elbo_args = e
-        if self.fused_loss:
+        if self.recon_loss is not None:
+            self._add_recon_loss(F)
+        elif self.fused_loss:
             self._add(F, "vae_elbo_fwd", e)
 
         # ================================================================ backward
@@ -553,10 +561,10 @@ class StepPlan:
         hb.bias = net.p("final_layer.3.bias")
         hb.target = self.x.data_ptr()
         hb.recon = self.recon.data_ptr()
-        if self.fused_loss:
-            hb.coef = self.head_coef.data_ptr()
-        else:
+        if self.seed_recon:
             hb.grad_recon = self.grad_recon.data_ptr()
+        else:
+            hb.coef = self.head_coef.data_ptr()
         hb.dx = self.g_fin.data_ptr()
         hb.dx_epi = self.bn_xf("final_layer.1", L.X_BN_ACT, cnt(self.fin))
         hb.dx_epi.aux = self.fin.data_ptr()
@@ -689,6 +697,26 @@ class StepPlan:
                 self.bwd_sums(a, enc_pre[i - 1])
                 self._add(Bw, "vae_conv2d_bwd_data", a)
 
+    def _add_recon_loss(self, F):
+        """The recon_loss call closing the forward (vae_recon_loss): loss terms into `out`, per-image
+        MSE from the head's SSE, and dL/drecon into grad_recon for the backward."""
+        img, BS = self.net.img_size, self.B * self.S
+        cfg = self.recon_loss
+        if cfg["kind"] == "center":
+            self._rl_mask = cfg["mask"].to(self.net.device, torch.float32).contiguous().view(img, img)
+            a = L.recon_loss_args(L.RLOSS_CENTER, BS, 3, img, img, mask=self._rl_mask)
+        elif cfg["kind"] == "mssim":
+            a = L.recon_loss_args(L.RLOSS_MSSIM, BS, 3, img, img, window=cfg["window"],
+                                  levels=cfg.get("levels", 5), normalize=cfg.get("normalize", True))
+        else:
+            raise ValueError(f"recon_loss kind {cfg['kind']!r}")
+        a.recon, a.target, a.grad, a.out = (self.recon.data_ptr(), self.x.data_ptr(), self.grad_recon.data_ptr(),
+                                            self.out.data_ptr())
+        a.sse, a.per_img = self.sse.data_ptr(), self.per_img.data_ptr()
+        self._rl_ws = torch.zeros(max(1, L.recon_loss_workspace(a) // 4), dtype=torch.float32, device=self.net.device)
+        a.workspace, a.workspace_bytes = self._rl_ws.data_ptr(), self._rl_ws.numel() * 4
+        self._add(F, "vae_recon_loss", a)
+
     def _wide_head_fwd(self, F, cnt):
         """Head of a final layer wider than 32 channels: Conv2d(C -> 3 padded to 8, k3 s1 p1) on the
         conv-GEMM path with BatchNorm+LeakyReLU applied to its input on load, then vae_recon_fwd:
@@ -705,7 +733,7 @@ class StepPlan:
         self._add(F, "vae_conv2d_fwd", a)
         rc = L.ReconArgs(dtype=T, n=BS, h=img, w=img, c=3, ld=8)
         rc.y, rc.target, rc.recon, rc.sse = self.y8.data_ptr(), self.x.data_ptr(), self.recon.data_ptr(), self.sse.data_ptr()
-        if self.fused_loss and self.training:
+        if self.fused_loss and self.training and self.recon_loss is None:
             rc.dy, rc.grad_scale = self.g8.data_ptr(), 1.0 / (self.B * 3 * img * img)
         self._add(F, "vae_recon_fwd", rc)
 
@@ -715,7 +743,7 @@ class StepPlan:
         head, and the padded gradients' first 3 rows added into the parameter gradients."""
         net, T, img, BS = self.net, self.net.dcode, self.net.img_size, self.B * self.S
         C = self.fin.shape[-1]
-        if not self.fused_loss:
+        if self.seed_recon:
             rb = L.ReconArgs(dtype=T, n=BS, h=img, w=img, c=3, ld=8)
             rb.target, rb.recon = self.x.data_ptr(), self.recon.data_ptr()
             rb.dy, rb.grad_recon = self.g8.data_ptr(), self.grad_recon.data_ptr()

@@ -135,7 +135,7 @@ class VQStepPlan:
 
     loss_kind = L.LOSS_VQ
 
-    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True, concurrent: bool = True):
+    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True, concurrent: bool = False):
         self.net, self.B, self.beta, self.fused_loss = net, batch, beta, fused_loss
         dev, T = net.device, net.dtype
         h, E, img = net.hidden_dims, net.embedding_dim, net.img_size
@@ -194,18 +194,13 @@ class VQStepPlan:
         self.g_q = torch.empty_like(self.q)
         self.g_lat = torch.empty_like(self.latpre)
         self.g_enc = [torch.empty_like(t) for t in self.enc]
-        npad = (h[0] * 16 * 8 + r_[-1] * 16 * 8 + 8) if self.pad_rgb else 0
-        nz = _pad4(net.layout.total) + 4 + _pad4(B) + 4 + npad
+        nz = _pad4(net.layout.total) + 4 + _pad4(B) + 4
         self.zero = torch.zeros(nz, **f32)
         o = 0
         self.grads = self.zero[o:o + net.layout.total]; o += _pad4(net.layout.total)
         self.metrics = self.zero[o:o + 4]; o += 4                  # rank-averaged loss terms (engine.py)
         self.sse = self.zero[o:o + B]; o += _pad4(B)
         self.vq_sse = self.zero[o:o + 1]; o += 4
-        if self.pad_rgb:                                            # padded weight gradients
-            self.dw8e = self.zero[o:o + h[0] * 16 * 8]; o += h[0] * 16 * 8
-            self.dw8d = self.zero[o:o + r_[-1] * 16 * 8]; o += r_[-1] * 16 * 8
-            self.db8d = self.zero[o:o + 8]; o += 8
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
@@ -377,14 +372,21 @@ class VQStepPlan:
             if last and self.pad_rgb:
                 a.wt, a.bias = self.w8d.data_ptr(), self.b8d.data_ptr()
             a.y = dst.data_ptr()
-            self._add(F, "vae_convT2d_fwd", a)
+            if not (last and self.pad_rgb):
+                self._add(F, "vae_convT2d_fwd", a)
             src = dst
         # ---------------------------------------------------------------- Tanh + SSE + loss
         rc = L.ReconArgs(dtype=net.dcode, n=B, h=img, w=img, c=3, ld=self.cy)
         rc.y, rc.target, rc.recon, rc.sse = self.y.data_ptr(), self.x.data_ptr(), self.recon.data_ptr(), self.sse.data_ptr()
         if self.fused_loss:
             rc.dy, rc.grad_scale = self.g_y.data_ptr(), 1.0 / (B * 3 * img * img)
-        self._add(F, "vae_recon_fwd", rc)
+        if self.pad_rgb:
+            # the output ConvT(128 -> 3) and Tanh + reconstruction + SSE + seed as one call
+            # (vaehip.h vae_convT2d_fwd_recon: an input-centric kernel, no pre-tanh tensor in HBM)
+            self._keep += [a, rc]
+            F.append(("vae_convT2d_fwd_recon", (ctypes.byref(a), ctypes.byref(rc))))
+        else:
+            self._add(F, "vae_recon_fwd", rc)
         self.n_decode1 = len(F)
         e = L.ElboArgs(kind=L.LOSS_VQ, batch=B, samples=1, latent=1, img_elems=3 * img * img,
                        vq_beta=self.beta, vq_elems=float(B * self.s * self.s * E))
@@ -411,17 +413,19 @@ class VQStepPlan:
             a = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
             a.dy, a.wt = gouts[i].data_ptr(), (self.w8d.data_ptr() if padded else net.w(name + ".weight"))
             a.dx, a.dx_epi = gups[i].data_ptr(), _act(SLOPE, xin)
+            if padded:
+                # the output ConvT's data, weight and bias gradients in one call (vae_convT2d_bwd: one
+                # pass over dy and x on the RGB-end kernel), dW / db straight into the parameters'
+                # own [128][4][4][3] / [3] (dw_inner = 3: no padded gradient, no unpad launches)
+                a.x, a.x_xf = xin.data_ptr(), _act()
+                a.dw, a.db, a.dw_inner = self.g(name + ".weight"), self.g(name + ".bias"), 3
+                self._add(Bw, "vae_convT2d_bwd", a)
+                continue
             self._add(Bw, "vae_convT2d_bwd_data", a)
             f = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
             f.x, f.x_xf = xin.data_ptr(), _act()
-            if padded:
-                f.dy, f.dw, f.db = gouts[i].data_ptr(), self.dw8d.data_ptr(), self.db8d.data_ptr()
-            else:
-                f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
+            f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
             self._add(Bw, "vae_convT2d_bwd_filter", f)
-            if padded:
-                Bw.append(("vae_unpad_accumulate", (r[-1] * 16, 8, 3, self.dw8d.data_ptr(), self.g(name + ".weight"))))
-                Bw.append(("vae_unpad_accumulate", (1, 8, 3, self.db8d.data_ptr(), self.g(name + ".bias"))))
         g_din = self._res_stack_bwd("decoder", 1, self.d_in, self.d_t, self.d_h)
         a = self._conv(self.q, E, C, 3, 1, 1)
         a.dy, a.wt, a.dx = g_din.data_ptr(), net.w("decoder.0.0.weight"), self.g_q.data_ptr()
@@ -463,10 +467,8 @@ class VQStepPlan:
                 f.x, f.x_xf = self.enc[i - 1].data_ptr(), _act()
             f.dy, f.dw, f.db = self.g_enc[i].data_ptr(), self.g(f"encoder.{i}.0.weight"), self.g(f"encoder.{i}.0.bias")
             if i == 0 and self.pad_rgb:
-                f.dw = self.dw8e.data_ptr()
+                f.dw_inner = 3          # dW straight into [128][4][4][3] from the 8-channel image
             self._add(Bw, "vae_conv2d_bwd_filter", f)
-            if i == 0 and self.pad_rgb:
-                Bw.append(("vae_unpad_accumulate", (h[0] * 16, 8, 3, self.dw8e.data_ptr(), self.g("encoder.0.0.weight"))))
             if i > 0:
                 a = mk()
                 a.dy, a.wt = self.g_enc[i].data_ptr(), net.w(f"encoder.{i}.0.weight")

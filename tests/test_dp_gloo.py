@@ -69,7 +69,19 @@ def _worker(rank, world, port, q):
         comm = BucketedAllReduce(mine, buckets)
         for k in range(len(buckets)):
             comm.launch(k)
+            # the launch returns at once with a handle (the step queues its next backward segment
+            # here): a bucket is never scaled before its wait — never already the mean
+            assert len(comm.works) == k + 1
         comm.wait()
+        # allreduce_mean on gloo: an in-flight handle, mean only after wait()
+        from vae_amd.dp import allreduce_mean
+        t = torch.full((1 << 16,), float(rank + 1))
+        h = allreduce_mean(t, async_op=True)
+        assert h is not None
+        before = float(t[0])
+        assert before in (float(rank + 1), float(sum(range(1, world + 1))))   # not yet scaled
+        h.wait()
+        assert torch.equal(t, torch.full_like(t, sum(range(1, world + 1)) / world))
         broadcast_buffers(run)
         err = float((mine - want).abs().max() / want.abs().max())
         assert err < 1e-6, err
