@@ -289,7 +289,7 @@ long rl_workspace_floats(const vae_recon_loss_args* a) {
   return a->kind == VAE_RLOSS_MSSIM ? planes * 2 * a->levels + 2 * a->levels : planes;
 }
 
-int rl_check(const vae_recon_loss_args* a) {
+int rl_check(const vae_recon_loss_args* a, bool tensors = true) {
   if (!a) return fail(VAE_E_BADARG, "recon_loss: null args");
   if (a->n <= 0 || a->c <= 0 || a->h <= 0 || a->w <= 0) return fail(VAE_E_BADSHAPE, "recon_loss: bad shape");
   if (a->kind != VAE_RLOSS_CENTER && a->kind != VAE_RLOSS_MSSIM) return fail(VAE_E_BADARG, "recon_loss: kind %d", a->kind);
@@ -301,11 +301,11 @@ int rl_check(const vae_recon_loss_args* a) {
       return fail(VAE_E_BADARG, "recon_loss: window %d (odd, <= %d)", a->window_size, RL_MAXWIN);
     if (!a->size_average) return fail(VAE_E_UNSUPPORTED, "recon_loss: size_average=False (the reference's MS-SSIM "
                                                         "combines per-level scalars)");
-  } else if (!a->mask) {
+  } else if (tensors && !a->mask) {
     return fail(VAE_E_BADARG, "recon_loss: centre-weighted MSE needs the mask");
   }
   if ((long)a->h * a->w > RL_MAXHW) return fail(VAE_E_UNSUPPORTED, "recon_loss: plane %dx%d > 64x64", a->h, a->w);
-  if (!a->recon || !a->target || !a->out) return fail(VAE_E_BADARG, "recon_loss: recon / target / out");
+  if (tensors && (!a->recon || !a->target || !a->out)) return fail(VAE_E_BADARG, "recon_loss: recon / target / out");
   return VAE_OK;
 }
 
@@ -315,7 +315,7 @@ int rl_check(const vae_recon_loss_args* a) {
 using namespace vae;
 
 extern "C" int vae_recon_loss_workspace_size(const vae_recon_loss_args* a, size_t* bytes) {
-  if (int rc = rl_check(a)) return rc;
+  if (int rc = rl_check(a, false)) return rc;              // (sizes only: tensors may be unset)
   if (!bytes) return fail(VAE_E_BADARG, "recon_loss_workspace_size: bytes");
   *bytes = (size_t)rl_workspace_floats(a) * 4;
   return VAE_OK;
