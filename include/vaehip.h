@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 18
+#define VAE_ABI_VERSION 19
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -520,6 +520,25 @@ int vae_latent_fc_fwd(const vae_latent_args* a, void* stream);
 int vae_latent_dec_fwd(const vae_latent_args* a, void* stream);
 int vae_latent_dec_bwd(const vae_latent_args* a, void* stream);
 int vae_latent_fc_bwd(const vae_latent_args* a, void* stream);
+
+/* --- Materialised per-channel transform (the operand of the large transform-free GEMMs) ---------
+ * out[r][c] = xf(x[r][c]) in bf16, same [rows][channels] layout: lrelu(BN(y)) of a forward
+ * activation (xf BN_ACT; running statistics updated when set — this call is then the BatchNorm's
+ * first consumer), lrelu(y) (ACT), or the BatchNorm-backward gradient A g + B y + C of the stored
+ * gradient g (xf BN_DY, aux = y; dgamma_out / dbeta_out and the closed-form conv-bias gradient db
+ * published when set, as a weight-gradient call applying BN_DY itself would).  The Autoencoder's
+ * wide layers (models/autoencoder.py:16-86) and the VQ-VAE's strided 4x4 layers take it so their
+ * GEMMs run on the LDS-DMA pipeline (vae_bgemm.hip) with plain operands. */
+typedef struct vae_bn_apply_args {
+  int32_t dtype;             /* VAE_BF16 */
+  int64_t rows;
+  int32_t channels;          /* % 8 */
+  const void* x;
+  vae_xform xf;
+  float* db;
+  void* out;
+} vae_bn_apply_args;
+int vae_bn_apply(const vae_bn_apply_args* a, void* stream);
 
 /* --- The Autoencoder's other reconstruction losses (forward + backward seed) ----------------------
  * VAE_RLOSS_CENTER: mean(mask * (recon - target)^2) over n*c*h*w (models/autoencoder.py:95-146,

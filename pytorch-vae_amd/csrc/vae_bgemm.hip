@@ -1,0 +1,344 @@
+// The large bf16 implicit-GEMM convolutions (Conv2d / ConvTranspose2d forward and data gradient)
+// on an LDS-DMA pipeline: the Autoencoder's wide layers (configs/big_ae.yaml ..
+// patient_vvbig_ae.yaml: 9.7 GFLOP per layer and pass at B = 64, models/autoencoder.py:16-86) and
+// the VQ-VAE's strided 4x4 layers (models/vq_vae.py:98-105, :140-154), whose arithmetic intensity
+// is above the MFMA ridge.
+//
+// Why a fourth GEMM kernel: the conv-GEMM (vae_cgemm.hpp) stages operands through registers so it
+// can apply the BatchNorm / LeakyReLU transform on the way into LDS; at 128 x 128 tiles its
+// register budget leaves two K-steps in flight, against a ~1-2 us load latency and ~0.2 us of MFMA
+// work per K-step — it ran these layers at 3-10 % of the bf16 peak (profiles/r3_v4_*).  Here the
+// operands come transform-free (the caller materialises lrelu(BN(y)) / the BatchNorm-backward
+// gradient once per layer, vae_bn_apply) and go global -> LDS by buffer_load ... lds (no VGPR
+// staging, no VALU work between load and MFMA):
+//   * 128 x 128 x 64 tiles, 4 waves (2 x 2, 64 x 64 each: 4 x 4 v_mfma_f32_16x16x32_bf16 frags),
+//     two LDS buffers of 32 KB: K-step k+1 is in flight while k computes (counted vmcnt + raw
+//     s_barrier: an LDS-DMA counts on vmcnt, and __syncthreads' fence would drain it);
+//   * the LDS image is lane-linear (LDS-DMA writes base + lane * 16): row r of a tile holds its
+//     eight 16-byte k-chunks at slot c ^ ((r >> 1) & 7), set through the per-lane SOURCE address,
+//     which makes the ds_read_b128 fragment reads of 16 rows x one chunk conflict-free;
+//   * one K-step = 64 channels of one tap (host: C % 64 == 0), so a lane's gather address is its
+//     row base + one per-step tap offset (out-of-image taps read zeros through the buffer
+//     resource's range check);
+//   * XCD-aware tile order (n fastest within an XCD's contiguous tile range), split-K through fp32
+//     slabs + the shared finalize (vae_launch.hpp launch_finalize) when the tiles do not cover the
+//     CUs; the epilogue stages the fp32 tile through LDS in two 64-row halves and applies the bias
+//     + BatchNorm statistics (E_STORE) or the activation backward + BatchNorm-backward sums
+//     (E_BNBWD) of the cgemm contract, 16-byte stores.
+#include "vae_launch.hpp"
+#include "vae_bgemm.hpp"
+
+namespace vae {
+namespace {
+
+constexpr int BG_M = 128, BG_N = 128, BG_K = 64, BG_T = 256;
+constexpr int BG_TILE = BG_M * BG_K * 2;              // bytes of one operand tile (16 KB)
+constexpr int BG_STAGE = 2 * BG_TILE;                 // A + B
+constexpr int BG_OPS = 2 * BG_STAGE;                  // two stages (64 KB)
+constexpr int BG_LDC = BG_N + 4;                      // fp32 epilogue rows (one 64-row half at a time)
+static_assert(64 * BG_LDC * 4 <= BG_OPS, "epilogue half-tile fits the operand buffers");
+
+// One 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... lds: lane l's 16 bytes land at M0 + 16 l).
+// (The compiler's wait-count pass leaves the K-step in flight across the loop's ds_reads here —
+// one LDS array, explicit vmcnt(N) waits; checked in the ISA.)
+typedef __attribute__((address_space(3))) void lds_void;
+__device__ __forceinline__ void glds16(rsrc_t r, const char* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(uintptr_t)(uint32_t)(uintptr_t)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ int bg_slot(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <int AM, int EM>
+__global__ void __launch_bounds__(BG_T, 2) bgemm_kernel(const GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object (see header)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // ---- tile: XCD-aware order (1-D grid), as vae_cgemm.hpp
+  const int gm = (p.M + BG_M - 1) / BG_M, gn = p.N / BG_N, gz = p.nphase * p.ksplit;
+  int tile;
+  {
+    const int nb = gm * gn * gz, b = blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
+  }
+  const int tn = tile % gn, tz = (tile / gn) % gz, tmi = tile / (gn * gz);
+  const int m0 = tmi * BG_M, n0 = tn * BG_N;
+  const int phase = (p.nphase > 1) ? (int)(tz / p.ksplit) : 0;
+  const int ks = tz - phase * p.ksplit;
+  const PhaseInfo pq = make_phase(p, phase);
+  const int Kp = AM == A_CONVT ? pq.nth * pq.ntw * p.gc : p.K;
+  const int ktiles = Kp / BG_K;                       // host: Kp % 64 == 0
+  const int kper = (ktiles + p.ksplit - 1) / p.ksplit;
+  const int kt0 = ks * kper, kt1 = min(ktiles, kt0 + kper);
+
+  // ---- this lane's 4 A rows and 4 B rows (wave-instruction j: tile rows 8 (4 wave + j) .. + 7)
+  const rsrc_t ra = make_rsrc(p.a_ptr, p.a_bytes), rb = make_rsrc(p.b_ptr, p.b_bytes);
+  RowOperand<__bf16, AM, true> ar[4];
+  int bbase[4], slot_c[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * wave + j) + (lane >> 3);
+    slot_c[j] = bg_slot(row, lane & 7);               // the logical chunk this lane's slot holds
+    ar[j].init(p, m0 + row, p.M, phase, p.a_ld);
+    bbase[j] = (n0 + row) * p.b_ld;
+  }
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BG_K;
+    const KTap t = RowOperand<__bf16, AM, true>::tap(p, pq, p.fd_ach, p.a_xf.channels, false, k0, Kp);
+    int boff = k0;
+    if constexpr (AM == A_CONVT) {
+      const int rr = pq.t0h - p.gs * t.r, ss = pq.t0w - p.gs * t.s;
+      boff = (rr * p.gr + ss) * p.gc + t.ch;
+    }
+    char* la = smem + buf * BG_STAGE + wave * 4 * 1024;
+    char* lb = la + BG_TILE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = ar[j].valid && (uint32_t)(ar[j].hi0 + t.r) < (uint32_t)p.gh &&
+                      (uint32_t)(ar[j].wi0 + t.s) < (uint32_t)p.gw;
+      const uint32_t offa = ok ? (uint32_t)(ar[j].base + t.toff + 8 * slot_c[j]) * 2u : kOOB;
+      glds16(ra, la + j * 1024, offa);
+      glds16(rb, lb + j * 1024, (uint32_t)(bbase[j] + boff + 8 * slot_c[j]) * 2u);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes within a tile): row, chunk (ks2 * 4 + lane >> 4) at its slot
+  int aoff[4][2], boffs[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const int ra_ = wm * 64 + i * 16 + (lane & 15), rb_ = wn * 64 + i * 16 + (lane & 15);
+      const int c = k2 * 4 + (lane >> 4);
+      aoff[i][k2] = ra_ * 128 + bg_slot(ra_, c) * 16;
+      boffs[i][k2] = rb_ * 128 + bg_slot(rb_, c) * 16;
+    }
+
+  if (kt0 < kt1) issue(kt0, 0);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    if (kt + 1 < kt1) {
+      issue(kt + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // this wave's loads of step kt landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();                           // ... and every wave's
+    const char* la = smem + buf * BG_STAGE;
+    const char* lb = la + BG_TILE;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(la + aoff[i][k2]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(lb + boffs[j][k2]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                           // every wave is done reading `buf`
+  }
+
+  // ================================================================ epilogue (two 64-row halves)
+  float* Cs = reinterpret_cast<float*>(smem);              // [64][BG_LDC]
+  // per-channel tables of the epilogue transform (E_BNBWD with a BatchNorm+LeakyReLU), after the
+  // operand area; scratch for their in-kernel build on the operand area (free by now)
+  float* tq = reinterpret_cast<float*>(smem + BG_OPS);
+  const int ce = tab_stride(p.epi_xf.channels);
+  const Tab te{tq, tq + ce, nullptr, tq + 2 * ce, tq + 3 * ce};
+  if constexpr (EM == E_BNBWD) {
+    if (!p.slab && p.epi_xf.kind == VAE_X_BN_ACT) tab_fill(p.epi_xf, te, true, false, Cs);
+  }
+  __syncthreads();
+  if (p.slab) {
+    // split-K partial -> slab [phase][ks][M][N] (plain fp32, the finalize adds the slices)
+    float* sl = p.slab + ((long)(phase * p.ksplit + ks) * p.M) * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + e, col = n0 + wn * 64 + j * 16 + (lane & 15);
+          if (row < p.M) sl[(long)row * p.N + col] = acc[i][j][e];
+        }
+    return;
+  }
+  // thread -> 8 consecutive columns (ec) of rows er, er + 16, er + 32, er + 48 of a half
+  const int ec = tid & 15, er = tid >> 4;
+  const int col = n0 + ec * 8;
+  float bias[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bias[e] = (EM == E_STORE && p.bias) ? p.bias[col + e] : 0.f;
+  const rsrc_t raux = epi_aux_rsrc<EM>(p);
+  int ech = 0;
+  if constexpr (EM == E_BNBWD) ech = (int)(col - p.fd_ech.div(col) * p.epi_xf.channels);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  __bf16* out = static_cast<__bf16*>(p.out);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (wm == h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Cs[(i * 16 + 4 * (lane >> 4) + e) * BG_LDC + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][e];
+    }
+    __syncthreads();
+    int obase[4];
+    uint32_t aux[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = m0 + h * 64 + er + 16 * u;
+      obase[u] = out_row_base(p, phase, row < p.M ? row : 0) + col;
+      const bool ld = EM == E_BNBWD && p.epi_xf.kind != VAE_X_NONE && row < p.M;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(raux, ld ? (uint32_t)obase[u] * 2u : kOOB, 0, 0);
+      aux[u][0] = v[0]; aux[u][1] = v[1]; aux[u][2] = v[2]; aux[u][3] = v[3];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rl = er + 16 * u, row = m0 + h * 64 + rl;
+      if (row >= p.M) continue;
+      const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + rl * BG_LDC + ec * 8);
+      const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + rl * BG_LDC + ec * 8 + 4);
+      const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (EM == E_STORE) {
+          s1[e] += v[e];
+          s2[e] = fmaf(v[e], v[e], s2[e]);
+          o[e] = v[e] + bias[e];
+        } else {
+          const float ax = __uint_as_float((e & 1) ? (aux[u][e >> 1] & 0xffff0000u) : (aux[u][e >> 1] << 16));
+          float g = v[e];
+          if (p.epi_xf.kind == VAE_X_BN_ACT) {
+            const float z = fmaf(ax, te.a[ech + e], te.b[ech + e]);
+            g = z > 0.f ? g : g * p.epi_xf.slope;
+            s1[e] += g;
+            s2[e] = fmaf(g, fmaf(ax, te.p[ech + e], te.q[ech + e]), s2[e]);
+          } else if (p.epi_xf.kind == VAE_X_ACT) {
+            g = ax > 0.f ? g : g * p.epi_xf.slope;
+          }
+          o[e] = g;
+        }
+      }
+      uint4 pk;
+      uint32_t* pp = reinterpret_cast<uint32_t*>(&pk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bf16x2 hh;
+        hh[0] = (__bf16)o[2 * e];
+        hh[1] = (__bf16)o[2 * e + 1];
+        pp[e] = *reinterpret_cast<uint32_t*>(&hh);
+      }
+      *reinterpret_cast<uint4*>(out + obase[u]) = pk;
+    }
+    __syncthreads();                                        // Cs is rewritten by the next half
+  }
+  if (!epi_wants_sums<EM>(p)) return;
+  // per-column sums: lanes l and l ^ 16, l ^ 32 hold the same columns (ec = tid & 15) -> butterfly,
+  // then one partial per wave and column in LDS, added in wave order
+#pragma unroll
+  for (int m = 16; m < 64; m <<= 1)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += __shfl_xor(s1[e], m);
+      s2[e] += __shfl_xor(s2[e], m);
+    }
+  float* part = Cs;                                         // [4 waves][2][BG_N]
+  if (lane < 16) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      part[(wave * 2) * BG_N + lane * 8 + e] = s1[e];
+      part[(wave * 2 + 1) * BG_N + lane * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  if (tid < BG_N) {
+    const float t1 = (part[0 * BG_N + tid] + part[2 * BG_N + tid]) + (part[4 * BG_N + tid] + part[6 * BG_N + tid]);
+    const float t2 = (part[1 * BG_N + tid] + part[3 * BG_N + tid]) + (part[5 * BG_N + tid] + part[7 * BG_N + tid]);
+    epi_flush_sums<EM>(p, (int)blockIdx.x, n0 + tid, t1, t2);
+  }
+}
+
+template <int AM, int EM>
+int bgemm_go(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
+  int kmax = p.K;
+  if (AM == A_CONVT) {
+    kmax = 0;
+    for (int ph = 0; ph < p.nphase; ++ph) {
+      const int k = p.ntap_h[ph / p.gs] * p.ntap_w[ph % p.gs] * p.gc;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  const int ktiles = kmax / BG_K;
+  const long tiles = (long)((p.M + BG_M - 1) / BG_M) * (p.N / BG_N) * p.nphase;
+  // split K until the tiles fill the CUs (two workgroups each), >= 4 K-steps per slice
+  int split = 1;
+  static const int wgpercu = tune_env("VAE_BG_WGPERCU", 2);
+  if (tiles < (long)wgpercu * kCUs) {
+    split = (int)(((long)wgpercu * kCUs) / tiles);
+    if (split > ktiles / 4) split = ktiles / 4;
+    if (split < 1) split = 1;
+  }
+  if (split > 1) {
+    if (!ws && !querying()) split = 1;
+    else if (!ws_fits((long)split * p.M * p.N * p.nphase * 4, ws_bytes, "bgemm split-K")) return VAE_E_BADARG;
+  }
+  p.ksplit = split;
+  p.slab = split > 1 ? static_cast<float*>(ws) : nullptr;
+  const size_t lds = (size_t)BG_OPS + (EM == E_BNBWD ? (size_t)tab_floats(p.epi_xf, true) * 4 : 0);
+  if (lds > (size_t)kLdsBytes) return kHeadFallback;
+  const unsigned nb = (unsigned)(tiles * split);
+  VAE_LAUNCH((bgemm_kernel<AM, EM>), dim3(nb), dim3(BG_T), lds, st, p);
+  if (int rc = check_launch("bgemm")) return rc;
+  if (p.slab) return launch_finalize<__bf16, EM>(p, st);
+  return VAE_OK;
+}
+
+}  // namespace
+
+// Eligible: transform-free bf16 operands (the caller materialised the activation), 64-channel
+// K-steps that stay inside one tap, 128-column tiles, no residual, work large enough to pay for a
+// 128 x 128 tile (>= 1 GFLOP), packed NHWC alignment.
+bool bgemm_ok(const GemmParams& p, int am, int em) {
+  static const bool off = getenv("VAE_NO_BGEMM") != nullptr;
+  if (off || (am != A_CONV && am != A_CONVT) || (em != E_STORE && em != E_BNBWD)) return false;
+  if (p.a_xf.kind != VAE_X_NONE || p.g_nchw || p.ones_col >= 0 || p.residual || p.out_f32) return false;
+  if (p.gc % BG_K || p.N % BG_N || p.out_ld % 8 || p.b_ld % 8) return false;
+  if (((uintptr_t)p.a_ptr | (uintptr_t)p.b_ptr | (uintptr_t)p.out) & 15) return false;
+  if (em == E_STORE && p.sum && (p.sum_reps < 1)) return false;
+  if (em == E_BNBWD && p.epi_xf.kind != VAE_X_NONE && (((uintptr_t)p.epi_xf.aux & 15) || p.epi_xf.channels % 8)) return false;
+  int kmax = p.K;
+  if (am == A_CONVT) {
+    kmax = 0;
+    for (int ph = 0; ph < p.nphase; ++ph) {
+      const int k = p.ntap_h[ph / p.gs] * p.ntap_w[ph % p.gs] * p.gc;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  const double flops = 2.0 * p.M * p.N * (double)kmax * p.nphase;      // (upper bound over phases)
+  static const double minf = tune_env("VAE_BG_MINGF", 0) > 0 ? tune_env("VAE_BG_MINGF", 0) * 1e9 : 4e9;
+  return flops >= minf;
+}
+
+int bgemm_launch(const GemmParams& p, int am, int em, void* ws, long ws_bytes, hipStream_t st) {
+  if (am == A_CONV) return em == E_STORE ? bgemm_go<A_CONV, E_STORE>(p, ws, ws_bytes, st) : bgemm_go<A_CONV, E_BNBWD>(p, ws, ws_bytes, st);
+  return em == E_STORE ? bgemm_go<A_CONVT, E_STORE>(p, ws, ws_bytes, st) : bgemm_go<A_CONVT, E_BNBWD>(p, ws, ws_bytes, st);
+}
+
+}  // namespace vae

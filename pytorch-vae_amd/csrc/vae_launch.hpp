@@ -3,6 +3,7 @@
 #pragma once
 #include "vae_fgemm.hpp"
 #include "vae_cgemm.hpp"
+#include "vae_bgemm.hpp"
 #include <stdlib.h>
 
 #ifdef VAE_PROBE
@@ -581,6 +582,11 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
 #ifdef VAE_PROBE
   p.probe = vae_probe_buffer();
 #endif
+  // transform-free large layers (an operand the caller materialised): the LDS-DMA pipeline
+  if (split_req <= 0 && bgemm_ok(p, AM, EM)) {
+    const int rc = bgemm_launch(p, AM, EM, ws, ws_bytes, st);
+    if (rc != kHeadFallback) return rc;
+  }
   const CgTile t = cg_pick(p.M, p.N, p.nphase, cg_table_bytes(p, EM));
   const int bk = t.bm >= 128 ? 64 : 128;
   int kmax = p.K;

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -99,6 +99,12 @@ class ReconArgs(ctypes.Structure):
     _fields_ = [("dtype", c_int32), ("n", c_int32), ("h", c_int32), ("w", c_int32), ("c", c_int32),
                 ("y", c_void_p), ("target", c_void_p), ("recon", c_void_p), ("sse", c_void_p), ("dy", c_void_p),
                 ("grad_scale", c_float), ("grad_recon", c_void_p), ("ld", c_int32)]
+
+
+class BnApplyArgs(ctypes.Structure):
+    """vaehip.h vae_bn_apply_args (a materialised lrelu(BN(y)) / BN-backward gradient)."""
+    _fields_ = [("dtype", c_int32), ("rows", c_int64), ("channels", c_int32), ("x", c_void_p), ("xf", Xform),
+                ("db", c_void_p), ("out", c_void_p)]
 
 
 class ReconLossArgs(ctypes.Structure):
@@ -199,6 +205,7 @@ _SIGS = {
     "vae_latent_dec_bwd": [POINTER(LatentArgs), c_void_p],
     "vae_latent_fc_bwd": [POINTER(LatentArgs), c_void_p],
     "vae_recon_loss": [POINTER(ReconLossArgs), c_void_p],
+    "vae_bn_apply": [POINTER(BnApplyArgs), c_void_p],
     "vae_recon_loss_workspace_size": [POINTER(ReconLossArgs), POINTER(ctypes.c_size_t)],
 }
 EXPORTED = tuple(_SIGS)

@@ -25,6 +25,7 @@ from . import _lib as L
 from .layout import Layout, default_init, reference_key_order, vanilla_layout
 
 SLOPE = 0.01         # nn.LeakyReLU default
+MAT_MIN_FLOPS = 4e9  # layers at least this large take materialised operands (StepPlan.big_layer)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 
@@ -264,6 +265,8 @@ class StepPlan:
         # edges cost more than the overlap gains, as the per-call side stream of round 1 did
         wg_overlap = wg_overlap or bool(os.environ.get("VAE_WG_OVERLAP"))        # (A/B timing)
         self.wg_overlap = wg_overlap and training and not concurrent and not os.environ.get("VAE_NO_WG_OVERLAP")
+        self._mat_a: Dict[str, torch.Tensor] = {}         # materialised lrelu(BN(y)) per BatchNorm
+        self._mat_dz: Dict[str, torch.Tensor] = {}        # materialised BN-backward gradients
         self.side_all = self.side is not None            # concurrent: every weight-gradient call
         if self.wg_overlap:
             self.side = torch.cuda.Stream(device=dev)
@@ -383,6 +386,42 @@ class StepPlan:
             a.db = self.g(self._bn_prod_bias(prefix))
         self._add(lst, "vae_bn_finalize", a)
 
+    # ---- materialised transforms for the large layers (vaehip.h vae_bn_apply + vae_bgemm.hip)
+    def big_layer(self, flops: float) -> bool:
+        """A layer whose GEMMs take materialised (transform-free) operands: bf16 training, >= 4 GFLOP
+        per pass (the Autoencoder's wide layers; the VanillaVAE's are 0.6).  VAE_NO_MAT=1 keeps every
+        transform fused into its consumers (A/B timing)."""
+        return (self.net.dtype == torch.bfloat16 and self.training and flops >= MAT_MIN_FLOPS
+                and not os.environ.get("VAE_NO_MAT"))
+
+    def mat_act(self, F, prefix: str, t: torch.Tensor, count: int):
+        """lrelu(BN(t)) written once (vae_bn_apply: running statistics updated there, the forward's
+        first consumer of the BatchNorm); returns the tensor every later consumer reads plainly."""
+        out = self._mat_a.get(prefix)
+        if out is None:
+            out = self._mat_a[prefix] = torch.empty_like(t)
+            a = L.BnApplyArgs(dtype=self.net.dcode, rows=t.numel() // t.shape[-1], channels=t.shape[-1])
+            a.x, a.out = t.data_ptr(), out.data_ptr()
+            a.xf = self.bn_xf(prefix, L.X_BN_ACT, count, running=True)
+            self._add(F, "vae_bn_apply", a)
+        return out
+
+    def mat_dz(self, Bw, prefix: str, g: torch.Tensor, y: torch.Tensor, count: int):
+        """The BatchNorm-backward gradient A g + B y + C of a big layer's output written once
+        (vae_bn_apply BN_DY, which also publishes dgamma, dbeta and the conv's closed-form bias
+        gradient unless vae_bn_finalize did); the layer's data and weight gradients read it plainly."""
+        out = self._mat_dz[prefix] = torch.empty_like(g)
+        a = L.BnApplyArgs(dtype=self.net.dcode, rows=g.numel() // g.shape[-1], channels=g.shape[-1])
+        a.x, a.out = g.data_ptr(), out.data_ptr()
+        xf = self.bn_xf(prefix, L.X_BN_DY, count, aux=y)
+        if self.bn_in_consumer and not self.wide_bn(prefix):
+            xf.dgamma_out = self.g(prefix + ".weight")
+            xf.dbeta_out = self.g(prefix + ".bias")
+            a.db = self.g(self._bn_prod_bias(prefix))
+        a.xf = xf
+        self._add(Bw, "vae_bn_apply", a)
+        return out
+
     def _fuse_finalize(self, calls):
         """Fold every vae_bn_finalize call (modes 0/1) into the call that produced its statistics
         (the GEMM whose epilogue wrote them): that call's last workgroup then builds the table
@@ -454,6 +493,8 @@ class StepPlan:
             elif i == 0:
                 a.x_nchw_f32 = 1
                 a.x = self.x.data_ptr()
+            elif self.big_layer(2.0 * B * (sp // 2) ** 2 * h[i] * 9 * h[i - 1]):
+                a.x = self.mat_act(F, enc_pre[i - 1], self.enc[i - 1], cnt(self.enc[i - 1])).data_ptr()
             else:
                 a.x = self.enc[i - 1].data_ptr()
                 a.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]), running=True)
@@ -507,7 +548,9 @@ class StepPlan:
             cout = r[i + 1] if i < len(r) - 1 else r[-1]
             a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
             a.x = prev.data_ptr()
-            if prev_pre is not None:
+            if prev_pre is not None and self.big_layer(2.0 * BS * sp * sp * cin * cout * 9):
+                a.x = self.mat_act(F, prev_pre, prev, cnt(prev)).data_ptr()
+            elif prev_pre is not None:
                 a.x_xf = self.bn_xf(prev_pre, L.X_BN_ACT, cnt(prev), running=True)
             a.wt = net.w(dec_w[i] + ".weight")
             a.wt_t = net.wt_t.get(dec_w[i] + ".weight")
@@ -587,8 +630,12 @@ class StepPlan:
             gx_t = self.g_h0 if i == 0 else g_dec_out[i - 1]
             self.bn_finalize(Bw, dec_pre[i], 1, cnt(dec_out[i]))
             dy_xf = self.bn_xf(dec_pre[i], L.X_BN_DY, cnt(dec_out[i]), aux=dec_out[i])
+            dz = (self.mat_dz(Bw, dec_pre[i], g_dec_out[i], dec_out[i], cnt(dec_out[i]))
+                  if self.big_layer(2.0 * BS * sp * sp * cin * cout * 9) else None)
+            if dz is not None:
+                dy_xf = L.Xform(kind=L.X_NONE, channels=cout)
             a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
-            a.dy = g_dec_out[i].data_ptr()
+            a.dy = (dz if dz is not None else g_dec_out[i]).data_ptr()
             a.dy_xf = dy_xf
             a.wt = net.w(dec_w[i] + ".weight")
             a.dx = gx_t.data_ptr()
@@ -598,12 +645,15 @@ class StepPlan:
             f = a if i == len(r) - 1 else L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp,
                                                       r=3, stride=2, pad=1)
             f.x = x_t.data_ptr()
-            if i > 0:
+            if i > 0 and dec_pre[i - 1] in self._mat_a:
+                f.x = self._mat_a[dec_pre[i - 1]].data_ptr()
+            elif i > 0:
                 f.x_xf = self.bn_xf(dec_pre[i - 1], L.X_BN_ACT, cnt(x_t))
-            f.dy = g_dec_out[i].data_ptr()
+            f.dy = (dz if dz is not None else g_dec_out[i]).data_ptr()
             f.dy_xf = dy_xf
             f.dw = self.g(dec_w[i] + ".weight")      # bias gradient: closed form (bn_finalize / bwd_extras)
-            self.bwd_extras(f, dec_pre[i])
+            if dz is None:
+                self.bwd_extras(f, dec_pre[i])
             if i == len(r) - 1:
                 # the full-resolution last ConvTranspose2d: both gradients in one pass over dy
                 # (vaehip.h vae_convT2d_bwd; other shapes run the two calls inside it)
@@ -669,8 +719,12 @@ class StepPlan:
             cin = 3 if i == 0 else h[i - 1]
             self.bn_finalize(Bw, enc_pre[i], 1, cnt(self.enc[i]))
             dy_xf = self.bn_xf(enc_pre[i], L.X_BN_DY, cnt(self.enc[i]), aux=self.enc[i])
+            dz = (self.mat_dz(Bw, enc_pre[i], self.g_enc[i], self.enc[i], cnt(self.enc[i]))
+                  if i > 0 and self.big_layer(2.0 * B * (sp // 2) ** 2 * h[i] * 9 * cin) else None)
+            if dz is not None:
+                dy_xf = L.Xform(kind=L.X_NONE, channels=h[i])
             f = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
-            f.dy = self.g_enc[i].data_ptr()
+            f.dy = (dz if dz is not None else self.g_enc[i]).data_ptr()
             f.dy_xf = dy_xf
             if i == 0 and self.pad_rgb:
                 # the 8-channel padded image; dW lands in the parameter's own [k][3][3][3] layout
@@ -679,16 +733,19 @@ class StepPlan:
             elif i == 0:
                 f.x_nchw_f32 = 1
                 f.x = self.x.data_ptr()
+            elif enc_pre[i - 1] in self._mat_a:
+                f.x = self._mat_a[enc_pre[i - 1]].data_ptr()
             else:
                 f.x = self.enc[i - 1].data_ptr()
                 f.x_xf = self.bn_xf(enc_pre[i - 1], L.X_BN_ACT, cnt(self.enc[i - 1]))
             if not (i == 0 and self.pad_rgb):
                 f.dw = self.g(f"encoder.{i}.0.weight")   # bias gradient: closed form (bn_finalize / bwd_extras)
-            self.bwd_extras(f, enc_pre[i])
+            if dz is None:
+                self.bwd_extras(f, enc_pre[i])
             self._add(Bw, "vae_conv2d_bwd_filter", f)
             if i > 0:
                 a = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
-                a.dy = self.g_enc[i].data_ptr()
+                a.dy = (dz if dz is not None else self.g_enc[i]).data_ptr()
                 a.dy_xf = dy_xf
                 a.wt = net.w(f"encoder.{i}.0.weight")
                 a.wt_t = net.wt_t.get(f"encoder.{i}.0.weight")

@@ -18,13 +18,14 @@ loss are their own small kernels.  All convolutions are MFMA implicit GEMMs (vae
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, List, Optional
 
 import torch
 
 from . import _lib as L
 from .layout import Layout, default_init, vq_layout, vq_param_spec
-from .net import SLOPE, _pad4, make_swaps, run_calls, size_workspaces
+from .net import MAT_MIN_FLOPS, SLOPE, _pad4, make_swaps, run_calls, size_workspaces
 
 NRES = 6             # ResidualLayers per stack (vq_vae.py:111, :138)
 
@@ -204,6 +205,7 @@ class VQStepPlan:
         self.step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.fwd_calls: List = []
         self.bwd_calls: List = []
+        self._mat: Dict[int, torch.Tensor] = {}     # materialised lrelu(t) of large layers' inputs (by t)
         self.side = torch.cuda.Stream(device=dev) if concurrent else None     # weight gradients (run_calls)
         self._build()
         self._attach_swaps()
@@ -295,6 +297,22 @@ class VQStepPlan:
             self._add(Bw, "vae_conv2d_bwd_filter", f)
         return gh[0]
 
+    def _mat_lrelu(self, F, t: torch.Tensor) -> torch.Tensor:
+        """lrelu(t) written once (vaehip.h vae_bn_apply, ACT) for a large strided layer, so its GEMM
+        runs transform-free on the LDS-DMA pipeline (vae_bgemm.hip); its weight gradient reads the
+        same tensor.  bf16 only (the fp32 parity mode keeps the fused transform)."""
+        key = t.data_ptr()
+        out = self._mat.get(key)
+        if out is None:
+            out = self._mat[key] = torch.empty_like(t)
+            a = L.BnApplyArgs(dtype=self.net.dcode, rows=t.numel() // t.shape[-1], channels=t.shape[-1])
+            a.x, a.out, a.xf = t.data_ptr(), out.data_ptr(), _act()
+            self._add(F, "vae_bn_apply", a)
+        return out
+
+    def _mat_ok(self, flops: float) -> bool:
+        return self.net.dtype == torch.bfloat16 and flops >= MAT_MIN_FLOPS and not os.environ.get("VAE_NO_MAT")
+
     # ------------------------------------------------------------------ plan
     def _build(self):
         net = self.net
@@ -324,6 +342,8 @@ class VQStepPlan:
                     a.c, a.x = 8, self.x8.data_ptr()
                 else:
                     a.x_nchw_f32, a.x = 1, self.x.data_ptr()
+            elif self._mat_ok(2.0 * B * a.p * a.q * h[i] * 16 * cin):
+                a.x = self._mat_lrelu(F, src).data_ptr()
             else:
                 a.x, a.x_xf = src.data_ptr(), _act()
             a.wt, a.bias = net.w(f"encoder.{i}.0.weight"), net.p(f"encoder.{i}.0.bias")
@@ -368,6 +388,8 @@ class VQStepPlan:
             cout = self.cy if last else r[i + 1]
             a = self._conv(src, r[i], cout, 4, 2, 1, transposed=True)
             a.x, a.x_xf = src.data_ptr(), _act()
+            if not last and self._mat_ok(2.0 * B * src.shape[1] * src.shape[2] * r[i] * cout * 16):
+                a.x, a.x_xf = self._mat_lrelu(F, src).data_ptr(), L.Xform()
             a.wt, a.bias = net.w(f"decoder.{iup + i}.0.weight"), net.p(f"decoder.{iup + i}.0.bias")
             if last and self.pad_rgb:
                 a.wt, a.bias = self.w8d.data_ptr(), self.b8d.data_ptr()
@@ -424,6 +446,8 @@ class VQStepPlan:
             self._add(Bw, "vae_convT2d_bwd_data", a)
             f = self._conv(xin, r[i], cout, 4, 2, 1, transposed=True)
             f.x, f.x_xf = xin.data_ptr(), _act()
+            if xin.data_ptr() in self._mat:
+                f.x, f.x_xf = self._mat[xin.data_ptr()].data_ptr(), L.Xform()
             f.dy, f.dw, f.db = gouts[i].data_ptr(), self.g(name + ".weight"), self.g(name + ".bias")
             self._add(Bw, "vae_convT2d_bwd_filter", f)
         g_din = self._res_stack_bwd("decoder", 1, self.d_in, self.d_t, self.d_h)
@@ -463,6 +487,8 @@ class VQStepPlan:
                 f.c, f.x = 8, self.x8.data_ptr()
             elif i == 0:
                 f.x_nchw_f32, f.x = 1, self.x.data_ptr()
+            elif self.enc[i - 1].data_ptr() in self._mat:
+                f.x = self._mat[self.enc[i - 1].data_ptr()].data_ptr()
             else:
                 f.x, f.x_xf = self.enc[i - 1].data_ptr(), _act()
             f.dy, f.dw, f.db = self.g_enc[i].data_ptr(), self.g(f"encoder.{i}.0.weight"), self.g(f"encoder.{i}.0.bias")
