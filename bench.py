@@ -165,6 +165,12 @@ def kernel_costs(plan, dsz):
     from vae_amd import _lib as L
     out = []
     for fn, ref in plan.fwd_calls + plan.bwd_calls:
+        if fn == "vae_convT2d_fwd_recon":           # (conv args, recon args): the ConvT + Tanh/MSE
+            a, rc = ref[0]._obj, ref[1]._obj
+            f, b = conv_cost("vae_convT2d_fwd", a, dsz)
+            img = rc.n * rc.c * rc.h * rc.w * 4
+            out.append((fn, ref, f, b + 2 * img + (rc.n * rc.h * rc.w * 8 * dsz if rc.dy else 0)))
+            continue
         if isinstance(ref, tuple) or ref is None:
             out.append((fn, None, 0, 0))
             continue
@@ -181,6 +187,10 @@ def kernel_costs(plan, dsz):
             f, b = head_cost(fn, a, dsz)
         elif isinstance(a, L.VqArgs):
             f, b = vq_cost(fn, a, dsz)
+        elif isinstance(a, L.BnApplyArgs):          # materialised transform: read (+ aux), write
+            f, b = 0, a.rows * a.channels * dsz * (3 if a.xf.kind == L.X_BN_DY else 2)
+        elif isinstance(a, L.ReconLossArgs):        # recon, target read; dL/drecon written
+            f, b = 0, 3 * a.n * a.c * a.h * a.w * 4
         else:
             f, b = 0, 0
         out.append((fn, ref, f, b))

@@ -27,6 +27,7 @@
 //     (E_BNBWD) of the cgemm contract, 16-byte stores.
 #include "vae_launch.hpp"
 #include "vae_bgemm.hpp"
+#include "vae_wgemm.hpp"
 
 namespace vae {
 namespace {
@@ -275,6 +276,142 @@ __global__ void __launch_bounds__(BG_T, 2) bgemm_kernel(const GemmParams p) {
   }
 }
 
+// ------------------------------------------------------------------ weight gradient
+//   dW[m][r][s][j] += Σ_pix U[pix][m] · V[pix -> (hu*S-P+r, wu*S-P+s)][j]     (vae_wgemm.hpp)
+// on the same pipeline, for transform-free operands (the materialised activation and gradient of
+// the large layers): 128 (m) x 128 (j) tiles of one tap, K-step 64 pixels.  A K-step stages the
+// U rows [64 pixels][128 m] and the tap-shifted V rows [64][128 j] as 256-byte LDS rows by
+// LDS-DMA, 16-byte chunk c of row P at slot c ^ (((P & 3) << 2) | ((P >> 2) & 3)) (set through
+// the source address; cdna_hip_programming.md T10 image (b)), and the MFMA operands are read
+// column-major with ds_read_b64_tr_b16 (K = pixels).  Out-of-image taps and pixels past the
+// slice read zeros (buffer range check).  Partials: one K slice adds with plain load + store,
+// several with fp32 atomics (wg_epilogue).
+constexpr int BW_KP = 64;
+constexpr int BW_TILE = BW_KP * 256;                  // 16 KB: 64 pixel rows x 128 channels
+constexpr int BW_STAGE = 2 * BW_TILE;
+constexpr int BW_OPS = 2 * BW_STAGE;                  // two stages (64 KB)
+
+__device__ __forceinline__ int bw_sw(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+__global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int gm = p.M / 128, gj = p.J / 128, taps = p.R * p.R;
+  const int per_slice = gm * gj * taps;
+  int b;
+  {
+    // XCD-aware order: each XCD takes a contiguous range (j fastest, then tap, m tile, slice), so
+    // the workgroups re-reading one U slice sit on one L2
+    const int nb = (int)gridDim.x, x = (int)blockIdx.x & 7, loc = (int)blockIdx.x >> 3;
+    const int q = nb >> 3, rr = nb & 7;
+    b = x * q + min(x, rr) + loc;
+  }
+  const int slice = b / per_slice;
+  int t = b - slice * per_slice;
+  const int tj = t % gj;
+  t /= gj;
+  const int tap = t % taps, tmi = t / taps;
+  const int r = tap / p.R, s = tap - r * p.R;
+  const int m0 = tmi * 128, j0 = tj * 128;
+  const long npix = (long)p.n * p.hu * p.wu;
+  const long k0 = (long)slice * p.kper;
+  const long k1 = min(npix, k0 + p.kper);
+  const int nsteps = (int)((k1 - k0 + BW_KP - 1) / BW_KP);
+  const rsrc_t ru = make_rsrc(p.u, p.u_bytes), rv = make_rsrc(p.v, p.v_bytes);
+
+  // wave-instruction j writes LDS rows 4 (4 wave + j) .. + 3: lane -> row + (lane >> 4), slot lane & 15
+  int rowj[4], cj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    rowj[j] = 4 * (4 * wave + j) + (lane >> 4);
+    cj[j] = (lane & 15) ^ bw_sw(rowj[j]);                       // the logical chunk this slot holds
+  }
+  auto issue = [&](int step, int buf) {
+    const long kb = k0 + (long)step * BW_KP;
+    char* lu = smem + buf * BW_STAGE + wave * 4096;
+    char* lv = lu + BW_TILE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long pix = kb + rowj[j];
+      const bool in = pix < k1;
+      const uint32_t pp = in ? (uint32_t)pix : 0u;
+      const uint32_t qd = p.fd_wu.div(pp);                      // n * hu + hu_i
+      const int wu_i = (int)(pp - qd * (uint32_t)p.wu);
+      const uint32_t nn = p.fd_hu.div(qd);
+      const int hu_i = (int)(qd - nn * (uint32_t)p.hu);
+      const int hv_i = hu_i * p.S - p.P + r, wv_i = wu_i * p.S - p.P + s;
+      const bool vin = in && (uint32_t)hv_i < (uint32_t)p.hv && (uint32_t)wv_i < (uint32_t)p.wv;
+      const uint32_t ou = in ? (uint32_t)((pp * (uint32_t)p.M + (uint32_t)(m0 + 8 * cj[j])) * 2u) : kOOB;
+      const uint32_t ov = vin ? (uint32_t)(((((uint32_t)nn * p.hv + hv_i) * p.wv + wv_i) * (uint32_t)p.J +
+                                            (uint32_t)(j0 + 8 * cj[j])) * 2u) : kOOB;
+      glds16(ru, lu + j * 1024, ou);
+      glds16(rv, lv + j * 1024, ov);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed reads: lane 4q+p of 16-lane group g reads pixel row 8g + 4h + q, channels
+  // c0 + 4p .. +3 of the fragment's 16 (T10: off(row, c0 + (p >> 1)) + 8 (p & 1)); rows + 32 for
+  // the second MFMA K-step keep the same swizzle
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  int aoff[4][2], boff[4][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q4;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int ca = (wm * 64 + f * 16) / 8 + (p4 >> 1), cb = (wn * 64 + f * 16) / 8 + (p4 >> 1);
+      aoff[f][h] = row * 256 + 16 * (ca ^ bw_sw(row)) + 8 * (p4 & 1);
+      boff[f][h] = row * 256 + 16 * (cb ^ bw_sw(row)) + 8 * (p4 & 1);
+    }
+  }
+
+  if (nsteps > 0) issue(0, 0);
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) {
+      issue(st + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // this wave's loads of step st landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();                           // ... and every wave's
+    const char* lu = smem + buf * BW_STAGE;
+    const char* lv = lu + BW_TILE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const wgm_bf16x4 a0 = wgm_tr_read(lu + kk * 32 * 256 + aoff[f][0]);
+        const wgm_bf16x4 a1 = wgm_tr_read(lu + kk * 32 * 256 + aoff[f][1]);
+        const wgm_bf16x4 b0 = wgm_tr_read(lv + kk * 32 * 256 + boff[f][0]);
+        const wgm_bf16x4 b1 = wgm_tr_read(lv + kk * 32 * 256 + boff[f][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          af[f][e] = a0[e]; af[f][4 + e] = a1[e];
+          bfr[f][e] = b0[e]; bfr[f][4 + e] = b1[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();                           // every wave is done reading `buf`
+  }
+  const long rowstride = (long)taps * p.J;
+  wg_epilogue<4, 4>(p, nullptr, acc, m0 + wm * 64 + 4 * g, j0 + wn * 64 + li, rowstride, (long)tap * p.J);
+}
+
 template <int AM, int EM>
 int bgemm_go(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
   int kmax = p.K;
@@ -339,6 +476,46 @@ bool bgemm_ok(const GemmParams& p, int am, int em) {
 int bgemm_launch(const GemmParams& p, int am, int em, void* ws, long ws_bytes, hipStream_t st) {
   if (am == A_CONV) return em == E_STORE ? bgemm_go<A_CONV, E_STORE>(p, ws, ws_bytes, st) : bgemm_go<A_CONV, E_BNBWD>(p, ws, ws_bytes, st);
   return em == E_STORE ? bgemm_go<A_CONVT, E_STORE>(p, ws, ws_bytes, st) : bgemm_go<A_CONVT, E_BNBWD>(p, ws, ws_bytes, st);
+}
+
+// Weight gradients on the LDS-DMA pipeline: transform-free operands (the materialised activation
+// and BatchNorm-backward gradient), 128-multiple channel counts, work >= 4 GFLOP (VAE_BG_MINGF).
+bool bwg_ok(const WgParams& p) {
+  static const bool off = getenv("VAE_NO_BWG") != nullptr;
+  if (off || p.u_xf.kind != VAE_X_NONE || p.v_xf.kind != VAE_X_NONE || p.jst || p.db) return false;
+  if (p.M % 128 || p.J % 128 || p.M <= 0 || p.J <= 0) return false;
+  if (((uintptr_t)p.u | (uintptr_t)p.v) & 15) return false;
+  const long npix = (long)p.n * p.hu * p.wu;
+  if (npix * p.M * 2 >= (1l << 31) || (long)p.n * p.hv * p.wv * p.J * 2 >= (1l << 31)) return false;
+  const double flops = 2.0 * p.M * p.J * p.R * p.R * (double)npix;
+  static const double minf = tune_env("VAE_BG_MINGF", 0) > 0 ? tune_env("VAE_BG_MINGF", 0) * 1e9 : 4e9;
+  return flops >= minf;
+}
+
+int bwg_launch(WgParams p, hipStream_t st) {
+  p.fd_wu = make_fastdiv(p.wu);
+  p.fd_hu = make_fastdiv(p.hu);
+  p.fd_r = make_fastdiv(p.R);
+  const long npix = (long)p.n * p.hu * p.wu;
+  p.u_bytes = (uint32_t)(npix * p.M * 2);
+  p.v_bytes = (uint32_t)((long)p.n * p.hv * p.wv * p.J * 2);
+  const long tiles = (long)(p.M / 128) * (p.J / 128) * p.R * p.R;
+  const long ksteps = (npix + BW_KP - 1) / BW_KP;
+  // K slices: one round of two workgroups per CU (floor: no overflow round), >= 8 K-steps each
+  static const int wgpercu = tune_env("VAE_BWG_WGPERCU", 2);
+  static const int mink = tune_env("VAE_BWG_MINK", 8);
+  const long slots = (long)wgpercu * kCUs;
+  long split = slots / tiles;
+  if (split > ksteps / mink) split = ksteps / mink;
+  if (split < 1) split = 1;
+  p.kper = (int)(((ksteps + split - 1) / split) * BW_KP);
+  split = (npix + p.kper - 1) / p.kper;
+  p.slab = nullptr;
+  p.slab_ld = 0;
+  p.own = split == 1 ? 1 : 0;
+  p.jst = 0;
+  VAE_LAUNCH(bwg_kernel, dim3((unsigned)(tiles * split)), dim3(BG_T), BW_OPS, st, p);
+  return check_launch("bwg");
 }
 
 }  // namespace vae

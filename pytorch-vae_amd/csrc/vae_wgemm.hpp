@@ -730,7 +730,12 @@ inline int wg2_reduce(const WgPlan& w, hipStream_t st) {
   return check_launch("wg_slab_reduce");
 }
 
+// the LDS-DMA weight-gradient GEMM for the large transform-free layers (vae_bgemm.hip)
+bool bwg_ok(const WgParams& p);
+int bwg_launch(WgParams p, hipStream_t st);
+
 inline int wg2_launch(WgParams p, void* ws, long ws_bytes, hipStream_t st) {
+  if (bwg_ok(p)) return bwg_launch(p, st);
   WgPlan w;
   if (int rc = wg2_plan(p, ws, ws_bytes, &w)) return rc;
   wg2_launch_main(w, st);

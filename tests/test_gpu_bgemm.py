@@ -119,3 +119,23 @@ def test_bn_apply_matches_torch():
         got = out.float().permute(0, 3, 1, 2).cpu()
         err = float((got - want).abs().max() / want.abs().max())
         assert err < 8e-3, (kind, err)
+
+
+WGRAD_B = [  # transposed, N, cin, cout, hw (input grid), stride, R, pad
+    (False, 64, 256, 512, 16, 2, 3, 1),     # big_ae encoder.2 (K split over workgroups: atomics)
+    (False, 64, 1024, 2048, 4, 2, 3, 1),    # big_ae encoder.4 (one K slice: plain accumulate)
+    (True, 64, 512, 256, 8, 2, 3, 1),       # big_ae decoder ConvT
+    (False, 64, 128, 256, 32, 2, 4, 1),     # VQ-VAE encoder.1 (k4 s2)
+    (True, 64, 256, 128, 16, 2, 4, 1),      # VQ-VAE decoder ConvT(256 -> 128)
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_B)
+def test_bwg_weight_gradient(shape):
+    """Weight gradients of transform-free operands (the materialised activation / gradient) on the
+    LDS-DMA kernel (bwg_kernel), against the fp64 autograd weight gradient (bar 2e-3 of max)."""
+    from test_gpu_cgemm import run_wgrad
+    from vae_amd import _lib as L
+    tr, *rest = shape
+    log = _launched(lambda: run_wgrad(tr, *rest, L.X_NONE, L.X_NONE))
+    assert "bwg_kernel" in log, log
