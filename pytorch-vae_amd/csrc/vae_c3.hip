@@ -260,6 +260,207 @@ __global__ void __launch_bounds__(BN * 4) c3_kernel(const C3Params p) {
   }
 }
 
+// ------------------------------------------------------------------ forward / data gradient, LDS-DMA
+// The same correlation on an LDS-DMA pipeline (buffer_load ... lds: no VGPR staging, no store
+// phase between the chunks).  A stage is one 32-channel chunk x one tap row r: the 16 patch rows
+// that row reads (18 x 16 = 288 pixels, 64-B LDS rows) and its 3 taps x 128 weight rows — 43 KB,
+// three stages in a ring (two in flight while one computes), where the whole-chunk stage of
+// c3_kernel (95 KB) left room for one and exposed the chunk loads and LDS stores (~10 us per call,
+// DESIGN §4 ablation).  Re-reading the patch per tap row costs 36 % more L2 -> LDS bytes.
+// The LDS image is lane-linear (lane l of a wave-instruction writes base + 16 l): row P holds its
+// chunk c at slot c ^ ((P >> 1) & 2), set through the per-lane source address; out-of-image patch
+// pixels read zeros through the buffer resource's range check.  The LeakyReLU of an activated A
+// (ACT) is applied to the fragments after their LDS reads.
+constexpr int D3_PROWS = 384;                      // patch image rows per stage (288 used, DMA-uniform)
+constexpr int D3_WROWS = 384;                      // 3 taps x 128 weight rows
+constexpr int D3_STAGE = (D3_PROWS + D3_WROWS) * 64;        // 49152
+constexpr int D3_OPS = 3 * D3_STAGE;                        // 147456
+constexpr int D3_EPI = 256 * C3T<128>::LDC * 4;             // 135168
+constexpr int D3_LDS = D3_OPS > D3_EPI ? D3_OPS : D3_EPI;
+
+typedef __attribute__((address_space(3))) void c3_lds_void;
+__device__ __forceinline__ void c3_glds16(rsrc_t r, const char* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (c3_lds_void*)(uintptr_t)(uint32_t)(uintptr_t)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 lrelu8(bf16x8 v, float slope) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) w[e] = lrelu_pk(w[e], slope);
+  return v;
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(512) c3d_kernel(const C3Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[D3_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt = p.N / 128;
+  int tile;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
+  }
+  const int img = tile / nt, n0 = (tile - img * nt) * 128;
+  const rsrc_t ra = make_rsrc(p.a, p.a_bytes);
+  const rsrc_t rb = make_rsrc(p.b, p.b_bytes);
+  const int C = p.C;
+  const int rowb = 16 * C * 2;                                // bytes of one image row of A
+
+  // this wave's 6 DMA instructions per stage: I = wave + 8u; I < 24 patch rows 16I.., else weights
+  int poff[3], prow[3], pwok[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int L = 16 * (wave + 8 * u) + (lane >> 2);
+    const int c = (lane & 3) ^ ((L >> 1) & 2);
+    const int ph = L / C3_PW, pw = L - ph * C3_PW;
+    prow[u] = L < 288 ? ph : 99;                              // patch row within the tap row's 16
+    pwok[u] = (unsigned)(pw - 1) < 16u;
+    poff[u] = (((img * 16 + ph - 1) * 16 + (pw - 1)) * C + c * 8) * 2;   // at dr = 0 (may be < 0: masked)
+  }
+  int woff[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int L = 16 * (wave + 8 * u) + (lane >> 2);         // weight row s * 128 + nl
+    const int c = (lane & 3) ^ ((L >> 1) & 2);
+    const int sc = L >> 7, nl = L & 127;
+    woff[u] = (((n0 + nl) * 9 + sc) * C + c * 8) * 2;         // at tap row 0
+  }
+  // stage (chunk kc, tap row r) -> buffer b
+  auto issue = [&](int kc, int r, int b) {
+    const int dr = p.flip ? 2 - r : r;
+    char* base = smem + b * D3_STAGE;
+    const uint32_t cb = (uint32_t)kc * 64u;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const bool ok = pwok[u] && (unsigned)(prow[u] + dr - 1) < 16u;
+      c3_glds16(ra, base + (wave + 8 * u) * 1024, ok ? (uint32_t)(poff[u] + dr * rowb) + cb : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      c3_glds16(rb, base + D3_PROWS * 64 + (wave + 8 * u) * 1024, (uint32_t)(woff[u] + r * 3 * C * 2) + cb);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kq = lane >> 4, lr = lane & 15;
+  // fragment byte offsets within a stage: A at tap column shift ds (0..2), B at tap column s
+  auto aoff = [&](int i, int ds) {
+    const int P = (wm * 4 + i) * C3_PW + lr + ds;
+    return P * 64 + ((kq ^ ((P >> 1) & 2)) << 4);
+  };
+  auto boff = [&](int s, int j) {
+    const int P = s * 128 + wn * 64 + j * 16 + lr;
+    return D3_PROWS * 64 + P * 64 + ((kq ^ ((P >> 1) & 2)) << 4);
+  };
+  auto frags = [&](const char* st, int s, bf16x8 (&af)[4], bf16x8 (&bfr)[4]) {
+    const int ds = p.flip ? 2 - s : s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(st + aoff(i, ds));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(st + boff(s, j));
+  };
+  auto compute = [&](const char* st) {
+    bf16x8 af[2][4], bfr[2][4];
+    frags(st, 0, af[0], bfr[0]);
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0): this tap's fragments
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < 3) frags(st, s + 1, af[(s + 1) & 1], bfr[(s + 1) & 1]);
+      if constexpr (ACT) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[s & 1][i] = lrelu8(af[s & 1][i], p.a_slope);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s & 1][i], bfr[s & 1][j], acc[i][j], 0, 0, 0);
+      if (s + 1 < 3) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      }
+    }
+  };
+
+  const int nchunks = C / 32;
+  const int nst = 3 * nchunks;
+  issue(0, 0, 0);
+  if (nst > 1) issue(0, 1, 1);
+  for (int kc = 0; kc < nchunks; ++kc) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int k = 3 * kc + r;
+      if (k + 2 < nst) {
+        issue(kc + (r + 2) / 3, (r + 2) % 3, (r + 2) % 3);
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      } else if (k + 1 < nst) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      compute(smem + r * D3_STAGE);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+
+  // ---- epilogue through LDS (as c3_kernel): fp32 tile [256 pixels][128 (+4)], 16-byte rows
+  constexpr int LDC = C3T<128>::LDC;
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Cs[((wm * 4 + i) * 16 + 4 * (lane >> 4) + e) * LDC + wn * 64 + j * 16 + lr] = acc[i][j][e];
+  __syncthreads();
+  const rsrc_t rres = make_rsrc(p.residual ? p.residual : p.out, p.residual ? p.o_bytes : 0u);
+  const rsrc_t raux = make_rsrc(p.aux ? p.aux : p.out, p.aux ? p.o_bytes : 0u);
+  __bf16* out = static_cast<__bf16*>(p.out);
+#pragma unroll 2
+  for (int k = 0; k < 8; ++k) {
+    const int it = tid + 512 * k;
+    const int pix = it / 16, cg = (it % 16) * 8;
+    const uint32_t o = (uint32_t)((img * 256 + pix) * p.N + n0 + cg);
+    uint32_t rs[4], ax[4];
+    bload<16>(rres, p.residual ? o * 2u : kOOB, rs);
+    bload<16>(raux, p.aux ? o * 2u : kOOB, ax);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + pix * LDC + cg);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + pix * LDC + cg + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    uint32_t pk[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float g0 = v[2 * e] + __uint_as_float(rs[e] << 16);
+      float g1 = v[2 * e + 1] + __uint_as_float(rs[e] & 0xffff0000u);
+      if (p.bias) { g0 += p.bias[n0 + cg + 2 * e]; g1 += p.bias[n0 + cg + 2 * e + 1]; }
+      if (p.aux) {
+        if (!(__uint_as_float(ax[e] << 16) > 0.f)) g0 *= p.aux_slope;
+        if (!(__uint_as_float(ax[e] & 0xffff0000u) > 0.f)) g1 *= p.aux_slope;
+      }
+      bf16x2 h;
+      h[0] = (__bf16)g0;
+      h[1] = (__bf16)g1;
+      pk[e] = *reinterpret_cast<uint32_t*>(&h);
+    }
+    *reinterpret_cast<uint4*>(out + o) = uint4{pk[0], pk[1], pk[2], pk[3]};
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 //   dW[m][r][s][c] += Σ_{n,h,w} U[n,h,w,m] · V'[n, h+r-1, w+s-1, c]     (U = dy, V' = xf(x))
 // One workgroup: 128 m x 32 c x all 9 taps over a group of G images.  Per image it stages U
@@ -668,7 +869,12 @@ int c3_launch(const C3Args& a, hipStream_t st) {
   // VAE_C3_BN=64: two 256-thread workgroups per CU (A/B timing: 65 vs 48 us forward, slower)
   static const int bn = (getenv("VAE_C3_BN") && atoi(getenv("VAE_C3_BN")) == 64) ? 64 : 128;
   const unsigned grid = (unsigned)(a.n * (a.N / bn));
-  if (bn == 128) VAE_LAUNCH(c3_kernel<128>, dim3(grid), dim3(512), 0, st, p);
+  // VAE_C3_V1=1: the register-staged whole-chunk kernel (A/B timing)
+  static const bool v1 = getenv("VAE_C3_V1") != nullptr;
+  if (bn == 128 && !v1 && a.C % 32 == 0) {
+    if (a.a_act) VAE_LAUNCH(c3d_kernel<1>, dim3(grid), dim3(512), 0, st, p);
+    else VAE_LAUNCH(c3d_kernel<0>, dim3(grid), dim3(512), 0, st, p);
+  } else if (bn == 128) VAE_LAUNCH(c3_kernel<128>, dim3(grid), dim3(512), 0, st, p);
   else VAE_LAUNCH(c3_kernel<64>, dim3(grid), dim3(256), 0, st, p);
   return check_launch("c3");
 }

@@ -37,8 +37,17 @@ def test_c3_forward(n, cin, cout, act, bias):
         a.x_xf = L.Xform(kind=L.X_ACT, channels=cin, slope=0.01)
     if bias:
         a.bias = bd.data_ptr()
-    L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    lib = L.load()
+    lib.vae_launch_log(1)
+    try:
+        L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    finally:
+        lib.vae_launch_log(0)
     torch.cuda.synchronize()
+    need = lib.vae_launch_log_names(None, 0)
+    buf = ctypes.create_string_buffer(int(need))
+    lib.vae_launch_log_names(buf, need)
+    assert b"c3d_kernel" in buf.value, buf.value             # the LDS-DMA image-tile kernel ran
     assert rel(to_nchw(out), ref) < TOL
 
 
