@@ -60,6 +60,42 @@ __device__ __forceinline__ uint32_t p1_lrelu(uint32_t w, float slope) {
   return *reinterpret_cast<uint32_t*>(&pk);
 }
 
+// out[m0 + row][n0 + cg..+7] = epi(Cs[row][cg..+7]): + bias, + xf(residual), * act'(aux); bf16
+__device__ __forceinline__ void p1_epilogue(const P1Params& p, const float* Cs, int m0, int n0, int tid) {
+  const rsrc_t rres = make_rsrc(p.residual ? p.residual : p.out, p.residual ? p.o_bytes : 0u);
+  const rsrc_t raux = make_rsrc(p.aux ? p.aux : p.out, p.aux ? p.o_bytes : 0u);
+  __bf16* out = static_cast<__bf16*>(p.out);
+#pragma unroll 2
+  for (int k = 0; k < P1_BM * (P1_BN / 8) / P1_NT; ++k) {
+    const int it = tid + P1_NT * k;
+    const int row = it >> 4, cg = (it & 15) * 8;
+    const uint32_t o = (uint32_t)((m0 + row) * p.N + n0 + cg);
+    uint32_t rs[4], ax[4];
+    bload<16>(rres, p.residual ? o * 2u : kOOB, rs);
+    bload<16>(raux, p.aux ? o * 2u : kOOB, ax);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * P1_LDC + cg);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * P1_LDC + cg + 4);
+    const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    uint32_t pk[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float r0 = __uint_as_float(rs[e] << 16), r1 = __uint_as_float(rs[e] & 0xffff0000u);
+      if (p.res_act) { r0 = fmaxf(r0, r0 * p.res_slope); r1 = fmaxf(r1, r1 * p.res_slope); }
+      float g0 = v[2 * e] + r0, g1 = v[2 * e + 1] + r1;
+      if (p.bias) { g0 += p.bias[n0 + cg + 2 * e]; g1 += p.bias[n0 + cg + 2 * e + 1]; }
+      if (p.aux) {
+        if (!(__uint_as_float(ax[e] << 16) > 0.f)) g0 *= p.aux_slope;
+        if (!(__uint_as_float(ax[e] & 0xffff0000u) > 0.f)) g1 *= p.aux_slope;
+      }
+      bf16x2 h;
+      h[0] = (__bf16)g0;
+      h[1] = (__bf16)g1;
+      pk[e] = *reinterpret_cast<uint32_t*>(&h);
+    }
+    *reinterpret_cast<uint4*>(out + o) = uint4{pk[0], pk[1], pk[2], pk[3]};
+  }
+}
+
 __global__ void __launch_bounds__(P1_NT) p1_kernel(const P1Params p) {
   __shared__ __attribute__((aligned(16))) char smem[P1_LDS];
   char* const As = smem;
@@ -152,38 +188,108 @@ __global__ void __launch_bounds__(P1_NT) p1_kernel(const P1Params p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) Cs[(wm * 64 + i * 16 + 4 * kq + e) * P1_LDC + wn * 64 + j * 16 + lr] = acc[i][j][e];
   __syncthreads();
-  const rsrc_t rres = make_rsrc(p.residual ? p.residual : p.out, p.residual ? p.o_bytes : 0u);
-  const rsrc_t raux = make_rsrc(p.aux ? p.aux : p.out, p.aux ? p.o_bytes : 0u);
-  __bf16* out = static_cast<__bf16*>(p.out);
-#pragma unroll 2
-  for (int k = 0; k < P1_BM * (P1_BN / 8) / P1_NT; ++k) {
-    const int it = tid + P1_NT * k;
-    const int row = it >> 4, cg = (it & 15) * 8;
-    const uint32_t o = (uint32_t)((m0 + row) * p.N + n0 + cg);
-    uint32_t rs[4], ax[4];
-    bload<16>(rres, p.residual ? o * 2u : kOOB, rs);
-    bload<16>(raux, p.aux ? o * 2u : kOOB, ax);
-    const f32x4 v0 = *reinterpret_cast<const f32x4*>(Cs + row * P1_LDC + cg);
-    const f32x4 v1 = *reinterpret_cast<const f32x4*>(Cs + row * P1_LDC + cg + 4);
-    const float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    uint32_t pk[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float r0 = __uint_as_float(rs[e] << 16), r1 = __uint_as_float(rs[e] & 0xffff0000u);
-      if (p.res_act) { r0 = fmaxf(r0, r0 * p.res_slope); r1 = fmaxf(r1, r1 * p.res_slope); }
-      float g0 = v[2 * e] + r0, g1 = v[2 * e + 1] + r1;
-      if (p.bias) { g0 += p.bias[n0 + cg + 2 * e]; g1 += p.bias[n0 + cg + 2 * e + 1]; }
-      if (p.aux) {
-        if (!(__uint_as_float(ax[e] << 16) > 0.f)) g0 *= p.aux_slope;
-        if (!(__uint_as_float(ax[e] & 0xffff0000u) > 0.f)) g1 *= p.aux_slope;
-      }
-      bf16x2 h;
-      h[0] = (__bf16)g0;
-      h[1] = (__bf16)g1;
-      pk[e] = *reinterpret_cast<uint32_t*>(&h);
-    }
-    *reinterpret_cast<uint4*>(out + o) = uint4{pk[0], pk[1], pk[2], pk[3]};
+  p1_epilogue(p, Cs, m0, n0, tid);
+}
+
+// LDS-DMA form (p1d_kernel): the operands go global -> LDS by buffer_load ... lds (lane l of a
+// wave-instruction writes base + 16 l; row P holds chunk c at slot c ^ ((P >> 1) & 7), set through
+// the source address), two 32 KB stages with one K-step in flight behind the MFMAs (counted vmcnt +
+// raw barriers, vae_bgemm.hip), the ReLU / LeakyReLU of an activated A applied to the fragments.
+// Same tile, epilogue and XCD order as p1_kernel; 67.6 KB of LDS, two workgroups per CU.
+typedef __attribute__((address_space(3))) void p1_lds_void;
+__device__ __forceinline__ void p1_glds16(rsrc_t r, const char* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (p1_lds_void*)(uintptr_t)(uint32_t)(uintptr_t)lds_wave_base, 16, voff, 0, 0, 0);
+}
+
+constexpr int P1D_STAGE = (P1_BM + P1_BN) * P1_ROW;       // 32768
+constexpr int P1D_LDS = 2 * P1D_STAGE > P1_EPI ? 2 * P1D_STAGE : P1_EPI;
+
+template <int ACT>
+__global__ void __launch_bounds__(P1_NT, 2) p1d_kernel(const P1Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[P1D_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt = p.N / P1_BN;
+  int tile;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
   }
+  const int mt = tile / nt, n0 = (tile - mt * nt) * P1_BN, m0 = mt * P1_BM;
+  const rsrc_t ra = make_rsrc(p.a, p.a_bytes);
+  const rsrc_t rb = make_rsrc(p.b, p.b_bytes);
+  // wave-instruction j (0..3) of this wave: tile rows 8 (4 wave + j) .. + 7, lane -> row + (lane >> 3)
+  uint32_t aoffg[4], boffg[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 8 * (4 * wave + j) + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    aoffg[j] = (uint32_t)(((m0 + row) * p.C + c * 8) * 2);
+    boffg[j] = (uint32_t)(((n0 + row) * p.C + c * 8) * 2);
+  }
+  auto issue = [&](int kc, int buf) {
+    char* la = smem + buf * P1D_STAGE + wave * 4096;
+    char* lb = la + P1_BM * P1_ROW;
+    const uint32_t cb = (uint32_t)kc * (P1_KC * 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p1_glds16(ra, la + j * 1024, aoffg[j] + cb);
+      p1_glds16(rb, lb + j * 1024, boffg[j] + cb);
+    }
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kq = lane >> 4, lr = lane & 15;
+  const int nchunks = p.C / P1_KC;
+  issue(0, 0);
+  for (int kc = 0; kc < nchunks; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nchunks) {
+      issue(kc + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* As = smem + buf * P1D_STAGE;
+    const char* Bs = As + P1_BM * P1_ROW;
+#pragma unroll
+    for (int kk = 0; kk < P1_KC / 32; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const bf16x8*>(As + p1_sw(wm * 64 + i * 16 + lr, kk * 4 + kq));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + p1_sw(wn * 64 + j * 16 + lr, kk * 4 + kq));
+      if constexpr (ACT) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t* w = reinterpret_cast<uint32_t*>(&af[i]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = p1_lrelu(w[e], p.a_slope);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Cs[(wm * 64 + i * 16 + 4 * kq + e) * P1_LDC + wn * 64 + j * 16 + lr] = acc[i][j][e];
+  __syncthreads();
+  p1_epilogue(p, Cs, m0, n0, tid);
 }
 
 inline bool p1_al16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
@@ -208,7 +314,11 @@ int p1_launch(const P1Args& a, hipStream_t st) {
   p.a_slope = a.a_slope; p.res_slope = a.res_slope; p.aux_slope = a.aux_slope;
   p.a_act = a.a_act; p.res_act = a.res_act; p.M = (int)a.M; p.C = a.C; p.N = a.N;
   const unsigned grid = (unsigned)((a.M / P1_BM) * (a.N / P1_BN));
-  VAE_LAUNCH(p1_kernel, dim3(grid), dim3(P1_NT), 0, st, p);
+  // VAE_P1_V1=1: the register-staged kernel (A/B timing)
+  static const bool v1 = getenv("VAE_P1_V1") != nullptr;
+  if (v1) VAE_LAUNCH(p1_kernel, dim3(grid), dim3(P1_NT), 0, st, p);
+  else if (a.a_act) VAE_LAUNCH(p1d_kernel<1>, dim3(grid), dim3(P1_NT), 0, st, p);
+  else VAE_LAUNCH(p1d_kernel<0>, dim3(grid), dim3(P1_NT), 0, st, p);
   return check_launch("p1");
 }
 

@@ -69,3 +69,19 @@ def give_workspace(a, *fns):
     a.workspace = ws.data_ptr()
     a.workspace_bytes = ws.numel() * 4
     return ws
+
+
+def launched(fn):
+    """Run fn() with the library's launch log on; return the names of the kernels it launched."""
+    import ctypes
+    from vae_amd import _lib as L
+    lib = L.load()
+    lib.vae_launch_log(1)
+    try:
+        fn()
+    finally:
+        lib.vae_launch_log(0)
+    need = lib.vae_launch_log_names(None, 0)
+    buf = ctypes.create_string_buffer(int(need))
+    lib.vae_launch_log_names(buf, need)
+    return buf.value.decode()

@@ -178,7 +178,9 @@ def test_p1_forward(n, cin, cout, act, res, res_act, bias):
         a.residual = rd.data_ptr()
         if res_act:
             a.residual_xf = L.Xform(kind=L.X_ACT, channels=cout, slope=0.01)
-    L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    from gpu_util import launched
+    log = launched(lambda: L.call("vae_conv2d_fwd", ctypes.byref(a), torch.cuda.current_stream().cuda_stream))
+    assert "p1d_kernel" in log, log                          # the LDS-DMA pointwise kernel ran
     torch.cuda.synchronize()
     assert rel(to_nchw(out), ref) < TOL
 
