@@ -293,6 +293,20 @@ constexpr int BW_OPS = 2 * BW_STAGE;                  // two stages (64 KB)
 
 __device__ __forceinline__ int bw_sw(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
+// Transposed reads as inline asm: the wait-count pass gives the ds_read_tr intrinsic no LDS address
+// and makes it wait for every LDS-DMA in flight (vmcnt(0) at each K-step head, seen in the ISA);
+// asm reads are invisible to it, so their results are waited for explicitly — bw_wait passes the
+// fragments through the s_waitcnt so no consumer can be scheduled above it.
+__device__ __forceinline__ wgm_bf16x4 bw_tr(uint32_t lds_addr) {
+  wgm_bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
+  return r;
+}
+__device__ __forceinline__ void bw_wait(bf16x8 (&a)[4], bf16x8 (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]),
+               "+v"(b[2]), "+v"(b[3])::"memory");
+}
+
 __global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
@@ -383,27 +397,33 @@ __global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();                           // ... and every wave's
-    const char* lu = smem + buf * BW_STAGE;
-    const char* lv = lu + BW_TILE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfr[4];
+    const uint32_t lu = (uint32_t)(uintptr_t)smem + buf * BW_STAGE;
+    const uint32_t lv = lu + BW_TILE;
+    bf16x8 af[2][4], bfr[2][4];
+    auto rd = [&](int kk, bf16x8 (&a)[4], bf16x8 (&b)[4]) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
-        const wgm_bf16x4 a0 = wgm_tr_read(lu + kk * 32 * 256 + aoff[f][0]);
-        const wgm_bf16x4 a1 = wgm_tr_read(lu + kk * 32 * 256 + aoff[f][1]);
-        const wgm_bf16x4 b0 = wgm_tr_read(lv + kk * 32 * 256 + boff[f][0]);
-        const wgm_bf16x4 b1 = wgm_tr_read(lv + kk * 32 * 256 + boff[f][1]);
+        const wgm_bf16x4 a0 = bw_tr(lu + kk * 32 * 256 + aoff[f][0]);
+        const wgm_bf16x4 a1 = bw_tr(lu + kk * 32 * 256 + aoff[f][1]);
+        const wgm_bf16x4 b0 = bw_tr(lv + kk * 32 * 256 + boff[f][0]);
+        const wgm_bf16x4 b1 = bw_tr(lv + kk * 32 * 256 + boff[f][1]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          af[f][e] = a0[e]; af[f][4 + e] = a1[e];
-          bfr[f][e] = b0[e]; bfr[f][4 + e] = b1[e];
+          a[f][e] = a0[e]; a[f][4 + e] = a1[e];
+          b[f][e] = b0[e]; b[f][4 + e] = b1[e];
         }
       }
+    };
+    rd(0, af[0], bfr[0]);
+    bw_wait(af[0], bfr[0]);
+    rd(1, af[1], bfr[1]);                                   // in flight behind the first 16 MFMAs
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk == 1) bw_wait(af[1], bfr[1]);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                           // every wave is done reading `buf`

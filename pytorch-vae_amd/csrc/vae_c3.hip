@@ -673,6 +673,178 @@ __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
     }
 }
 
+// LDS-DMA form of the same weight gradient (c3wd_kernel): a stage is one half image (8 output
+// rows = 4 K blocks of 32 pixels) — its U rows [128 pixels][128 m] (32 KB, w3_usw image) and the
+// 10 x 18 patch rows of V it reads ([180 (256) pixels][32 c], w3_vsw image) — brought in by
+// buffer_load ... lds (the 32-byte-slot swizzles set through the per-lane source address), three
+// stages in a ring with two in flight; c3w_kernel staged one whole image through registers and
+// LDS stores between the compute phases.  The LeakyReLU of an activated V is applied to the B
+// fragments.  Same wave mapping, compute order and slab partials as c3w_kernel.
+constexpr int W3D_UROWS = 128, W3D_VROWS = 256;
+constexpr int W3D_STAGE = W3D_UROWS * W3_URS + W3D_VROWS * W3_VRS;    // 49152
+constexpr int W3D_LDS = 3 * W3D_STAGE;                                 // 147456
+
+// transposed reads as inline asm, waited for explicitly (vae_bgemm.hip bw_tr: the ds_read_tr
+// intrinsic makes the wait-count pass drain every LDS-DMA in flight before it)
+__device__ __forceinline__ w3_bf16x4 w3d_tr(uint32_t lds_addr) {
+  w3_bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
+  return r;
+}
+
+template <int VACT>
+__global__ void __launch_bounds__(W3_NT) c3wd_kernel(const W3Params p) {
+  __shared__ __attribute__((aligned(16))) char smem[W3D_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mq = wave / 3, tr = wave - 3 * (wave / 3);   // m rows 32mq..+31, tap row tr
+  const int ntc = p.J / W3_BC, per = (p.M / W3_BM) * ntc;
+  int tile;
+  {
+    const int nb = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+    tile = x * q + min(x, r) + loc;
+  }
+  const int grp = tile / per, rem = tile - grp * per;
+  const int tj = rem / ntc, tc = rem - tj * ntc;
+  const int j0 = tj * W3_BM, c0 = tc * W3_BC;
+  const int img0 = grp * p.G, img1 = min(p.n, img0 + p.G);
+  const rsrc_t ru = make_rsrc(p.u, p.u_bytes);
+  const rsrc_t rv = make_rsrc(p.v, p.v_bytes);
+
+  // this wave's 4 DMA instructions per stage: I = wave + 12 u (0..47); I < 32: U rows 4I..4I+3
+  // (16 chunks of 16 B per row), else V patch rows 16 (I - 32) .. +15 (4 chunks per row)
+  uint32_t goff[4];
+  int vph[4];
+  bool vok0[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int I = wave + 12 * u;
+    if (I < 32) {                                       // (wave-uniform)
+      const int P = 4 * I + (lane >> 4), sl = lane & 15;
+      const int c16 = ((((sl >> 1) ^ ((P & 3) | ((P >> 1) & 4)))) << 1) | (sl & 1);
+      goff[u] = (uint32_t)((P * p.M + j0 + c16 * 8) * 2);          // + image / half offset per stage
+      vph[u] = 0;
+      vok0[u] = true;
+    } else {
+      const int P = 16 * (I - 32) + (lane >> 2), sl = lane & 3;
+      const int c16 = ((((sl >> 1) ^ ((P >> 3) & 1))) << 1) | (sl & 1);
+      const int ph = P / C3_PW, pw = P - ph * C3_PW;
+      vph[u] = P < 180 ? ph : 99;                                  // patch row (image row 8hh + ph - 1)
+      vok0[u] = (unsigned)(pw - 1) < 16u;
+      goff[u] = (uint32_t)((((ph - 1) * 16 + (pw - 1)) * p.J + c0 + c16 * 8) * 2);   // at hh = 0 (wraps: masked)
+    }
+  }
+  // stage (image img, half hh) -> buffer b
+  auto issue = [&](int img, int hh, int b) {
+    char* base = smem + b * W3D_STAGE;
+    const uint32_t uo = (uint32_t)(img * 256 + hh * 128) * (uint32_t)p.M * 2u;
+    const uint32_t vo = (uint32_t)(img * 256 + hh * 128) * (uint32_t)p.J * 2u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int I = wave + 12 * u;
+      if (I < 32) {
+        c3_glds16(ru, base + I * 1024, goff[u] + uo);
+      } else {
+        const bool ok = vok0[u] && (unsigned)(8 * hh + vph[u] - 1) < 16u;
+        c3_glds16(rv, base + W3D_UROWS * W3_URS + (I - 32) * 1024, ok ? goff[u] + vo : kOOB);
+      }
+    }
+  };
+
+  f32x4 acc[2][2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) acc[i][cb][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  int aoff[2][2], prow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = 8 * g + 4 * h + q4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][h] = w3_usw(row, mq * 2 + i) + 8 * p4;
+    prow[h] = ((g >> 1) + tr) * C3_PW + 8 * (g & 1) + 4 * h + q4;
+  }
+  auto compute = [&](uint32_t Us) {
+    const uint32_t Vs = Us + W3D_UROWS * W3_URS;
+    auto afrag = [&](int kb, bf16x8 (&af)[2]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const w3_bf16x4 a0 = w3d_tr(Us + kb * 32 * W3_URS + aoff[i][0]);
+        const w3_bf16x4 a1 = w3d_tr(Us + kb * 32 * W3_URS + aoff[i][1]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+      }
+    };
+    auto bfrag = [&](int kb, int s, bf16x8 (&bfr)[2]) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int P0 = prow[0] + kb * 2 * C3_PW + s, P1 = prow[1] + kb * 2 * C3_PW + s;
+        const w3_bf16x4 b0 = w3d_tr(Vs + w3_vsw(P0, cb) + 8 * p4);
+        const w3_bf16x4 b1 = w3d_tr(Vs + w3_vsw(P1, cb) + 8 * p4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { bfr[cb][e] = b0[e]; bfr[cb][4 + e] = b1[e]; }
+      }
+    };
+    bf16x8 af[2], bfr[2][2];
+    bfrag(0, 0, bfr[0]);
+#pragma unroll 1
+    for (int kb = 0; kb < 4; ++kb) {
+      afrag(kb, af);
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        // this step's fragments have landed (passed through the wait: no consumer above it)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[s & 1][0]), "+v"(bfr[s & 1][1])::"memory");
+        bfrag(s < 2 ? kb : min(kb + 1, 3), s < 2 ? s + 1 : 0, bfr[(s + 1) & 1]);
+        if constexpr (VACT) {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) bfr[s & 1][cb] = lrelu8(bfr[s & 1][cb], p.v_slope);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            acc[i][cb][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s & 1][cb], acc[i][cb][s], 0, 0, 0);
+      }
+      bfr[0][0] = bfr[1][0]; bfr[0][1] = bfr[1][1];
+    }
+  };
+
+  const int nst = 2 * (img1 - img0);
+  issue(img0, 0, 0);
+  if (nst > 1) issue(img0, 1, 1);
+  for (int k = 0; k < nst; ++k) {
+    const int b = k % 3;
+    if (k + 2 < nst) {
+      issue(img0 + ((k + 2) >> 1), (k + 2) & 1, (k + 2) % 3);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (k + 1 < nst) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    compute((uint32_t)(uintptr_t)smem + b * W3D_STAGE);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  float* part = p.slab + (long)grp * p.slab_ld;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = j0 + mq * 32 + i * 16 + 4 * g + e;
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          part[((long)m * 9 + tr * 3 + s) * p.J + c0 + cb * 16 + li] = acc[i][cb][s][e];
+    }
+}
+
 // dw[i] += Σ_s slab[s * ld + i] (each element one writer), 4 consecutive floats per thread
 __global__ void __launch_bounds__(256) c3w_reduce(const float* slab, long ld, int slices, long cols, float* dw) {
   const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -908,7 +1080,10 @@ int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st) {
   p.v_act = a.v_act; p.v_slope = a.v_slope;
   p.n = a.n; p.M = a.M; p.J = a.J;
   const unsigned grid = (unsigned)(groups * (a.M / W3_BM) * (a.J / W3_BC));
-  VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
+  static const bool v1 = getenv("VAE_C3_V1") != nullptr;
+  if (v1) VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
+  else if (a.v_act) VAE_LAUNCH(c3wd_kernel<1>, dim3(grid), dim3(W3_NT), 0, st, p);
+  else VAE_LAUNCH(c3wd_kernel<0>, dim3(grid), dim3(W3_NT), 0, st, p);
   if (int rc = check_launch("c3w")) return rc;
   VAE_LAUNCH(c3w_reduce, dim3((unsigned)((cols / 4 + 255) / 256)), dim3(256), 0, st, (const float*)p.slab, cols, groups,
              cols, a.dw);
