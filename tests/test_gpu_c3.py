@@ -113,7 +113,9 @@ def test_c3_backward_filter(n, cin, cout, act, bias):
     if bias:
         a.db = db.data_ptr()
     ws = give_workspace(a, "vae_conv2d_bwd_filter")
-    L.call("vae_conv2d_bwd_filter", ctypes.byref(a), torch.cuda.current_stream().cuda_stream)
+    from gpu_util import launched
+    log = launched(lambda: L.call("vae_conv2d_bwd_filter", ctypes.byref(a), torch.cuda.current_stream().cuda_stream))
+    assert "c3wd_kernel" in log, log                         # the LDS-DMA weight-gradient kernel ran
     torch.cuda.synchronize()
     del ws
     got = (dw.cpu() - dw0).permute(0, 3, 1, 2)
