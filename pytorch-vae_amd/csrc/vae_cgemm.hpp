@@ -119,9 +119,11 @@ template <int BM, int BN, int XA> constexpr int cg_waves_per_eu() {
   return (BM >= 128 && BN >= 128) ? 2 : ((BM == 64 && BN == 32 && XA == VAE_X_BN_DY) ? 3 : 1);
 }
 
+// The tile work of workgroup `bid` (operand tiles / epilogue tile at `smem`, CgSmem<...NBUF>::BYTES)
+// — run by cgemm_kernel (one problem per launch) and by the paired data + weight gradient launch
+// (vae_bwd_pair.hip), whose other workgroups run a weight-gradient body in the same LDS.
 template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg_waves_per_eu<BM, BN, XA>())))
-cgemm_kernel(const GemmParams p) {
+__device__ __forceinline__ void cgemm_body(const GemmParams& p, const int bid, char* smem) {
   using WG = CgWaves<BM, BN>;
   constexpr int TM = WG::TM, TN = WG::TN, WTM = TM * 16, WTN = TN * 16;
   constexpr int LDK = CgSmem<BM, BN, BK>::LDK;
@@ -138,7 +140,6 @@ cgemm_kernel(const GemmParams p) {
   static_assert(BM % RPP == 0 || BM < RPP, "A tile rows");
   static_assert(BN % RPP == 0 || BN < RPP, "B tile rows");
 
-  __shared__ __attribute__((aligned(16))) char smem[CgSmem<BM, BN, BK, NBUF>::BYTES];
   extern __shared__ float tabs[];
   __bf16* As = reinterpret_cast<__bf16*>(smem);                 // [2][BM][LDK]
   __bf16* Bs = As + NBUF * BM * LDK;                             // [NBUF][BN][LDK]
@@ -159,7 +160,7 @@ cgemm_kernel(const GemmParams p) {
   const int gm = (p.M + BM - 1) / BM, gn = (p.N + BN - 1) / BN, gz = p.nphase * p.ksplit;
   int tile;
   {
-    const int nb = gm * gn * gz, b = blockIdx.x;
+    const int nb = gm * gn * gz, b = bid;
     const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
     tile = x * q + min(x, r) + loc;
   }
@@ -541,7 +542,7 @@ cgemm_kernel(const GemmParams p) {
         float t1 = 0.f, t2 = 0.f;
 #pragma unroll
         for (int w = 0; w < CgWaves<BM, BN>::WM; ++w) { t1 += fpart[w][0][c]; t2 += fpart[w][1][c]; }
-        epi_flush_sums<EM>(p, (int)blockIdx.x, n0 + c, t1, t2);
+        epi_flush_sums<EM>(p, bid, n0 + c, t1, t2);
       }
     }
   } else if (EM == E_BNBWD && epi_wants_sums<EM>(p)) {
@@ -569,7 +570,7 @@ cgemm_kernel(const GemmParams p) {
       if (n0 + c < p.N) {
         const float t1 = (part[0 * BN + c] + part[2 * BN + c]) + (part[4 * BN + c] + part[6 * BN + c]);
         const float t2 = (part[1 * BN + c] + part[3 * BN + c]) + (part[5 * BN + c] + part[7 * BN + c]);
-        epi_flush_sums<EM>(p, (int)blockIdx.x, n0 + c, t1, t2);
+        epi_flush_sums<EM>(p, bid, n0 + c, t1, t2);
       }
     }
   }
@@ -577,6 +578,24 @@ cgemm_kernel(const GemmParams p) {
 #pragma unroll
   for (int i = 0; i < EPT; ++i)
     if (rok[i]) *reinterpret_cast<uint4*>(out + obase[i]) = pk[i];
+}
+
+template <int BM, int BN, int BK, int OR> constexpr int cg_nbuf() { return OR == 2 ? 1 : 2; }
+
+// A layer's weight gradient riding on this thread's next conv-GEMM launch (vae_conv_bwd_pair,
+// vae_bwd_pair.hip): set around the layer's data-gradient call.  The cgemm launch site offers
+// its grid to pair_cg_launch, which launches data- and weight-gradient workgroups as ONE grid when
+// that pair is instantiated and returns false otherwise (the weight gradient then runs alone).
+struct PairRider;
+PairRider*& pair_rider();
+bool pair_cg_launch(const GemmParams& p, unsigned nb, int bm, int bn, int am, int xa, int em, int orr, size_t lds,
+                    hipStream_t st);
+
+template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg_waves_per_eu<BM, BN, XA>())))
+cgemm_kernel(const GemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[CgSmem<BM, BN, BK, cg_nbuf<BM, BN, BK, OR>()>::BYTES];
+  cgemm_body<BM, BN, BK, AM, XA, EM, OR>(p, (int)blockIdx.x, smem);
 }
 
 }  // namespace vae

@@ -554,6 +554,7 @@ inline void cg_launch_tile(const GemmParams& p, CgTile t, hipStream_t st) {
 #define VAE_CG_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
     const unsigned nb = (unsigned)(((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.nphase * p.ksplit); \
+    if (pair_rider() && pair_cg_launch(p, nb, BM_, BN_, AM, XA, EM, OR, lds, st)) return; \
     VAE_LAUNCH((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM, OR>), dim3(nb), dim3(256), lds, st, p); \
     return; \
   }

@@ -953,10 +953,15 @@ def batch_filter_calls(calls, ends, splits=()):
 
     for end in ends:
         deferred = []
+        paired = pair_calls(calls, lo, end)
         for i in range(lo, end):
             if i in splits and deferred:
                 emit(deferred, True)
                 deferred = []
+            if i in paired:
+                if paired[i] is not None:
+                    out.append(paired[i])
+                continue
             fn, ref = calls[i]
             if fn in DEFERRED_FNS:
                 deferred.append((fn, ref))
@@ -966,6 +971,40 @@ def batch_filter_calls(calls, ends, splits=()):
         new_ends.append(len(out))
         lo = end
     return out, new_ends
+
+
+PAIR_FN = "vae_conv_bwd_pair"
+_PAIRS = {"vae_conv2d_bwd_data": "vae_conv2d_bwd_filter", "vae_convT2d_bwd_data": "vae_convT2d_bwd_filter"}
+
+
+def pair_calls(calls, lo, end):
+    """A BatchNorm'd conv / convT block's bwd_data and bwd_filter calls (adjacent in the raw
+    backward, same dy) as one vae_conv_bwd_pair call at the data call's position: on the bf16
+    conv-GEMM paths its weight gradient runs in the data gradient's grid instead of in the
+    segment's grouped batch.  Returns {raw index: (PAIR_FN, PairCall) at the data call's index,
+    None at the filter call's}.  VAE_PAIR=0 keeps the batch."""
+    if os.environ.get("VAE_PAIR", "1") == "0":
+        return {}
+    out = {}
+    i = lo
+    while i + 1 < end:
+        (f0, r0), (f1, r1) = calls[i], calls[i + 1]
+        pair = None
+        if _PAIRS.get(f0) == f1:
+            pair = (i, r0, i + 1, r1, f0)
+        elif _PAIRS.get(f1) == f0:
+            pair = (i + 1, r1, i, r0, f1)
+        if pair is not None:
+            di, dref, fi, fref, dfn = pair
+            d, f = dref._obj, fref._obj
+            if (d.dy == f.dy and d.dtype == L.BF16 and d.dy_xf.kind == L.X_BN_DY and f.dy_xf.kind == L.X_BN_DY
+                    and not d.bn_finalize and not f.split_k):
+                out[di] = (PAIR_FN, L.PairCall(dfn, dref, fref))
+                out[fi] = None
+                i += 2
+                continue
+        i += 1
+    return out
 
 
 # Weight-gradient calls: nothing later in the backward reads their output (only the optimizer),
@@ -983,7 +1022,7 @@ def size_workspaces(plan, call_lists):
     sized = []
     for calls in call_lists:
         for fn, ref in calls:
-            if fn == BATCH_FN:
+            if fn in (BATCH_FN, PAIR_FN):
                 arg = ref
                 b = ref.workspace_size()
             elif fn not in L.WS_QUERY:
@@ -1035,7 +1074,7 @@ def run_calls(plan, calls, stream):
 def call_one(fn, arg, stream):
     """One entry of a plan's call list (struct argument, scalar-argument tuple or a batch of
     weight-gradient calls) on `stream`."""
-    if fn == BATCH_FN:
+    if fn in (BATCH_FN, PAIR_FN):
         arg(stream)
     elif isinstance(arg, tuple):
         L.call(fn, *arg, stream)
