@@ -9,6 +9,8 @@
 // the prefix of block counts and runs that layer's body (vae_wgemm.hpp wgemm_body /
 // wgemm_taps_body) — every layer's planning (tile, K slices, slab) is exactly that of its own
 // call, so the results are those of the calls made one after another.
+#include <string.h>
+
 #include "vae_launch.hpp"
 #include "vae_wgrad.hpp"
 #include "vae_wgemm.hpp"
@@ -167,6 +169,11 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   // K-steps behind everything else; there the K slices are sized instead so that every workgroup
   // of the class runs about the same number of K-steps (the class's work over its tile count,
   // >= 16 steps of 32 pixels).
+  // VAE_WG_SHARE=steps: shares in proportion to tile-steps (output tiles x 32-pixel K-steps)
+  // instead of MACs.  Measured slower (VanillaVAE B=64: 0.5498 vs 0.5416 ms/step, the batch 102.8
+  // vs 94 us): the first conv's K-steps (8 of its 32 tile columns real) cost a quarter of its
+  // class-mates', so the MAC shares were the balanced ones.
+  static const bool share_macs = !(getenv("VAE_WG_SHARE") && !strcmp(getenv("VAE_WG_SHARE"), "steps"));
   for (int c = group_slots0 > 0 ? 0 : 1; c < kClasses; ++c) {
     const int gs = c == 0 ? group_slots0 : group_slots;
     double macs = 0.0;
@@ -187,6 +194,11 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       if (cls[i] != c) continue;
       const double m = (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
       long slots = (long)(gs * m / macs + 0.5);
+      if (!share_macs && work > 0) {
+        const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
+        const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;
+        slots = (long)((double)gs * (double)(tiles * ks) / (double)work + 0.5);
+      }
       if (balance) {
         const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
         const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;

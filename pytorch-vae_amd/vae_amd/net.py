@@ -982,8 +982,13 @@ def pair_calls(calls, lo, end):
     backward, same dy) as one vae_conv_bwd_pair call at the data call's position: on the bf16
     conv-GEMM paths its weight gradient runs in the data gradient's grid instead of in the
     segment's grouped batch.  Returns {raw index: (PAIR_FN, PairCall) at the data call's index,
-    None at the filter call's}.  VAE_PAIR=0 keeps the batch."""
-    if os.environ.get("VAE_PAIR", "1") == "0":
+    None at the filter call's}.  Off by default (VAE_PAIR=1 turns it on): measured slower — the
+    VanillaVAE step 0.660 vs 0.5435 ms/step (B=64, graph-replayed; profiles/r4_v2_pair_sweep.txt):
+    each layer's weight gradient alone in its pair grid took longer than its share of the grouped
+    batch (its slices add whole tiles into dW with atomics), the 64 x 32 data tiles lost a third of
+    their occupancy to the pair's register budget, and the first conv's weight gradient, left alone,
+    took 96 us."""
+    if os.environ.get("VAE_PAIR", "0") != "1":
         return {}
     out = {}
     i = lo

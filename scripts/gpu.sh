@@ -7,6 +7,7 @@
 #
 #   tests            pytest -m gpu (all GPU tests)
 #   tests:EXPR       pytest -m gpu -k EXPR
+#   tenv:V=x,W=y:EXPR  pytest -m gpu -k EXPR with environment overrides
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench line (driver's command: N=1, CPU baseline included)
 #   quick            VanillaVAE bench, 200 steps, no CPU baseline, per-call breakdown
@@ -64,7 +65,8 @@ pmc() {   # name bench-args...   (one counter group per run: rocprofv3 does not 
 for step in "$@"; do
   IFS=: read -r kind a1 a2 <<< "$step"
   case $kind in
-    tests) if [ -n "$a1" ]; then run tests 900 $PT -k "$a1"; else run tests 900 $PT; fi ;;
+    tests) if [ -n "$a1" ]; then run tests_${a1//[^A-Za-z0-9]/_} 900 $PT -k "$a1"; else run tests 900 $PT; fi ;;
+    tenv) run tenv_${a1//[=,]/_} 900 env ${a1//,/ } $PT -k "$a2" ;;
     smoke) run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 400 python3 -u bench.py ;;
     quick) run quick 300 python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --kernel-breakdown ;;
@@ -88,5 +90,9 @@ for step in "$@"; do
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
   rc=$?
+  # a test step whose tests failed (pytest rc 1) ends nothing: the process exited normally; any
+  # other failure (abort, fault, time limit) ends the job before the next GPU step
+  if [ $rc -eq 1 ] && { [ "$kind" = tests ] || [ "$kind" = tenv ]; }; then echo "step $step: test failures (rc=1), continuing" >&2; FAILED=1; continue; fi
   [ $rc -eq 0 ] || { echo "step $step failed rc=$rc" >&2; exit $rc; }
 done
+exit ${FAILED:-0}

@@ -44,9 +44,10 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("loss,batch,samples", [("vanilla", 64, 1), ("betaH", 32, 1), ("iwae", 64, 5)])
 def test_pair_backward_equals_unpaired_backward(loss, batch, samples):
-    """One forward, then the backward twice from it: with the pair calls (the plan's default list)
+    """One forward, then the backward twice from it: with the pair calls (VAE_PAIR=1's list)
     and with VAE_PAIR=0's list (every weight gradient in the grouped batch).  Both differ only in
-    fp32 accumulation order (atomics), so every dx and weight gradient agrees to within bf16 rounding flips (2e-3 relative norm)."""
+    fp32 accumulation order (atomics): each tensor must agree with the unpaired result as closely
+    as the unpaired backward run twice agrees with itself (3x that noise floor + 1e-3)."""
     from oracle import vae_oracle as O
     from vae_amd import _lib as L
     from vae_amd.engine import FusedAdam
@@ -55,7 +56,15 @@ def test_pair_backward_equals_unpaired_backward(loss, batch, samples):
     x, eps = O.make_inputs(batch, 128, 17, samples=samples if samples > 1 else None)
     net = VAENet(latent_dim=128, dtype=torch.bfloat16, device="cuda")
     net.load_reference_state_dict(sd)
-    plan = StepPlan(net, batch, loss=loss, kld_weight=2.5e-4, samples=samples)
+    old = os.environ.get("VAE_PAIR")
+    os.environ["VAE_PAIR"] = "1"
+    try:
+        plan = StepPlan(net, batch, loss=loss, kld_weight=2.5e-4, samples=samples)
+    finally:
+        if old is None:
+            del os.environ["VAE_PAIR"]
+        else:
+            os.environ["VAE_PAIR"] = old
     paired = list(plan.bwd_calls)
     keep = (plan.workspace, plan.workspace_side)            # the paired calls' workspaces
     old = os.environ.get("VAE_PAIR")
@@ -79,11 +88,22 @@ def test_pair_backward_equals_unpaired_backward(loss, batch, samples):
     lib = L.load()
     g1, dx1, names1 = _backward(plan, paired, lib, st)
     g0, dx0, names0 = _backward(plan, unpaired, lib, st)
+    g2, dx2, _ = _backward(plan, unpaired, lib, st)           # the same list again: the noise floor
     del keep
     assert "pair_kernel" in names1 and "pair_kernel" not in names0
-    for i, (a, b) in enumerate(zip(dx1, dx0)):
-        assert _rel(a, b) < 2e-3, (i, _rel(a, b))
-    bad = [(k, _rel(g1[k], ref)) for k, ref in g0.items() if not _rel(g1[k], ref) < 2e-3]
-    # (pre-BatchNorm conv biases: analytically zero, both sides ~1e-9 of noise)
-    bad = [(k, e) for k, e in bad if not (k.endswith(".0.bias") and float(g0[k].abs().max()) < 1e-5)]
+
+    def bar(floor):
+        return 3 * floor + 1e-3
+    # every dx of the data-gradient chain; the BatchNorm-backward sums (fp32 atomics) differ in
+    # order from run to run and the chain amplifies that through nine BatchNorms — the unpaired
+    # list run twice measures it
+    for i, (a, b, c) in enumerate(zip(dx1, dx0, dx2)):
+        assert _rel(a, b) <= bar(_rel(c, b)), (i, _rel(a, b), _rel(c, b))
+    bad = []
+    for k, ref in g0.items():
+        if k.endswith(".0.bias") and float(ref.abs().max()) < 1e-5:
+            continue                      # pre-BatchNorm conv biases: analytically zero (noise)
+        e, f = _rel(g1[k], ref), _rel(g2[k], ref)
+        if not e <= bar(f):
+            bad.append((k, e, f))
     assert not bad, bad
