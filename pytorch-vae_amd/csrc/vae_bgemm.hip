@@ -295,16 +295,26 @@ __device__ __forceinline__ int bw_sw(int row) { return ((row & 3) << 2) | ((row 
 
 // Transposed reads as inline asm: the wait-count pass gives the ds_read_tr intrinsic no LDS address
 // and makes it wait for every LDS-DMA in flight (vmcnt(0) at each K-step head, seen in the ISA);
-// asm reads are invisible to it, so their results are waited for explicitly — bw_wait passes the
-// fragments through the s_waitcnt so no consumer can be scheduled above it.
+// asm reads are invisible to it, so their results are waited for explicitly.  The wait must take
+// the asm's OWN output registers ("+v"): the compiler treats an asm output as ready when the asm
+// ends, so any instruction touching those registers — even the register moves that pack two
+// 4-element halves into an MFMA operand (v_bfi_b32 vN, s, vN, vN) — may otherwise be scheduled
+// before the wait and read or rewrite them while the LDS return is in flight.  Waiting on the packed
+// operands instead (this file's first version) let the packing moves race the returns: weight
+// gradients off by up to 40 % of their max (tests/test_gpu_bgemm.py test_bwg_weight_gradient).
 __device__ __forceinline__ wgm_bf16x4 bw_tr(uint32_t lds_addr) {
   wgm_bf16x4 r;
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr) : "memory");
   return r;
 }
-__device__ __forceinline__ void bw_wait(bf16x8 (&a)[4], bf16x8 (&b)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]), "+v"(b[1]),
-               "+v"(b[2]), "+v"(b[3])::"memory");
+__device__ __forceinline__ void bw_wait(wgm_bf16x4 (&a)[4][2], wgm_bf16x4 (&b)[4][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]), "+v"(a[2][1]),
+                 "+v"(a[3][0]), "+v"(a[3][1]), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]),
+                 "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[3][0]), "+v"(b[3][1])::"memory");
+}
+__device__ __forceinline__ bf16x8 bw_cat(wgm_bf16x4 lo, wgm_bf16x4 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
 __global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
@@ -399,32 +409,31 @@ __global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
     __builtin_amdgcn_s_barrier();                           // ... and every wave's
     const uint32_t lu = (uint32_t)(uintptr_t)smem + buf * BW_STAGE;
     const uint32_t lv = lu + BW_TILE;
-    bf16x8 af[2][4], bfr[2][4];
-    auto rd = [&](int kk, bf16x8 (&a)[4], bf16x8 (&b)[4]) {
+    wgm_bf16x4 ra[2][4][2], rb[2][4][2];                  // raw read results [kk][fragment][half]
+    auto rd = [&](int kk) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
-        const wgm_bf16x4 a0 = bw_tr(lu + kk * 32 * 256 + aoff[f][0]);
-        const wgm_bf16x4 a1 = bw_tr(lu + kk * 32 * 256 + aoff[f][1]);
-        const wgm_bf16x4 b0 = bw_tr(lv + kk * 32 * 256 + boff[f][0]);
-        const wgm_bf16x4 b1 = bw_tr(lv + kk * 32 * 256 + boff[f][1]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[f][e] = a0[e]; a[f][4 + e] = a1[e];
-          b[f][e] = b0[e]; b[f][4 + e] = b1[e];
-        }
+        ra[kk][f][0] = bw_tr(lu + kk * 32 * 256 + aoff[f][0]);
+        ra[kk][f][1] = bw_tr(lu + kk * 32 * 256 + aoff[f][1]);
+        rb[kk][f][0] = bw_tr(lv + kk * 32 * 256 + boff[f][0]);
+        rb[kk][f][1] = bw_tr(lv + kk * 32 * 256 + boff[f][1]);
       }
     };
-    rd(0, af[0], bfr[0]);
-    bw_wait(af[0], bfr[0]);
-    rd(1, af[1], bfr[1]);                                   // in flight behind the first 16 MFMAs
+    auto mma = [&](int kk) {                               // (after bw_wait(ra[kk], rb[kk]))
+      bf16x8 af[4], bfr[4];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (kk == 1) bw_wait(af[1], bfr[1]);
+      for (int f = 0; f < 4; ++f) { af[f] = bw_cat(ra[kk][f][0], ra[kk][f][1]); bfr[f] = bw_cat(rb[kk][f][0], rb[kk][f][1]); }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+    rd(0);
+    bw_wait(ra[0], rb[0]);
+    rd(1);                                                  // in flight behind the first 16 MFMAs
+    mma(0);
+    bw_wait(ra[1], rb[1]);
+    mma(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();                           // every wave is done reading `buf`
   }
@@ -478,7 +487,6 @@ bool bgemm_ok(const GemmParams& p, int am, int em) {
   if (p.a_xf.kind != VAE_X_NONE || p.g_nchw || p.ones_col >= 0 || p.residual || p.out_f32) return false;
   if (p.gc % BG_K || p.N % BG_N || p.out_ld % 8 || p.b_ld % 8) return false;
   if (((uintptr_t)p.a_ptr | (uintptr_t)p.b_ptr | (uintptr_t)p.out) & 15) return false;
-  if (em == E_STORE && p.sum && (p.sum_reps < 1)) return false;
   if (em == E_BNBWD && p.epi_xf.kind != VAE_X_NONE && (((uintptr_t)p.epi_xf.aux & 15) || p.epi_xf.channels % 8)) return false;
   int kmax = p.K;
   if (am == A_CONVT) {

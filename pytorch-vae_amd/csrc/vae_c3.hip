@@ -770,46 +770,51 @@ __global__ void __launch_bounds__(W3_NT) c3wd_kernel(const W3Params p) {
   }
   auto compute = [&](uint32_t Us) {
     const uint32_t Vs = Us + W3D_UROWS * W3_URS;
-    auto afrag = [&](int kb, bf16x8 (&af)[2]) {
+    // raw read results, consumed only after a wait that takes these very registers (vae_bgemm.hip
+    // bw_tr: waiting on packed copies let the packing moves race the LDS returns)
+    w3_bf16x4 ra[2][2], rb[3][2][2];                      // A [i][half]; B [step buffer][cb][half]
+    auto afrag = [&](int kb) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const w3_bf16x4 a0 = w3d_tr(Us + kb * 32 * W3_URS + aoff[i][0]);
-        const w3_bf16x4 a1 = w3d_tr(Us + kb * 32 * W3_URS + aoff[i][1]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { af[i][e] = a0[e]; af[i][4 + e] = a1[e]; }
+        ra[i][0] = w3d_tr(Us + kb * 32 * W3_URS + aoff[i][0]);
+        ra[i][1] = w3d_tr(Us + kb * 32 * W3_URS + aoff[i][1]);
       }
     };
-    auto bfrag = [&](int kb, int s, bf16x8 (&bfr)[2]) {
+    auto bfrag = [&](int kb, int s, w3_bf16x4 (&r)[2][2]) {
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int P0 = prow[0] + kb * 2 * C3_PW + s, P1 = prow[1] + kb * 2 * C3_PW + s;
-        const w3_bf16x4 b0 = w3d_tr(Vs + w3_vsw(P0, cb) + 8 * p4);
-        const w3_bf16x4 b1 = w3d_tr(Vs + w3_vsw(P1, cb) + 8 * p4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { bfr[cb][e] = b0[e]; bfr[cb][4 + e] = b1[e]; }
+        r[cb][0] = w3d_tr(Vs + w3_vsw(P0, cb) + 8 * p4);
+        r[cb][1] = w3d_tr(Vs + w3_vsw(P1, cb) + 8 * p4);
       }
     };
-    bf16x8 af[2], bfr[2][2];
-    bfrag(0, 0, bfr[0]);
+    bfrag(0, 0, rb[0]);
 #pragma unroll 1
     for (int kb = 0; kb < 4; ++kb) {
-      afrag(kb, af);
+      afrag(kb);
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
-        // this step's fragments have landed (passed through the wait: no consumer above it)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bfr[s & 1][0]), "+v"(bfr[s & 1][1])::"memory");
-        bfrag(s < 2 ? kb : min(kb + 1, 3), s < 2 ? s + 1 : 0, bfr[(s + 1) & 1]);
-        if constexpr (VACT) {
+        // this step's fragments have landed (the wait takes the raw registers: no consumer above it)
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(ra[0][0]), "+v"(ra[0][1]), "+v"(ra[1][0]), "+v"(ra[1][1]), "+v"(rb[s][0][0]),
+                       "+v"(rb[s][0][1]), "+v"(rb[s][1][0]), "+v"(rb[s][1][1])::"memory");
+        // the next step's B fragments: steps 0, 1, 2 of a kb use buffers 0, 1, 2 (the next kb's
+        // step 0 goes to buffer 0, whose step is done)
+        bfrag(s < 2 ? kb : min(kb + 1, 3), s < 2 ? s + 1 : 0, rb[(s + 1) % 3]);
+        bf16x8 af[2], bfr[2];
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) bfr[s & 1][cb] = lrelu8(bfr[s & 1][cb], p.v_slope);
+        for (int i = 0; i < 2; ++i) af[i] = __builtin_shufflevector(ra[i][0], ra[i][1], 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          bfr[cb] = __builtin_shufflevector(rb[s][cb][0], rb[s][cb][1], 0, 1, 2, 3, 4, 5, 6, 7);
+          if constexpr (VACT) bfr[cb] = lrelu8(bfr[cb], p.v_slope);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb)
-            acc[i][cb][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[s & 1][cb], acc[i][cb][s], 0, 0, 0);
+            acc[i][cb][s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[cb], acc[i][cb][s], 0, 0, 0);
       }
-      bfr[0][0] = bfr[1][0]; bfr[0][1] = bfr[1][1];
     }
   };
 
@@ -1043,7 +1048,12 @@ int c3_launch(const C3Args& a, hipStream_t st) {
   const unsigned grid = (unsigned)(a.n * (a.N / bn));
   // VAE_C3_V1=1: the register-staged whole-chunk kernel (A/B timing)
   static const bool v1 = getenv("VAE_C3_V1") != nullptr;
-  if (bn == 128 && !v1 && a.C % 32 == 0) {
+  // An activated input (LeakyReLU of the stored tensor) stays on the register-staged kernel, which
+  // applies it once per element as it stages the patch: c3d_kernel<1> applies it to the A fragments
+  // (once per element and tap, VALU-bound) — 66-71 vs 35 us per call at B=128
+  // (profiles/r4_v3_vq_breakdown.txt); VAE_C3D_ACT=1 keeps it (A/B timing)
+  static const bool d_act = getenv("VAE_C3D_ACT") != nullptr;
+  if (bn == 128 && !v1 && a.C % 32 == 0 && (!a.a_act || d_act)) {
     if (a.a_act) VAE_LAUNCH(c3d_kernel<1>, dim3(grid), dim3(512), 0, st, p);
     else VAE_LAUNCH(c3d_kernel<0>, dim3(grid), dim3(512), 0, st, p);
   } else if (bn == 128) VAE_LAUNCH(c3_kernel<128>, dim3(grid), dim3(512), 0, st, p);
@@ -1081,7 +1091,10 @@ int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st) {
   p.n = a.n; p.M = a.M; p.J = a.J;
   const unsigned grid = (unsigned)(groups * (a.M / W3_BM) * (a.J / W3_BC));
   static const bool v1 = getenv("VAE_C3_V1") != nullptr;
-  if (v1) VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
+  // (an activated V operand: the register-staged kernel, as c3_launch — c3wd_kernel<1> took
+  // 114-131 vs 50 us per call; VAE_C3D_ACT=1 keeps it)
+  static const bool d_act = getenv("VAE_C3D_ACT") != nullptr;
+  if (v1 || (a.v_act && !d_act)) VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
   else if (a.v_act) VAE_LAUNCH(c3wd_kernel<1>, dim3(grid), dim3(W3_NT), 0, st, p);
   else VAE_LAUNCH(c3wd_kernel<0>, dim3(grid), dim3(W3_NT), 0, st, p);
   if (int rc = check_launch("c3w")) return rc;

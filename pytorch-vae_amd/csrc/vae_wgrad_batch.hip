@@ -67,6 +67,33 @@ wg_group_kernel(const WgGroup g) {
   }
 }
 
+// The 64 x 64 and 128 x 128 classes in ONE grid (per layer: var[i] = 4 * (tile == 128) + variant):
+// launched one after the other, each class ran a round of one workgroup per CU on its own (the
+// VanillaVAE's 25 + 30 us, profiles/r4_v1_kstats.json); in one grid they share the round.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wg_group_mixed_kernel(const WgGroup g) {
+  __shared__ __attribute__((aligned(16))) char lds[wgemm_lds_bytes<128, 128>()];
+  (void)g;
+  const WgGroup* gk = (const WgGroup*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = (int)blockIdx.x;
+  const int n = gk->n;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < kWgGroupMax; ++j) i = (j < n && b >= gk->start[j]) ? j : i;
+  i = __builtin_amdgcn_readfirstlane(i);
+  const int bid = b - gk->start[i];
+  const WgParams& p = gk->p[i];
+  switch (gk->var[i]) {
+    case 0: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
+    case 1: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds); break;
+    case 2: wgemm_body<64, 64, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds); break;
+    case 3: wgemm_body<64, 64, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds); break;
+    case 4: wgemm_body<128, 128, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
+    case 5: wgemm_body<128, 128, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds); break;
+    case 6: wgemm_body<128, 128, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds); break;
+    default: wgemm_body<128, 128, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds); break;
+  }
+}
+
 // group classes: 0 = 32 x 32 tiles with all 3x3 taps per workgroup, 1 = 64 x 64, 2 = 128 x 128
 constexpr int kClasses = 3;
 inline int wg_class(const WgPlan& w) {
@@ -213,17 +240,23 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       if (wg_class(plans[i]) != c) return fail(VAE_E_UNSUPPORTED, "conv_bwd_filter_batch: replanned class");
     }
   }
-  // one launch per tile class (chunks of kWgGroupMax layers)
+  // one launch per tile class (chunks of kWgGroupMax layers); classes 1 and 2 in one grid when
+  // their layers fit one group (VAE_WG_MIXED=0: a launch each)
+  static const bool mixed_ok = !(getenv("VAE_WG_MIXED") && !strcmp(getenv("VAE_WG_MIXED"), "0"));
+  int n12 = 0;
+  for (int i = 0; i < n; ++i) n12 += (cls[i] == 1 || cls[i] == 2) ? 1 : 0;
+  const bool mixed = mixed_ok && n12 <= kWgGroupMax && n12 > 0;
   for (int c = 0; c < kClasses; ++c) {
+    if (mixed && c == 2) continue;                       // (launched with class 1)
     WgGroup g;
     memset(&g, 0, sizeof(g));
     size_t lds = 0;
     for (int i = 0; i <= n; ++i) {
-      const bool take = i < n && cls[i] == c;
+      const bool take = i < n && (cls[i] == c || (mixed && c == 1 && cls[i] == 2));
       if (take) {
         const WgPlan& w = plans[i];
         g.p[g.n] = w.p;
-        g.var[g.n] = wg_variant(w.p);
+        g.var[g.n] = wg_variant(w.p) + (mixed && cls[i] == 2 ? 4 : 0);
         g.start[g.n + 1] = g.start[g.n] + (int)w.blocks;
         g.n++;
         const bool bu = w.p.u_xf.kind == VAE_X_BN_ACT || w.p.u_xf.kind == VAE_X_BN_DY;
@@ -233,7 +266,12 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
         lds = l > lds ? l : lds;
       }
       if (g.n > 0 && (g.n == kWgGroupMax || i == n)) {
-        if (int rc = group_launch(c, g, lds, st)) return rc;
+        if (mixed && c == 1) {
+          VAE_LAUNCH(wg_group_mixed_kernel, dim3((unsigned)g.start[g.n]), dim3(256), lds, st, g);
+          if (int rc = check_launch("wg_group_mixed")) return rc;
+        } else if (int rc = group_launch(c, g, lds, st)) {
+          return rc;
+        }
         memset(&g, 0, sizeof(g));
         lds = 0;
       }

@@ -127,6 +127,9 @@ WGRAD_B = [  # transposed, N, cin, cout, hw (input grid), stride, R, pad
     (True, 64, 512, 256, 8, 2, 3, 1),       # big_ae decoder ConvT
     (False, 64, 128, 256, 32, 2, 4, 1),     # VQ-VAE encoder.1 (k4 s2)
     (True, 64, 256, 128, 16, 2, 4, 1),      # VQ-VAE decoder ConvT(256 -> 128)
+    (True, 64, 256, 128, 16, 2, 3, 1),      # big_ae decoder.3 (16384 pixels, 26 K slices)
+    (True, 64, 128, 128, 32, 2, 3, 1),      # big_ae final ConvT (65536 pixels, 54 K slices)
+    (True, 16, 128, 128, 32, 2, 3, 1),      # the same at B=16 (tests/test_gpu_ae_wide.py)
 ]
 
 
