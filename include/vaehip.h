@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 20
+#define VAE_ABI_VERSION 21
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -93,6 +93,12 @@ typedef struct vae_xform {
    * When set, consumers load it instead of reducing the statistics themselves, and running
    * statistics / dgamma_out / dbeta_out are left to vae_bn_finalize. */
   const float* table;
+  /* BN_ACT, training: the consumer that updates the running statistics (the forward's first
+   * consumer of the BatchNorm, its first workgroup) also writes the BN_ACT table it built here,
+   * planar [4][C] as above — the backward's later consumers of the same statistics (activation-
+   * backward epilogues, weight-gradient operands) then take it as `table` instead of reducing the
+   * replicated statistics again in every workgroup.  NULL: not written. */
+  float* table_out;
 } vae_xform;
 
 /* One BatchNorm's per-step finalisation, run once between the kernel that produces its

@@ -326,7 +326,17 @@ wgemm_kernel(const WgParams p) {
 // transformed once and reused by every tap (per-tap workgroups did it R*R times), V is gathered
 // per tap from the pixel decomposition computed once per row.  Accumulators: R*R x the
 // (BM/2 x BJ/2) wave tile.
-template <int LOADS> constexpr int wgt_stages() { return LOADS > 10 ? 1 : wg_stages<LOADS>(); }
+// Stages in flight: one for the all-taps kernels above 10 loads a stage.  Two (the VAE_WGT_NS2
+// build: 256 VGPRs + 68 AGPRs, one workgroup per CU, which the grouped launch holds anyway) measured
+// no faster: VanillaVAE B=64 0.5395 vs 0.5337 ms/step (profiles/r4_v4_notes.txt); the 4x4
+// kernels spilled 33-39 VGPRs at two.
+template <int LOADS, int RR> constexpr int wgt_stages() {
+#ifdef VAE_WGT_NS2
+  return LOADS > 20 || (RR > 3 && LOADS > 10) ? 1 : (LOADS > 10 ? 2 : wg_stages<LOADS>());
+#else
+  return LOADS > 10 ? 1 : wg_stages<LOADS>();
+#endif
+}
 
 // K-step: every thread loads one 16-byte chunk of U and of each tap's V row — 64 pixels for the
 // 32-channel tiles (128 of the 256 threads idled at 32) — and the LDS holds one step (single
@@ -353,7 +363,7 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
   constexpr bool DU = XU == VAE_X_BN_DY, DV = XV == VAE_X_BN_DY;
   constexpr bool BU = XU == VAE_X_BN_ACT || DU, BV = XV == VAE_X_BN_ACT || DV;
   constexpr int LOADS = UPT * (DU ? 2 : 1) + TAPS * VPT * (DV ? 2 : 1);
-  constexpr int NS = wgt_stages<LOADS>();
+  constexpr int NS = wgt_stages<LOADS, RR>();
   constexpr int WTM = BM / 2, WTJ = BJ / 2;
   constexpr int TM = WTM / 16, TJ = WTJ / 16;
 

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
 if os.environ.get("VAE_HIP_LIB") == "probe":
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -36,7 +36,7 @@ class Xform(ctypes.Structure):
                 ("beta", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("aux", c_void_p),
                 ("running_mean", c_void_p), ("running_var", c_void_p),
                 ("reps", c_int32), ("rstride", c_int32), ("dgamma_out", c_void_p), ("dbeta_out", c_void_p),
-                ("table", c_void_p)]
+                ("table", c_void_p), ("table_out", c_void_p)]
 
 
 class BnArgs(ctypes.Structure):

@@ -155,6 +155,11 @@ class StepPlan:
         # the weight-gradient call's first workgroup writes dL/dgamma, dL/dbeta and the conv
         # bias gradient (closed form).  Eval mode keeps vae_bn_finalize (running statistics).
         self.bn_in_consumer = bn_in_consumer and training
+        # persist_tables (VAE_PERSIST=1, off by default): the forward's BN_ACT tables written once
+        # (vae_xform.table_out) and loaded by the backward's consumers of the same statistics.
+        # Measured slower (VanillaVAE B=64 0.5724 vs 0.5395 ms/step) and, in the fp32 parity mode,
+        # off against the oracle (encoder gradients) — kept as an experiment, not on the path
+        self.persist_tables = os.environ.get("VAE_PERSIST") == "1"
         self.S = samples if loss == "iwae" else 1
         self.loss_kind = {"vanilla": L.LOSS_VANILLA, "betaH": L.LOSS_BETA_H, "betaB": L.LOSS_BETA_B,
                           "iwae": L.LOSS_IWAE}[loss]
@@ -332,6 +337,15 @@ class StepPlan:
         if table:
             t = self.bntab[prefix]
             xf.table = t.data_ptr() + (4 * 4 * C if kind == L.X_BN_DY else 0)
+        elif kind == L.X_BN_ACT and self.bn_in_consumer and self.persist_tables:
+            # the forward's consumer of this BatchNorm (the one updating the running statistics)
+            # writes the table it builds; every later BN_ACT use of the step (the backward's
+            # activation-backward epilogues and weight-gradient operands) loads it instead of
+            # reducing the replicated statistics again (vaehip.h vae_xform.table_out)
+            if running:
+                xf.table_out = self.bntab[prefix].data_ptr()
+            else:
+                xf.table = self.bntab[prefix].data_ptr()
         if aux is not None:
             xf.aux = aux.data_ptr()
         if running:

@@ -44,7 +44,9 @@ def test_rgb_out_fwd_recon_matches_torch(n):
     w = _bf(torch.randn(128, 3, 4, 4, generator=g) * 0.05)           # ConvTranspose2d [Ci][Co][R][S]
     b = torch.randn(3, generator=g) * 0.1
     tgt = torch.rand(n, 3, 64, 64, generator=g)
-    y = F.conv_transpose2d(F.leaky_relu(x, SLOPE), w, b, stride=2, padding=1)
+    # the kernel's MFMA operand is the activation rounded to bf16 (the reference contract of a bf16
+    # operand); unrounded, the negative side's 0.01 x carries ~2e-5 of rounding into y
+    y = F.conv_transpose2d(_bf(F.leaky_relu(x, SLOPE)), w, b, stride=2, padding=1)
     yr = y.clone().requires_grad_(True)
     r = torch.tanh(yr)
     F.mse_loss(r, tgt).backward()
