@@ -90,7 +90,7 @@ def test_rgb_out_bwd_matches_torch(n):
     x_pre = _bf(torch.randn(n, 128, 32, 32, generator=g))
     w = _bf(torch.randn(128, 3, 4, 4, generator=g) * 0.05)
     dy = _bf(torch.randn(n, 3, 64, 64, generator=g))
-    xa = F.leaky_relu(x_pre, SLOPE).requires_grad_(True)
+    xa = _bf(F.leaky_relu(x_pre, SLOPE)).requires_grad_(True)      # (the bf16 operand the kernel reads)
     wr = w.clone().requires_grad_(True)
     br = torch.zeros(3, requires_grad=True)
     (F.conv_transpose2d(xa, wr, br, stride=2, padding=1) * dy).sum().backward()
