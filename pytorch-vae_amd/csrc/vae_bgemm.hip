@@ -35,9 +35,23 @@ namespace {
 constexpr int BG_M = 128, BG_N = 128, BG_K = 64, BG_T = 256;
 constexpr int BG_TILE = BG_M * BG_K * 2;              // bytes of one operand tile (16 KB)
 constexpr int BG_STAGE = 2 * BG_TILE;                 // A + B
-constexpr int BG_OPS = 2 * BG_STAGE;                  // two stages (64 KB)
+// A ring of NSTG stages with NSTG - 1 K-steps in flight: NSTG = 2 at two workgroups per CU (64 KB
+// each) when the tiles fill two rounds of CUs, NSTG = 4 at one per CU (128 KB) when they do not —
+// there one workgroup with three steps in flight replaces a split-K pair and its slab + finalize
+// (big_ae encoder.1: 49.6 -> 23.3 us), while grids of thousands of tiles keep the two-workgroup
+// form (its final ConvT: 59 vs 84 us at NSTG = 4; profiles/r4_v4_notes.txt).
+template <int NSTG> constexpr int bg_ops() { return NSTG * BG_STAGE; }
 constexpr int BG_LDC = BG_N + 4;                      // fp32 epilogue rows (one 64-row half at a time)
-static_assert(64 * BG_LDC * 4 <= BG_OPS, "epilogue half-tile fits the operand buffers");
+constexpr int BG_EPI = (64 * BG_LDC * 4 + 255) / 256 * 256;   // the epilogue's half-tile; its tables follow
+static_assert(BG_EPI <= bg_ops<2>(), "epilogue half-tile fits the operand buffers");
+
+// this wave's loads of the current step landed, `newer` later steps (8 LDS-DMA each) left in flight
+__device__ __forceinline__ void bg_wait_newer(int newer) {
+  if (newer >= 3) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (newer == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (newer == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 
 // One 16-byte-per-lane LDS-DMA (buffer_load_dwordx4 ... lds: lane l's 16 bytes land at M0 + 16 l).
 // (The compiler's wait-count pass leaves the K-step in flight across the loop's ds_reads here —
@@ -49,8 +63,9 @@ __device__ __forceinline__ void glds16(rsrc_t r, const char* lds_wave_base, uint
 
 __device__ __forceinline__ int bg_slot(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-template <int AM, int EM>
-__global__ void __launch_bounds__(BG_T, 2) bgemm_kernel(const GemmParams p) {
+template <int AM, int EM, int NSTG>
+__global__ void __launch_bounds__(BG_T, NSTG >= 4 ? 1 : 2) bgemm_kernel(const GemmParams p) {
+  static_assert(NSTG >= 2 && NSTG <= 4, "bg_wait_newer counts up to three steps in flight");
   extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object (see header)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -122,15 +137,16 @@ __global__ void __launch_bounds__(BG_T, 2) bgemm_kernel(const GemmParams p) {
       boffs[i][k2] = rb_ * 128 + bg_slot(rb_, c) * 16;
     }
 
-  if (kt0 < kt1) issue(kt0, 0);
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    if (kt + 1 < kt1) {
-      issue(kt + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // this wave's loads of step kt landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+  // ring: steps kt0 .. kt0 + NSTG - 2 requested up front; step i's refill goes into the slot step
+  // i - 1 used (released by that step's closing barrier); 8 LDS-DMA per wave per step
+  const int nk = kt1 - kt0;
+#pragma unroll
+  for (int u = 0; u < NSTG - 1; ++u)
+    if (u < nk) issue(kt0 + u, u);
+  for (int i = 0; i < nk; ++i) {
+    const int buf = i % NSTG;
+    if (i + NSTG - 1 < nk) issue(kt0 + i + NSTG - 1, (i + NSTG - 1) % NSTG);
+    bg_wait_newer(min(NSTG - 1, nk - 1 - i));              // this wave's loads of step i landed
     __builtin_amdgcn_s_barrier();                           // ... and every wave's
     const char* la = smem + buf * BG_STAGE;
     const char* lb = la + BG_TILE;
@@ -154,7 +170,7 @@ __global__ void __launch_bounds__(BG_T, 2) bgemm_kernel(const GemmParams p) {
   float* Cs = reinterpret_cast<float*>(smem);              // [64][BG_LDC]
   // per-channel tables of the epilogue transform (E_BNBWD with a BatchNorm+LeakyReLU), after the
   // operand area; scratch for their in-kernel build on the operand area (free by now)
-  float* tq = reinterpret_cast<float*>(smem + BG_OPS);
+  float* tq = reinterpret_cast<float*>(smem + BG_EPI);
   const int ce = tab_stride(p.epi_xf.channels);
   const Tab te{tq, tq + ce, nullptr, tq + 2 * ce, tq + 3 * ce};
   if constexpr (EM == E_BNBWD) {
@@ -289,7 +305,7 @@ __global__ void __launch_bounds__(BG_T, 2) bgemm_kernel(const GemmParams p) {
 constexpr int BW_KP = 64;
 constexpr int BW_TILE = BW_KP * 256;                  // 16 KB: 64 pixel rows x 128 channels
 constexpr int BW_STAGE = 2 * BW_TILE;
-constexpr int BW_OPS = 2 * BW_STAGE;                  // two stages (64 KB)
+template <int NSTG> constexpr int bw_ops() { return NSTG * BW_STAGE; }   // (bgemm's ring choice)
 
 __device__ __forceinline__ int bw_sw(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
@@ -317,7 +333,9 @@ __device__ __forceinline__ bf16x8 bw_cat(wgm_bf16x4 lo, wgm_bf16x4 hi) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-__global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
+template <int NSTG>
+__global__ void __launch_bounds__(BG_T, NSTG >= 4 ? 1 : 2) bwg_kernel(const WgParams p) {
+  static_assert(NSTG >= 2 && NSTG <= 4, "bg_wait_newer counts up to three steps in flight");
   extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -397,15 +415,13 @@ __global__ void __launch_bounds__(BG_T, 2) bwg_kernel(const WgParams p) {
     }
   }
 
-  if (nsteps > 0) issue(0, 0);
+#pragma unroll
+  for (int u = 0; u < NSTG - 1; ++u)
+    if (u < nsteps) issue(u, u);
   for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nsteps) {
-      issue(st + 1, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // this wave's loads of step st landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    const int buf = st % NSTG;
+    if (st + NSTG - 1 < nsteps) issue(st + NSTG - 1, (st + NSTG - 1) % NSTG);
+    bg_wait_newer(min(NSTG - 1, nsteps - 1 - st));         // this wave's loads of step st landed
     __builtin_amdgcn_s_barrier();                           // ... and every wave's
     const uint32_t lu = (uint32_t)(uintptr_t)smem + buf * BW_STAGE;
     const uint32_t lv = lu + BW_TILE;
@@ -453,9 +469,13 @@ int bgemm_go(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
   }
   const int ktiles = kmax / BG_K;
   const long tiles = (long)((p.M + BG_M - 1) / BG_M) * (p.N / BG_N) * p.nphase;
-  // split K until the tiles fill the CUs (two workgroups each), >= 4 K-steps per slice
+  // ring depth (bg_ops): two stages at two workgroups per CU for grids of >= two rounds of CUs,
+  // else four stages at one per CU, K split until the tiles cover the CUs (>= 4 K-steps a slice)
+  // (VAE_BG_NSTG=2/4 forces one)
+  static const int nstg_env = tune_env("VAE_BG_NSTG", 0);
+  const int nstg = nstg_env == 2 || nstg_env == 4 ? nstg_env : (tiles >= 2l * kCUs ? 2 : 4);
+  const int wgpercu = nstg == 2 ? 2 : 1;
   int split = 1;
-  static const int wgpercu = tune_env("VAE_BG_WGPERCU", 2);
   if (tiles < (long)wgpercu * kCUs) {
     split = (int)(((long)wgpercu * kCUs) / tiles);
     if (split > ktiles / 4) split = ktiles / 4;
@@ -467,10 +487,13 @@ int bgemm_go(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
   }
   p.ksplit = split;
   p.slab = split > 1 ? static_cast<float*>(ws) : nullptr;
-  const size_t lds = (size_t)BG_OPS + (EM == E_BNBWD ? (size_t)tab_floats(p.epi_xf, true) * 4 : 0);
+  const size_t lt = (size_t)BG_EPI + (EM == E_BNBWD ? (size_t)tab_floats(p.epi_xf, true) * 4 : 0);
+  const size_t ops = (size_t)(nstg == 2 ? bg_ops<2>() : bg_ops<4>());
+  const size_t lds = lt > ops ? lt : ops;
   if (lds > (size_t)kLdsBytes) return kHeadFallback;
   const unsigned nb = (unsigned)(tiles * split);
-  VAE_LAUNCH((bgemm_kernel<AM, EM>), dim3(nb), dim3(BG_T), lds, st, p);
+  if (nstg == 2) VAE_LAUNCH((bgemm_kernel<AM, EM, 2>), dim3(nb), dim3(BG_T), lds, st, p);
+  else VAE_LAUNCH((bgemm_kernel<AM, EM, 4>), dim3(nb), dim3(BG_T), lds, st, p);
   if (int rc = check_launch("bgemm")) return rc;
   if (p.slab) return launch_finalize<__bf16, EM>(p, st);
   return VAE_OK;
@@ -529,8 +552,13 @@ int bwg_launch(WgParams p, hipStream_t st) {
   p.v_bytes = (uint32_t)((long)p.n * p.hv * p.wv * p.J * 2);
   const long tiles = (long)(p.M / 128) * (p.J / 128) * p.R * p.R;
   const long ksteps = (npix + BW_KP - 1) / BW_KP;
-  // K slices: one round of two workgroups per CU (floor: no overflow round), >= 8 K-steps each
-  static const int wgpercu = tune_env("VAE_BWG_WGPERCU", 2);
+  // two stages at two workgroups per CU, K slices: one round of workgroups (floor: no overflow
+  // round), >= 8 K-steps each.  (Four stages at one per CU, VAE_BWG_NSTG=4, halves the slices the
+  // small-tile layers split into and measured slower: VQ-VAE encoder.1 72.6 -> 88.7 us, big_ae's
+  // weight-gradient batch 486 -> 512 us.)
+  static const int nstg_env = tune_env("VAE_BWG_NSTG", 0);
+  const int nstg = nstg_env == 4 ? 4 : 2;
+  const int wgpercu = nstg == 2 ? 2 : 1;
   static const int mink = tune_env("VAE_BWG_MINK", 8);
   const long slots = (long)wgpercu * kCUs;
   long split = slots / tiles;
@@ -542,7 +570,8 @@ int bwg_launch(WgParams p, hipStream_t st) {
   p.slab_ld = 0;
   p.own = split == 1 ? 1 : 0;
   p.jst = 0;
-  VAE_LAUNCH(bwg_kernel, dim3((unsigned)(tiles * split)), dim3(BG_T), BW_OPS, st, p);
+  if (nstg == 2) VAE_LAUNCH(bwg_kernel<2>, dim3((unsigned)(tiles * split)), dim3(BG_T), bw_ops<2>(), st, p);
+  else VAE_LAUNCH(bwg_kernel<4>, dim3((unsigned)(tiles * split)), dim3(BG_T), bw_ops<4>(), st, p);
   return check_launch("bwg");
 }
 

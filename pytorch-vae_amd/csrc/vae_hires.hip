@@ -523,7 +523,8 @@ int hires_convT_bwd_launch(const vae_conv_args* a, hipStream_t st) {
     return kHeadFallback;
   if (a->x_xf.kind == VAE_X_BN_ACT && (a->x_xf.table || !bn_fast_ok(a->x_xf))) return kHeadFallback;
   const int tiles = a->n * (HIN / IR);
-  const int grid = tiles < kHiresBwdGrid ? tiles : kHiresBwdGrid;
+  static const int gmax = tune_env("VAE_HIRES_GRID", kHiresBwdGrid);     // (sweeps)
+  const int grid = tiles < gmax ? tiles : gmax;
   const long need = (long)grid * NW * 4;
   if (!a->workspace && !querying()) return kHeadFallback;
   if (!ws_fits(need, a->workspace_bytes, "convT2d_bwd filter partials")) return VAE_E_BADARG;
