@@ -156,7 +156,11 @@ __device__ __forceinline__ void cgemm_body(const GemmParams& p, const int bid, c
   // workgroup b runs on XCD b % 8 (speed only, never correctness).  Each XCD takes a contiguous
   // range of tiles ordered n (column tile) fastest, then phase / K slice, then m: the output
   // rows of one XCD gather overlapping input rows (3x3 taps, the phases of a transposed conv,
-  // every column tile) that its own L2 then serves, instead of the Infinity Cache.
+  // every column tile) that its own L2 then serves, instead of the Infinity Cache.  Layers whose
+  // weights outweigh the gathered input (the deep 256-512-channel layers: 2.4 MB of weights
+  // against 0.3-1 MB of activations) order m fastest instead (p.m_fast), so an XCD fetches only its
+  // own weight columns (the n-fastest order fetched every column on all 8: 19.9 MB of traffic for
+  // a 3.2 MB layer, r4_v5_pmc.json).
   const int gm = (p.M + BM - 1) / BM, gn = (p.N + BN - 1) / BN, gz = p.nphase * p.ksplit;
   int tile;
   {
@@ -164,7 +168,9 @@ __device__ __forceinline__ void cgemm_body(const GemmParams& p, const int bid, c
     const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
     tile = x * q + min(x, r) + loc;
   }
-  const int tn = tile % gn, tz = (tile / gn) % gz, tmi = tile / (gn * gz);
+  int tn, tz, tmi;
+  if (p.m_fast) { tmi = tile % gm; tz = (tile / gm) % gz; tn = tile / (gm * gz); }
+  else { tn = tile % gn; tz = (tile / gn) % gz; tmi = tile / (gn * gz); }
   const int m0 = tmi * BM, n0 = tn * BN;
   const int phase = (p.nphase > 1) ? (int)(tz / p.ksplit) : 0;
   const int ks = tz - phase * p.ksplit;

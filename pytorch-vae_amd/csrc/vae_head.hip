@@ -1,23 +1,30 @@
-// Decoder head on MFMA (bf16 throughput mode): final_layer Conv2d(32->3, k3, s1, p1) + Tanh
-// (models/vanilla_vae.py:73-75), the reconstruction SSE of the ELBO (:140) and their backward.
+// Decoder head on MFMA (bf16 throughput mode): final_layer Conv2d(C->3, k3, s1, p1) + Tanh
+// (models/vanilla_vae.py:73-75, models/autoencoder.py:84-86), the reconstruction SSE of the ELBO
+// (vanilla_vae.py:140) and their backward, for C = 32 (the VAEs), 64 and 128 (the Autoencoder's
+// big_ae final layer, configs/big_ae.yaml).
 //
 // The layer has 3 output channels: as a GEMM over pixels its N is 3, so the forward pads N to
 // the 16 of one v_mfma_f32_16x16x32_bf16 (13/16 of the MFMA is wasted, and the MFMA is still far
-// from being the limit).  Everything is organised around one LDS tile per workgroup: 4 image
-// rows x 64 columns (+1 halo on every side) x 32 channels of act = lrelu(BN(y)), bf16, with the
-// 16-byte channel chunks of a pixel XOR-swizzled by (column & 3) so that 16 lanes reading 16
-// consecutive pixels hit 16 different bank slots.
+// from being the limit).  Everything is organised around one LDS tile per workgroup: ROWS image
+// rows x 64 columns (+1 halo on every side) x C channels of act = lrelu(BN(y)), bf16, staged once
+// per element (the conv-GEMM route gathered every input element 9 times through L2: big_ae's
+// head at C = 128 took 112 us forward and 89 us data gradient that way), with the 16-byte channel
+// chunks of a pixel XOR-swizzled by the column so that 16 lanes reading 16 consecutive pixels
+// hit different bank slots.  ROWS = 4 (C <= 64) or 2 (C = 128: the backward's tile, raw-y copy
+// and output staging then fit one CU's LDS).
 //
-//   forward : 16 pixels x 16 (3 real) outputs, K = 9 taps x 32 channels = 9 MFMAs;
+//   forward : 16 pixels x 16 (3 real) outputs, K = 9 taps x C channels (9 C/32 MFMAs);
 //             epilogue tanh -> recon (NCHW fp32, float4 stores), (recon - x)^2 -> SSE.
 //   backward: one persistent kernel, per tile
 //     data   dact[p][c] = sum_{tap,co} gseed[p + 1 - tap][co] W[co][tap][c]: K = 9 taps x 4 (3 co
-//            + pad) = 36 -> 2 k-steps, N = 32 channels; epilogue g = dact * lrelu'(z) (z = BN(y)),
+//            + pad) = 36 -> 2 k-steps, N = C channels; epilogue g = dact * lrelu'(z) (z = BN(y)),
 //            BatchNorm-backward sums (sum g, sum g*xhat) and g stored through LDS as whole rows;
-//     filter dW[co][tap][c] = sum_p gseed[p][co] act[p + tap - 1][c]: M = co (pad 16), N = 288,
-//            K = the tile's 256 pixels; the act operand is read transposed (ds_read_b64_tr_b16)
+//     filter dW[co][tap][c] = sum_p gseed[p][co] act[p + tap - 1][c]: M = co (pad 16), N = 9 C,
+//            K = the tile's own pixels; the act operand is read transposed (ds_read_b64_tr_b16)
 //            from the same LDS tile; per-block partials go to a slab summed by vae_reduce_rows
 //            (fixed order: deterministic, and no same-address atomics).
+// Tiles are dealt XCD-aware (workgroup b runs on XCD b % 8): the workgroups one XCD runs at once
+// take consecutive tiles, so a tile's halo rows are its neighbours' own rows in the same L2.
 #include <stdlib.h>
 
 #include "vae_common.hpp"
@@ -25,14 +32,26 @@
 namespace vae {
 namespace {
 
-constexpr int HC = 32;                 // channels entering the head
 constexpr int HW = 64;                 // image width (one tile row)
-constexpr int ROWS = 4;                // image rows per tile
-constexpr int TR = ROWS + 2, TCOLS = HW + 2, TPIX = TR * TCOLS;   // tile with halo
-constexpr int OCT = TPIX * (HC / 8);   // 16-byte octets in the act tile
-constexpr int OCT_PER_T = (OCT + 255) / 256;
-constexpr int OWN = ROWS * HW;         // pixels a tile produces
 constexpr int NCO = 3;
+
+template <int HC>
+struct HT {
+  static constexpr int ROWS = HC >= 128 ? 2 : 4;       // image rows per tile
+  static constexpr int TR = ROWS + 2, TCOLS = HW + 2, TPIX = TR * TCOLS;   // tile with halo
+  static constexpr int CH = HC / 8;                    // 16-byte channel chunks per pixel
+  static constexpr int SW = CH >= 8 ? 7 : CH - 1;      // chunk XOR-swizzle mask
+  static constexpr int OCT = TPIX * CH;                // 16-byte octets in the act tile
+  static constexpr int OCT_PER_T = (OCT + 255) / 256;
+  static constexpr int OWN = ROWS * HW;                // pixels a tile produces
+  static constexpr int GPW = OWN / 64;                 // 16-pixel groups per wave
+  static constexpr int CC = HC / 32;                   // forward K-steps per tap
+  static constexpr int NF = HC / 16;                   // data-gradient n-frags (16 channels)
+  static constexpr int NFR = 9 * NF;                   // weight-gradient n-frags over (tap, c)
+  static constexpr int NFW = (NFR + 3) / 4;            // ... per wave
+  static constexpr int NW = NCO * 9 * HC;              // weight-gradient entries
+  static constexpr int SLAB_COLS = NW + NCO;           // + 3 bias-gradient entries
+};
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -43,13 +62,13 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t kOOB = 0x80000000u;
 
 struct HeadQ {
-  int n, h, samples, tiles;
+  int n, h, samples, tiles, xcd;
   const __bf16* x; vae_xform xf;       // fin (pre-BN), its BatchNorm+LeakyReLU
-  const float* wt; const float* bias;  // [3][3][3][32] fp32 native, [3]
+  const float* wt; const float* bias;  // [3][3][3][C] fp32 native, [3]
   const float* target; float* recon; float* sse;
   const float* coef; const float* grad_recon;
   __bf16* dx; float* dgamma; float* dbeta; int sum_reps, sum_rstride;
-  float* slab;                         // [grid][3*288 + 3] filter partials, or NULL: atomics into dw/db
+  float* slab;                         // [grid][27 C + 3] filter partials, or NULL: atomics into dw/db
   float* dw; float* db;
   int data, filter;
 };
@@ -59,8 +78,16 @@ __device__ __forceinline__ rsrc_t rsrc(const void* p, uint32_t bytes) {
 }
 
 // byte offset of (tile pixel, 16-byte channel chunk) in the act tile
+template <int HC>
 __device__ __forceinline__ int act_off(int trow, int tcol, int chunk) {
-  return (trow * TCOLS + tcol) * (HC * 2) + ((chunk ^ (tcol & 3)) << 4);
+  return (trow * HT<HC>::TCOLS + tcol) * (HC * 2) + ((chunk ^ (tcol & HT<HC>::SW)) << 4);
+}
+
+// XCD-aware order (a permutation of [0, nb)): the nb / 8 workgroups of XCD x = b % 8 take one
+// contiguous range of positions
+__device__ __forceinline__ int head_xcd_order(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+  return x * q + min(x, r) + loc;
 }
 
 __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(bits16 << 16); }
@@ -68,6 +95,7 @@ __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(
 // Per-channel BN coefficients in LDS (from vae_bn_finalize's table when present).
 // Without a precomputed table the workgroup reduces the producer's replicated statistics itself
 // (tab_build; `update_running`: this workgroup also applies the running-statistic update).
+template <int HC>
 __device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq, bool update_running = false) {
   if (xf.kind == VAE_X_BN_ACT && !xf.table && xf.channels == HC && bn_fast_ok(xf)) {
     tab_build(xf, Tab{ta, tb, nullptr, tp, tq}, true, update_running);
@@ -82,33 +110,43 @@ __device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp
       bn_moments(xf, c, mean, invstd, var);
       ta[c] = xf.gamma[c] * invstd; tb[c] = xf.beta[c] - mean * ta[c];
       tp[c] = invstd; tq[c] = -mean * invstd;
+      if (update_running && xf.running_mean) {     // (C = 128: 32 statistic replicas, no tab_build)
+        const float m = xf.momentum;
+        const float unb = xf.count > 1.f ? var * xf.count / (xf.count - 1.f) : var;
+        xf.running_mean[c] = (1.f - m) * xf.running_mean[c] + m * mean;
+        xf.running_var[c] = (1.f - m) * xf.running_var[c] + m * unb;
+      }
     }
   }
 }
 
 // Raw y octets of the tile (halo included) -> registers; issued together (out of image: 0).
-__device__ __forceinline__ void tile_load(const HeadQ& q, rsrc_t ry, int n, int h0, u32x4 (&raw)[OCT_PER_T]) {
+template <int HC>
+__device__ __forceinline__ void tile_load(const HeadQ& q, rsrc_t ry, int n, int h0, u32x4 (&raw)[HT<HC>::OCT_PER_T]) {
+  using T = HT<HC>;
 #pragma unroll
-  for (int j = 0; j < OCT_PER_T; ++j) {
+  for (int j = 0; j < T::OCT_PER_T; ++j) {
     const int o = threadIdx.x + 256 * j;
-    const int pix = o >> 2, ch = o & 3;
-    const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+    const int pix = o / T::CH, ch = o % T::CH;
+    const int trow = pix / T::TCOLS, tcol = pix - trow * T::TCOLS;
     const int hi = h0 + trow - 1, wi = tcol - 1;
-    const bool ok = o < OCT && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+    const bool ok = o < T::OCT && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
     const uint32_t off = ok ? (uint32_t)((((n * q.h + hi) * HW + wi) * HC + ch * 8) * 2) : kOOB;
     raw[j] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
   }
 }
 
 // act = lrelu(a*y + b) (0 outside the image) -> bf16 tile in LDS
-__device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (&raw)[OCT_PER_T], char* tile,
+template <int HC>
+__device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (&raw)[HT<HC>::OCT_PER_T], char* tile,
                                            const float* ta, const float* tb) {
+  using T = HT<HC>;
 #pragma unroll
-  for (int j = 0; j < OCT_PER_T; ++j) {
+  for (int j = 0; j < T::OCT_PER_T; ++j) {
     const int o = threadIdx.x + 256 * j;
-    if (o >= OCT) continue;
-    const int pix = o >> 2, ch = o & 3;
-    const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+    if (o >= T::OCT) continue;
+    const int pix = o / T::CH, ch = o % T::CH;
+    const int trow = pix / T::TCOLS, tcol = pix - trow * T::TCOLS;
     const int hi = h0 + trow - 1, wi = tcol - 1;
     const bool ok = hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
     u32x4 out;
@@ -124,65 +162,79 @@ __device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (
       bf16x2 pk; pk[0] = (__bf16)lo; pk[1] = (__bf16)hi2;
       out[e] = *reinterpret_cast<uint32_t*>(&pk);
     }
-    *reinterpret_cast<u32x4*>(tile + act_off(trow, tcol, ch)) = out;
+    *reinterpret_cast<u32x4*>(tile + act_off<HC>(trow, tcol, ch)) = out;
   }
 }
 
 // ======================================================================= forward
-__global__ void __launch_bounds__(256) head_fwd_mfma(HeadQ q) {
-  __shared__ __attribute__((aligned(16))) char tile[TPIX * HC * 2];
+template <int HC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_fwd_mfma(HeadQ q) {
+  using T = HT<HC>;
+  __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float red[4];
-  __shared__ __attribute__((aligned(16))) float wsh[NCO * 9 * HC];
+  __shared__ __attribute__((aligned(16))) __bf16 wsb[T::NW];         // W[co][tap][c] as bf16
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int tiles_per_img = q.h / ROWS;
-  const int n = blockIdx.x / tiles_per_img, h0 = (blockIdx.x - n * tiles_per_img) * ROWS;
+  const int tiles_per_img = q.h / T::ROWS;
+  const int ti = q.xcd ? head_xcd_order((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int n = ti / tiles_per_img, h0 = (ti - n * tiles_per_img) * T::ROWS;
   const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
-  u32x4 raw[OCT_PER_T];
-  tile_load(q, ry, n, h0, raw);
+  u32x4 raw[T::OCT_PER_T];
+  tile_load<HC>(q, ry, n, h0, raw);
   const int co = lane & 15, g = lane >> 4;
   // the epilogue's target pixels, in flight with the tile (no global load after the MFMAs)
-  f32x4v tgv[4];
+  f32x4v tgv[T::GPW];
 #pragma unroll
-  for (int gi = 0; gi < 4; ++gi) {
-    const int grp = wave * 4 + gi, row = grp >> 2, c0 = (grp & 3) * 16;
+  for (int gi = 0; gi < T::GPW; ++gi) {
+    const int grp = wave * T::GPW + gi, row = grp >> 2, c0 = (grp & 3) * 16;
     tgv[gi] = co < NCO ? *reinterpret_cast<const f32x4v*>(q.target + (((long)(n / q.samples) * NCO + co) * q.h + h0 + row) * HW +
                                                          c0 + 4 * g)
                        : f32x4v{0.f, 0.f, 0.f, 0.f};
   }
-  // the 864 weights: one coalesced pass into LDS (per-lane scattered scalar loads of the
-  // fragments cost ~72 vector-memory instructions per wave)
-  for (int i = threadIdx.x; i < NCO * 9 * HC; i += 256) wsh[i] = q.wt[i];
+  // the weights: one coalesced pass into LDS (per-lane scattered scalar loads of the fragments
+  // cost ~72 vector-memory instructions per wave at C = 32)
+  for (int i = threadIdx.x; i < T::NW; i += 256) wsb[i] = (__bf16)q.wt[i];
   const float bco = co < NCO ? q.bias[co] : 0.f;
-  head_tables(q.xf, ta, tb, tp, tq, blockIdx.x == 0);
+  head_tables<HC>(q.xf, ta, tb, tp, tq, blockIdx.x == 0);
   __syncthreads();
-  tile_store(q, h0, raw, tile, ta, tb);
-  // B fragments: W[co = lane&15][tap][8*(lane>>4) .. +7] (zero for co >= 3)
-  bf16x8 bw[9];
+  tile_store<HC>(q, h0, raw, tile, ta, tb);
+  // B fragment of (tap t, K-step cc): W[co = lane&15][t][32 cc + 8 (lane>>4) .. +7] (zero for co >= 3);
+  // held in registers while they fit (C <= 64), read from LDS per K-step otherwise
+  constexpr int KS = 9 * T::CC;
+  constexpr bool BREG = KS <= 18;
+  const bf16x8 bz = {};
+  bf16x8 bw[BREG ? KS : 1];
+  if constexpr (BREG) {
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int wr = (co < NCO ? co : 0) * 9 + t;   // rows co >= 3 read row 0, then zeroed
-    const f32x4 w0 = *reinterpret_cast<const f32x4*>(&wsh[wr * HC + 8 * g]);
-    const f32x4 w1 = *reinterpret_cast<const f32x4*>(&wsh[wr * HC + 8 * g + 4]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bw[t][j] = (__bf16)(co < NCO ? w0[j] : 0.f);
-      bw[t][4 + j] = (__bf16)(co < NCO ? w1[j] : 0.f);
+    for (int k = 0; k < KS; ++k) {
+      const int t = k / T::CC, cc = k - t * T::CC;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(&wsb[((co < NCO ? co : 0) * 9 + t) * HC + 32 * cc + 8 * g]);
+      bw[k] = co < NCO ? v : bz;
     }
   }
   __syncthreads();
   float sq = 0.f;
 #pragma unroll
-  for (int gi = 0; gi < 4; ++gi) {
-    const int grp = wave * 4 + gi;                  // 16 groups of 16 pixels
+  for (int gi = 0; gi < T::GPW; ++gi) {
+    const int grp = wave * T::GPW + gi;             // groups of 16 pixels, 4 per image row
     const int row = grp >> 2, c0 = (grp & 3) * 16;
     f32x4v acc = {0.f, 0.f, 0.f, 0.f};
     const f32x4v tg = tgv[gi];
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int r = t / 3, s = t - 3 * (t / 3);
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + act_off(row + r, c0 + (lane & 15) + s, g));
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[t], acc, 0, 0, 0);
+#pragma unroll
+      for (int cc = 0; cc < T::CC; ++cc) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + act_off<HC>(row + r, c0 + (lane & 15) + s, g + 4 * cc));
+        bf16x8 b;
+        if constexpr (BREG) {
+          b = bw[t * T::CC + cc];
+        } else {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(&wsb[((co < NCO ? co : 0) * 9 + t) * HC + 32 * cc + 8 * g]);
+          b = co < NCO ? v : bz;
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+      }
     }
     // lane: output channel co, pixels c0 + 4g + i
     if (co < NCO) {
@@ -214,15 +266,17 @@ __device__ __forceinline__ bf16x4v tr16_read(const char* generic_lds_addr) {
 // and the arithmetic: ld = (recon y, grad_recon or target)
 struct SeedLd { float y[2][NCO], t[2][NCO]; };
 
+template <int HC>
 __device__ __forceinline__ void seed_load(const HeadQ& q, int tile_i, SeedLd& ld) {
-  const int tiles_per_img = q.h / ROWS;
-  const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * ROWS;
+  using T = HT<HC>;
+  const int tiles_per_img = q.h / T::ROWS;
+  const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * T::ROWS;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int pix = threadIdx.x + 256 * j;
-    const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
+    const int trow = pix / T::TCOLS, tcol = pix - trow * T::TCOLS;
     const int hi = h0 + trow - 1, wi = tcol - 1;
-    const bool ok = pix < TPIX && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
+    const bool ok = pix < T::TPIX && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
 #pragma unroll
     for (int co = 0; co < NCO; ++co) {
       const long oi = (((long)n * NCO + co) * q.h + hi) * HW + wi;
@@ -240,58 +294,81 @@ __device__ __forceinline__ float gseed(const HeadQ& q, int n, const SeedLd& ld, 
   return q.coef[n] * (y - ld.t[j][co]) * (1.f - y * y);   // 0 outside the image (y = t = 0)
 }
 
-constexpr int NW = NCO * 9 * HC;        // 864 weight-gradient entries
-constexpr int SLAB_COLS = NW + NCO;     // + 3 bias-gradient entries
-
-// Registers capped for 2 workgroups per CU (VAE_HEAD_GRID=512 then runs two tiles in flight per
-// CU; at the default grid of 256 the cap only bounds the allocation).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_bwd_mfma(HeadQ q) {
-  __shared__ __attribute__((aligned(16))) char tile[TPIX * HC * 2];
-  __shared__ __attribute__((aligned(16))) uint2 gsA[TPIX];               // [pixel][co0..2, 0] bf16
-  __shared__ __attribute__((aligned(16))) __bf16 gsT[4][OWN];            // [co][own pixel]
-  __shared__ __attribute__((aligned(16))) __bf16 gst[4][16 * HC];        // per-wave output staging
-  __shared__ __attribute__((aligned(16))) char ytile[OWN * HC * 2];      // raw y of the own pixels
+// C = 32: registers capped for 2 workgroups per CU (the grid of 512 then runs two tiles in flight
+// per CU).  C >= 64: the LDS holds one workgroup per CU (C = 128: 130 KB), which keeps all 512
+// VGPRs of a SIMD for its wave.
+template <int HC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 64 ? 1 : 2))) head_bwd_mfma(HeadQ q) {
+  using T = HT<HC>;
+  __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];
+  __shared__ __attribute__((aligned(16))) uint2 gsA[T::TPIX];              // [pixel][co0..2, 0] bf16
+  __shared__ __attribute__((aligned(16))) __bf16 gsT[4][T::OWN];           // [co][own pixel]
+  __shared__ __attribute__((aligned(16))) __bf16 gst[4][16 * HC];          // per-wave output staging
+  __shared__ __attribute__((aligned(16))) char ytile[T::OWN * HC * 2];     // raw y of the own pixels
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float r1[4][HC], r2[4][HC], rdb[4][NCO];
-  __shared__ float wsh[NCO * 9 * HC];
+  __shared__ bf16x8 bdl[HT<HC>::NF > 4 ? 2 * HT<HC>::NF * 64 : 1];      // [ks][nf][lane] (C = 128)
+  // the fp32 weights pass through the output staging area before the first tile (27 C floats
+  // in 128 C bytes)
+  float* wsh = reinterpret_cast<float*>(&gst[0][0]);
+  static_assert(T::NW * 4 <= 4 * 16 * HC * 2, "weights fit the staging area");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int tiles_per_img = q.h / ROWS;
+  const int tiles_per_img = q.h / T::ROWS;
   const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
+  // tile_i = k * gridDim.x + bpos: at every step the workgroups of one XCD hold consecutive tiles
+  const int bpos = q.xcd ? head_xcd_order((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
 
-  // the 864 weights through LDS in one coalesced pass (built into fragments after the prologue)
-  for (int i = threadIdx.x; i < NCO * 9 * HC; i += 256) wsh[i] = q.wt[i];
-  // filter accumulators: this wave's n-frags f = wave + 4*i (18 n-frags of 16 over (tap, c))
-  constexpr int NFW = 5;
-  f32x4v accw[NFW];
+  for (int i = threadIdx.x; i < T::NW; i += 256) wsh[i] = q.wt[i];
+  // filter accumulators: this wave's n-frags f = wave + 4*i (9 C / 16 n-frags of 16 over (tap, c))
+  f32x4v accw[T::NFW];
 #pragma unroll
-  for (int i = 0; i < NFW; ++i) accw[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, dbp[NCO] = {0.f, 0.f, 0.f};
+  for (int i = 0; i < T::NFW; ++i) accw[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float s1[T::NF], s2[T::NF], dbp[NCO] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nf = 0; nf < T::NF; ++nf) { s1[nf] = 0.f; s2[nf] = 0.f; }
 
-  head_tables(q.xf, ta, tb, tp, tq);
+  head_tables<HC>(q.xf, ta, tb, tp, tq);
   // software pipeline: the raw y tile and the seed inputs of the next tile are loaded while
-  // this tile's MFMAs run (one workgroup per CU leaves no other wave to hide the latency)
-  u32x4 raw[OCT_PER_T];
+  // this tile's MFMAs run (one or two workgroups per CU leave few other waves to hide the latency)
+  u32x4 raw[T::OCT_PER_T];
   SeedLd sld;
-  if ((int)blockIdx.x < q.tiles) {
-    const int n0 = blockIdx.x / tiles_per_img;
-    tile_load(q, ry, n0, (blockIdx.x - n0 * tiles_per_img) * ROWS, raw);
-    seed_load(q, blockIdx.x, sld);
+  if (bpos < q.tiles) {
+    const int n0 = bpos / tiles_per_img;
+    tile_load<HC>(q, ry, n0, (bpos - n0 * tiles_per_img) * T::ROWS, raw);
+    seed_load<HC>(q, bpos, sld);
   }
   __syncthreads();
-  // dgrad B fragments: B[k = tap*4 + co][n = c] = W[co][tap][c], k-step ks, n-frag nf
-  bf16x8 bd[2][2];
+  // dgrad B fragments: B[k = tap*4 + co][n = c] = W[co][tap][c], k-step ks, n-frag nf — in
+  // registers up to C = 64; at C = 128 (64 more VGPRs than the wave has: 146 spilled) they are
+  // built once into LDS and read per use
+  constexpr bool BDREG = T::NF <= 4;
+  bf16x8 bd[2][BDREG ? T::NF : 1];
+  if constexpr (BDREG) {
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int nf = 0; nf < 2; ++nf)
+      for (int nf = 0; nf < T::NF; ++nf)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int tap = ks * 8 + 2 * g + (j >> 2), c2 = j & 3, c = nf * 16 + li;
+          bd[ks][nf][j] = (__bf16)(tap < 9 && c2 < NCO ? wsh[(c2 * 9 + tap) * HC + c] : 0.f);
+        }
+  } else {
+    for (int idx = threadIdx.x; idx < 2 * T::NF * 64; idx += 256) {
+      const int ln = idx & 63, ks = idx / (64 * T::NF), nf = (idx >> 6) - ks * T::NF;
+      const int lg = ln >> 4, ll = ln & 15;
+      bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int tap = ks * 8 + 2 * g + (j >> 2), c2 = j & 3, c = nf * 16 + li;
-        bd[ks][nf][j] = (__bf16)(tap < 9 && c2 < NCO ? wsh[(c2 * 9 + tap) * HC + c] : 0.f);
+        const int tap = ks * 8 + 2 * lg + (j >> 2), c2 = j & 3, c = nf * 16 + ll;
+        v[j] = (__bf16)(tap < 9 && c2 < NCO ? wsh[(c2 * 9 + tap) * HC + c] : 0.f);
       }
-  for (int tile_i = blockIdx.x; tile_i < q.tiles; tile_i += gridDim.x) {
-    const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * ROWS;
+      bdl[idx] = v;
+    }
+  }
+  for (int tile_i = bpos; tile_i < q.tiles; tile_i += gridDim.x) {
+    const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * T::ROWS;
     // gseed over the halo tile: threads walk pixels (2 per thread)
     float gv[2][NCO];
     int gpix[2];
@@ -301,30 +378,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
 #pragma unroll
       for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = gseed(q, n, sld, j, c2);
     }
-    __syncthreads();                    // previous tile's LDS reads done (and tables ready)
-    tile_store(q, h0, raw, tile, ta, tb);
+    __syncthreads();                    // previous tile's LDS reads done (and tables / weights read)
+    tile_store<HC>(q, h0, raw, tile, ta, tb);
     // raw y (pre-BN) of the own pixels for the data epilogue, from the same registers:
-    // [own pixel][32 ch] bf16, 16-byte chunks XOR-swizzled by (pixel & 3)
+    // [own pixel][C] bf16, 16-byte chunks XOR-swizzled by the pixel
     if (q.data) {
 #pragma unroll
-      for (int j = 0; j < OCT_PER_T; ++j) {
+      for (int j = 0; j < T::OCT_PER_T; ++j) {
         const int o = threadIdx.x + 256 * j;
-        if (o >= OCT) continue;
-        const int pix = o >> 2, chk = o & 3;
-        const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
-        if (trow < 1 || trow > ROWS || tcol < 1 || tcol > HW) continue;
+        if (o >= T::OCT) continue;
+        const int pix = o / T::CH, chk = o % T::CH;
+        const int trow = pix / T::TCOLS, tcol = pix - trow * T::TCOLS;
+        if (trow < 1 || trow > T::ROWS || tcol < 1 || tcol > HW) continue;
         const int own = (trow - 1) * HW + (tcol - 1);
-        *reinterpret_cast<u32x4*>(ytile + own * (HC * 2) + ((chk ^ (own & 3)) << 4)) = raw[j];
+        *reinterpret_cast<u32x4*>(ytile + own * (HC * 2) + ((chk ^ (own & T::SW)) << 4)) = raw[j];
       }
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int pix = gpix[j];
-      if (pix >= TPIX) continue;
+      if (pix >= T::TPIX) continue;
       bf16x4v v; v[0] = (__bf16)gv[j][0]; v[1] = (__bf16)gv[j][1]; v[2] = (__bf16)gv[j][2]; v[3] = (__bf16)0.f;
       gsA[pix] = *reinterpret_cast<uint2*>(&v);
-      const int trow = pix / TCOLS, tcol = pix - trow * TCOLS;
-      if (trow >= 1 && trow <= ROWS && tcol >= 1 && tcol <= HW) {
+      const int trow = pix / T::TCOLS, tcol = pix - trow * T::TCOLS;
+      if (trow >= 1 && trow <= T::ROWS && tcol >= 1 && tcol <= HW) {
         const int own = (trow - 1) * HW + (tcol - 1);
 #pragma unroll
         for (int c2 = 0; c2 < NCO; ++c2) gsT[c2][own] = v[c2];
@@ -338,19 +415,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
       const int nx = tile_i + gridDim.x;
       if (nx < q.tiles) {
         const int n1 = nx / tiles_per_img;
-        tile_load(q, ry, n1, (nx - n1 * tiles_per_img) * ROWS, raw);
-        seed_load(q, nx, sld);
+        tile_load<HC>(q, ry, n1, (nx - n1 * tiles_per_img) * T::ROWS, raw);
+        seed_load<HC>(q, nx, sld);
       }
     }
 
     if (q.data) {
-      // ---- dact for this wave's 4 groups of 16 pixels, N = 32 channels (2 n-frags)
+      // ---- dact for this wave's groups of 16 pixels, N = C channels (C / 16 n-frags)
 #pragma unroll 1
-      for (int gi = 0; gi < 4; ++gi) {
-        const int grp = wave * 4 + gi;
+      for (int gi = 0; gi < T::GPW; ++gi) {
+        const int grp = wave * T::GPW + gi;
         const int row = grp >> 2, c0 = (grp & 3) * 16;
         const int hh = h0 + row;
-        f32x4v acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        f32x4v acc[T::NF];
+#pragma unroll
+        for (int nf = 0; nf < T::NF; ++nf) acc[nf] = f32x4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           bf16x8 a;
@@ -360,23 +439,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
             uint2 v = {0u, 0u};
             if (tap < 9) {
               const int r = tap / 3, s = tap - 3 * r;
-              v = gsA[(row + 2 - r) * TCOLS + (c0 + li + 2 - s)];
+              v = gsA[(row + 2 - r) * T::TCOLS + (c0 + li + 2 - s)];
             }
             const bf16x4v b4 = *reinterpret_cast<bf16x4v*>(&v);
 #pragma unroll
             for (int j = 0; j < 4; ++j) a[4 * half + j] = b4[j];
           }
 #pragma unroll
-          for (int nf = 0; nf < 2; ++nf) acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bd[ks][nf], acc[nf], 0, 0, 0);
+          for (int nf = 0; nf < T::NF; ++nf) {
+            bf16x8 b;
+            if constexpr (BDREG) b = bd[ks][nf];
+            else b = bdl[(ks * T::NF + nf) * 64 + lane];
+            acc[nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[nf], 0, 0, 0);
+          }
         }
-        // g = dact * lrelu'(z); BN-backward sums; stage [16 px][32 ch] for whole-row stores
+        // g = dact * lrelu'(z); BN-backward sums; stage [16 px][C] for whole-row stores
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf) {
+        for (int nf = 0; nf < T::NF; ++nf) {
           const int c = nf * 16 + li;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int own = row * HW + c0 + 4 * g + i;
-            const float y = (float)*reinterpret_cast<const __bf16*>(ytile + own * (HC * 2) + (((c >> 3) ^ (own & 3)) << 4) + (c & 7) * 2);
+            const float y = (float)*reinterpret_cast<const __bf16*>(ytile + own * (HC * 2) +
+                                                                    (((c >> 3) ^ (own & T::SW)) << 4) + (c & 7) * 2);
             const float z = fmaf(y, ta[c], tb[c]);
             const float gg = z > 0.f ? acc[nf][i] : acc[nf][i] * q.xf.slope;
             s1[nf] += gg;
@@ -385,26 +470,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
           }
         }
         __builtin_amdgcn_wave_barrier();
-        // 16 pixels x 64 B = 1 KB contiguous (NHWC): 16 B per lane
-        const u32x4 v = *reinterpret_cast<const u32x4*>(&gst[wave][lane * 8]);
-        *reinterpret_cast<u32x4*>(q.dx + (((long)n * q.h + hh) * HW + c0) * HC + lane * 8) = v;
+        // 16 pixels x 2C B contiguous (NHWC): 16 B per lane per 1 KB
+#pragma unroll
+        for (int j = 0; j < HC / 32; ++j) {
+          const u32x4 v = *reinterpret_cast<const u32x4*>(&gst[wave][lane * 8 + 512 * j]);
+          *reinterpret_cast<u32x4*>(q.dx + (((long)n * q.h + hh) * HW + c0) * HC + lane * 8 + 512 * j) = v;
+        }
         __builtin_amdgcn_wave_barrier();
       }
     }
 
     if (q.filter) {
-      // ---- dW partials: M = co (rows 0..2 of 16), N = (tap, c), K = 256 own pixels
-#pragma unroll
-      for (int ks = 0; ks < OWN / 32; ++ks) {
+      // ---- dW partials: M = co (rows 0..2 of 16), N = (tap, c), K = the own pixels
+      // (C = 128: one K-step at a time — unrolled, the scheduler hoisted all 144 transposed reads)
+      constexpr int KU = T::NF > 4 ? 1 : T::OWN / 32;
+#pragma unroll KU
+      for (int ks = 0; ks < T::OWN / 32; ++ks) {
         const int k0 = ks * 32 + 8 * g;                 // this lane group's 8 pixels
         const int row = k0 / HW, col = k0 - row * HW;
         // rows co >= 3 of the M = 16 fragment read the all-zero row 3
         const bf16x8 az = *reinterpret_cast<const bf16x8*>(&gsT[li < 4 ? li : 3][k0]);
 #pragma unroll
-        for (int i = 0; i < NFW; ++i) {
+        for (int i = 0; i < T::NFW; ++i) {
           const int f = wave + 4 * i;
-          if (f < 18) {
-            const int tap = f >> 1, cb = (f & 1) * 16;
+          if (f < T::NFR) {
+            const int tap = f / T::NF, cb = (f - tap * T::NF) * 16;
             const int r = tap / 3, s = tap - 3 * r;
             // lane 4qq+pp of the 16-lane group: pixel qq (+4), channels cb + 4pp .. +3
             const int qq = li >> 2, pp = li & 3;
@@ -413,7 +503,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
               const int tcol = col + 4 * half + qq + s, trow = row + r;
-              const char* addr = tile + act_off(trow, tcol, ch >> 3) + ((ch & 4) << 1);
+              const char* addr = tile + act_off<HC>(trow, tcol, ch >> 3) + ((ch & 4) << 1);
               const bf16x4v t4 = tr16_read(addr);
 #pragma unroll
               for (int j = 0; j < 4; ++j) b[4 * half + j] = t4[j];
@@ -428,7 +518,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
   // ---- block reductions
   if (q.data) {
 #pragma unroll
-    for (int nf = 0; nf < 2; ++nf) {
+    for (int nf = 0; nf < T::NF; ++nf) {
       float a = s1[nf], b = s2[nf];
       a += __shfl_xor(a, 16); a += __shfl_xor(a, 32);
       b += __shfl_xor(b, 16); b += __shfl_xor(b, 32);
@@ -451,21 +541,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
   __syncthreads();
   if (q.filter && threadIdx.x < NCO && q.db) {
     const float v = (rdb[0][threadIdx.x] + rdb[1][threadIdx.x]) + (rdb[2][threadIdx.x] + rdb[3][threadIdx.x]);
-    if (q.slab) q.slab[(long)blockIdx.x * SLAB_COLS + NW + threadIdx.x] = v;
+    if (q.slab) q.slab[(long)blockIdx.x * T::SLAB_COLS + T::NW + threadIdx.x] = v;
     else atomicAdd(q.db + threadIdx.x, v);
   }
   if (q.filter) {
     // dW[co][tap][c]: lane li = column within the n-frag, rows 4g+i = co (g == 0, i < 3 real)
-    float* out = q.slab ? q.slab + (long)blockIdx.x * SLAB_COLS : q.dw;
+    float* out = q.slab ? q.slab + (long)blockIdx.x * T::SLAB_COLS : q.dw;
 #pragma unroll
-    for (int i = 0; i < NFW; ++i) {
+    for (int i = 0; i < T::NFW; ++i) {
       const int f = wave + 4 * i;
-      if (f >= 18 || g != 0) continue;
-      const int nn = f * 16 + li;                       // = tap*32 + c
+      if (f >= T::NFR || g != 0) continue;
+      const int nn = f * 16 + li;                       // = tap*C + c
 #pragma unroll
       for (int e = 0; e < NCO; ++e) {
-        if (q.slab) out[e * 288 + nn] = accw[i][e];
-        else atomicAdd(out + e * 288 + nn, accw[i][e]);
+        if (q.slab) out[e * 9 * HC + nn] = accw[i][e];
+        else atomicAdd(out + e * 9 * HC + nn, accw[i][e]);
       }
     }
   }
@@ -475,18 +565,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
 // (columns < NW) and db (the NCO columns after): 16 columns x 16 row-parts per workgroup, each
 // part's loads issued together, parts combined in a fixed order (deterministic).
 constexpr int RR_COLS = 16, RR_PARTS = 16, RR_UNROLL = 8;
+template <int HC>
 __global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, float* dw, float* db) {
+  using T = HT<HC>;
   __shared__ float red[RR_PARTS][RR_COLS];
   const int cl = threadIdx.x % RR_COLS, part = threadIdx.x / RR_COLS;
   const int c = blockIdx.x * RR_COLS + cl;
   float s = 0.f;
-  if (c < SLAB_COLS && (c < NW || db)) {
+  if (c < T::SLAB_COLS && (c < T::NW || db)) {
     for (int r0 = part; r0 < rows; r0 += RR_PARTS * RR_UNROLL) {
       float v[RR_UNROLL];
 #pragma unroll
       for (int u = 0; u < RR_UNROLL; ++u) {
         const int r = r0 + u * RR_PARTS;
-        v[u] = r < rows ? src[(long)r * SLAB_COLS + c] : 0.f;
+        v[u] = r < rows ? src[(long)r * T::SLAB_COLS + c] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < RR_UNROLL; ++u) s += v[u];
@@ -494,24 +586,37 @@ __global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int 
   }
   red[part][cl] = s;
   __syncthreads();
-  if (part != 0 || c >= SLAB_COLS) return;
+  if (part != 0 || c >= T::SLAB_COLS) return;
   float t = 0.f;
 #pragma unroll
   for (int i = 0; i < RR_PARTS; ++i) t += red[i][cl];
-  if (c < NW) dw[c] += t;
-  else if (db) db[c - NW] += t;
+  if (c < T::NW) dw[c] += t;
+  else if (db) db[c - T::NW] += t;
 }
 
+inline int head_rows(int c) { return c >= 128 ? HT<128>::ROWS : HT<32>::ROWS; }
+
 bool head_mfma_ok(const vae_head_args* a) {
-  return a->dtype == VAE_BF16 && a->c == HC && a->w == HW && a->h % ROWS == 0 && a->h > 0 && a->n > 0 &&
+  return a->dtype == VAE_BF16 && (a->c == 32 || a->c == 64 || a->c == 128) && a->w == HW && a->h > 0 &&
+         a->h % head_rows(a->c) == 0 && a->n > 0 &&
          ((uintptr_t)a->x & 15) == 0 && ((uintptr_t)a->recon & 15) == 0 && ((uintptr_t)a->target & 15) == 0 &&
          (a->x_xf.kind == VAE_X_BN_ACT || a->x_xf.kind == VAE_X_ACT || a->x_xf.kind == VAE_X_NONE);
+}
+
+// XCD-aware tile order (VAE_HEAD_XCD=0 turns it off: A/B sweeps only; read once)
+int head_xcd() {
+  static const int v = [] {
+    const char* e = getenv("VAE_HEAD_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 HeadQ head_q(const vae_head_args* a) {
   HeadQ q;
   memset(&q, 0, sizeof(q));
-  q.n = a->n; q.h = a->h; q.samples = a->samples > 0 ? a->samples : 1; q.tiles = a->n * (a->h / ROWS);
+  q.n = a->n; q.h = a->h; q.samples = a->samples > 0 ? a->samples : 1; q.tiles = a->n * (a->h / head_rows(a->c));
+  q.xcd = head_xcd();
   q.x = static_cast<const __bf16*>(a->x); q.xf = a->x_xf;
   if (q.xf.channels <= 0) q.xf.channels = a->c;
   q.wt = a->wt; q.bias = a->bias; q.target = a->target; q.recon = a->recon; q.sse = a->sse;
@@ -522,32 +627,55 @@ HeadQ head_q(const vae_head_args* a) {
   return q;
 }
 
+template <int HC>
+int head_bwd_go(const vae_head_args* a, HeadQ q, int grid, hipStream_t st) {
+  using T = HT<HC>;
+  const long need = (long)grid * T::SLAB_COLS * 4;
+  float* ws = static_cast<float*>(a->workspace);
+  if (q.filter && ws && !ws_fits(need, a->workspace_bytes, "head_bwd filter partials")) return VAE_E_BADARG;
+  const bool slab = q.filter && ws;
+  q.slab = slab ? ws : nullptr;
+  VAE_LAUNCH(head_bwd_mfma<HC>, dim3(grid), dim3(256), 0, st, q);
+  int rc = check_launch("head_bwd_mfma");
+  if (rc || !q.filter) return rc;
+  if (slab) {
+    VAE_LAUNCH(reduce_rows_kernel<HC>, dim3((T::SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st, (const float*)ws,
+               grid, a->dw, a->db);
+    rc = check_launch("reduce_rows");
+  }
+  return rc;
+}
+
 }  // namespace
 
 // Entry points used by vae_misc.hip's C ABI for the bf16 MFMA path.
 int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
   if (!head_mfma_ok(a)) return kHeadFallback;       // caller falls back to the VALU kernels
   HeadQ q = head_q(a);
-  VAE_LAUNCH(head_fwd_mfma, dim3(q.tiles), dim3(256), 0, st, q);
+  switch (a->c) {
+    case 32: VAE_LAUNCH(head_fwd_mfma<32>, dim3(q.tiles), dim3(256), 0, st, q); break;
+    case 64: VAE_LAUNCH(head_fwd_mfma<64>, dim3(q.tiles), dim3(256), 0, st, q); break;
+    default: VAE_LAUNCH(head_fwd_mfma<128>, dim3(q.tiles), dim3(256), 0, st, q); break;
+  }
   return check_launch("head_fwd_mfma");
 }
 
-// Persistent grid of the backward: one workgroup per CU.  Swept on MI355X (B=64 step):
-// 128 -> 78.7 us, 192 -> 61.7, 256 -> 45.6, 512 -> 50.5, 1024 -> 61.4 (more blocks means more
-// filter partials to reduce and more halo re-reads; fewer leaves CUs idle).
-// Re-swept with the tile-ahead loads: 192 -> 50.4 us, 256 -> 38.5, 320 -> 55.6, 384 -> 49.8,
-// 512 -> 43.9 (scripts/gpu_headgrid.sh): 256 divides the 1024 tiles of B=64 evenly.
+// Persistent grid of the backward.  C = 32, swept on MI355X (B=64 step): 128 -> 78.7 us,
+// 192 -> 61.7, 256 -> 45.6, 512 -> 50.5, 1024 -> 61.4 (more blocks means more filter partials to
+// reduce and more halo re-reads; fewer leaves CUs idle).  Re-swept with the tile-ahead loads:
+// 192 -> 50.4 us, 256 -> 38.5, 320 -> 55.6, 384 -> 49.8, 512 -> 43.9 (scripts/gpu_headgrid.sh).
 // r2: with the registers capped for 2 workgroups per CU (amdgpu_waves_per_eu(2)), 512 -> 37.2 us
 // (two tiles in flight per CU), 256 -> 45.1 (the cap's spills without the second workgroup).
-constexpr int kHeadGrid = 512;
+// C >= 64: one workgroup per CU (LDS), so 256.
+constexpr int kHeadGrid = 512, kHeadGridWide = 256;
 // VAE_HEAD_GRID overrides it (tuning sweeps only; read once)
-int head_grid() {
+int head_grid(int c) {
   static const int g = [] {
     const char* e = getenv("VAE_HEAD_GRID");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : kHeadGrid;
+    return v > 0 ? v : 0;
   }();
-  return g;
+  return g > 0 ? g : c == 32 ? kHeadGrid : kHeadGridWide;
 }
 
 // data / filter: which halves of the backward to run.  The filter half writes per-block partials
@@ -557,21 +685,12 @@ int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStre
   if (data && a->dx_epi.kind != VAE_X_BN_ACT) return kHeadFallback;   // the fused epilogue is BatchNorm+LReLU
   HeadQ q = head_q(a);
   q.data = data; q.filter = filter;
-  const int grid = q.tiles < head_grid() ? q.tiles : head_grid();
-  const long need = (long)grid * SLAB_COLS * 4;
-  float* ws = static_cast<float*>(a->workspace);
-  if (filter && ws && !ws_fits(need, a->workspace_bytes, "head_bwd filter partials")) return VAE_E_BADARG;
-  const bool slab = filter && ws;
-  q.slab = slab ? ws : nullptr;
-  VAE_LAUNCH(head_bwd_mfma, dim3(grid), dim3(256), 0, st, q);
-  int rc = check_launch("head_bwd_mfma");
-  if (rc || !filter) return rc;
-  if (slab) {
-    VAE_LAUNCH(reduce_rows_kernel, dim3((SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st, (const float*)ws,
-                       grid, a->dw, a->db);
-    rc = check_launch("reduce_rows");
+  const int grid = q.tiles < head_grid(a->c) ? q.tiles : head_grid(a->c);
+  switch (a->c) {
+    case 32: return head_bwd_go<32>(a, q, grid, st);
+    case 64: return head_bwd_go<64>(a, q, grid, st);
+    default: return head_bwd_go<128>(a, q, grid, st);
   }
-  return rc;
 }
 
 }  // namespace vae

@@ -97,6 +97,8 @@ struct GemmParams {
   FastDiv fd_ech;            // epilogue transform channel count
   uint32_t out_aux_bytes;    // extent of the out-shaped aux tensor (residual / stored pre-activation)
   unsigned long long* probe; // VAE_PROBE builds: per-block phase timestamps (diagnostics only)
+  int m_fast;                // cgemm tile order: m fastest (an XCD's range spans few n columns:
+                             // weight-heavy layers) instead of n fastest (host: vae_launch.hpp)
 };
 
 // Phase timestamps of one block (VAE_PROBE builds): record = {block id, wall0, wall3, clk0..clk3,

@@ -590,6 +590,9 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   }
   const CgTile t = cg_pick(p.M, p.N, p.nphase, cg_table_bytes(p, EM));
   const int bk = t.bm >= 128 ? 64 : 128;
+  // tile order (vae_cgemm.hpp): m fastest when the weights outweigh the gathered input tensor
+  static const bool mf_off = getenv("VAE_NO_MFAST") != nullptr;
+  p.m_fast = (!mf_off && (long)p.b_bytes > (long)p.a_bytes) ? 1 : 0;
   int kmax = p.K;
   if (AM == A_CONVT) {
     kmax = 0;

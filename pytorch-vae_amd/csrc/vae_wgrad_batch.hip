@@ -21,6 +21,19 @@ namespace {
 
 constexpr int kWgGroupMax = 6;
 
+// XCD-aware order within each layer of a grouped launch: workgroups are dealt round-robin over the
+// 8 XCDs (block b runs on XCD b % 8; speed only, never correctness), so a layer's local index is
+// remapped to give each XCD a contiguous range of that layer — its K slices (pixel ranges,
+// slice-outermost) then share an L2 instead of every XCD fetching every layer's operands from the
+// fabric (VanillaVAE mixed launch: 86 -> 69 MB of FETCH/WRITE traffic at the same 49.5-50 us,
+// r4_v5 / r4n PMC).  Per layer, not over the whole grid: a grid-wide remap gave whole
+// (unequal-cost) layers to single XCDs and measured 4.7 us slower despite 35 MB less traffic (r4m).
+// Mixed launch only: the all-taps 32x32 group measured slower with it (39.6 -> 45.2 us).
+__device__ __forceinline__ int wg_xcd_order(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
+  return x * q + min(x, r) + loc;
+}
+
 struct WgGroup {
   int n;
   int start[kWgGroupMax + 1];      // first workgroup of each layer; start[n] = total
@@ -57,7 +70,7 @@ wg_group_kernel(const WgGroup g) {
 #pragma unroll
   for (int j = 1; j < kWgGroupMax; ++j) i = (j < n && b >= gk->start[j]) ? j : i;
   i = __builtin_amdgcn_readfirstlane(i);
-  const int bid = b - gk->start[i];
+  const int bid = b - gk->start[i];   // (the per-layer XCD order measured 39.6 -> 45.2 us here, r4n)
   const WgParams& p = gk->p[i];
   switch (gk->var[i]) {
     case 0: wg_group_body<T, RR, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
@@ -80,7 +93,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
 #pragma unroll
   for (int j = 1; j < kWgGroupMax; ++j) i = (j < n && b >= gk->start[j]) ? j : i;
   i = __builtin_amdgcn_readfirstlane(i);
-  const int bid = b - gk->start[i];
+  const int bid = wg_xcd_order(b - gk->start[i], gk->start[i + 1] - gk->start[i]);
   const WgParams& p = gk->p[i];
   switch (gk->var[i]) {
     case 0: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;

@@ -177,12 +177,16 @@ class StepPlan:
                              and C5 % 128 == 0 and (4 * r0) % 128 == 0 and net.img_size == 64
                              and not os.environ.get("VAE_NO_LATENT"))
         self._keep = []            # ctypes structs referenced by the call lists
-        # wide_head: a final layer wider than the MFMA head kernels' 32 channels (the Autoencoder's
-        # 128-512, configs/big_ae.yaml) runs the head Conv2d(C->3) on the conv-GEMM paths with its 3
-        # outputs zero-padded to 8, then vae_recon_fwd (tanh, NCHW reconstruction, SSE, backward
-        # seed) — the VQ-VAE output layer's route.  The reconstruction seed is the mean-MSE one, so
-        # not for IWAE's per-sample weights (S > 1 keeps the head kernels).
-        self.wide_head = h[0] > 32 and self.S == 1
+        # wide_head: a final layer wider than the head kernels take on MFMA (bf16, 64-wide images:
+        # 32, 64 or 128 channels — configs/big_ae.yaml's 128 included) runs the head Conv2d(C->3)
+        # on the conv-GEMM paths with its 3 outputs zero-padded to 8, then vae_recon_fwd (tanh, NCHW
+        # reconstruction, SSE, backward seed) — the VQ-VAE output layer's route (the Autoencoder's
+        # 256-512-channel final layers, and the fp32 parity mode above 32).  The reconstruction seed
+        # is the mean-MSE one, so not for IWAE's per-sample weights (S > 1 keeps the head kernels).
+        # VAE_WIDE_HEAD=1 keeps the conv-GEMM route for 64/128 channels (A/B timing).
+        head_mfma = (T == torch.bfloat16 and img == 64 and h[0] in (64, 128)
+                     and not os.environ.get("VAE_WIDE_HEAD"))
+        self.wide_head = h[0] > 32 and self.S == 1 and not head_mfma
 
         # -------- buffers
         f32 = dict(dtype=torch.float32, device=dev)

@@ -12,6 +12,7 @@
 #   bench            default bench line (driver's command: N=1, CPU baseline included)
 #   quick            VanillaVAE bench, 200 steps, no CPU baseline, per-call breakdown
 #   qenv:V=x,W=y     the quick bench with environment overrides (tunable sweeps)
+#   aenv:V=x:A:B     the same as arch:A:B with environment overrides
 #   arch:A:B         bench --arch A --batch B (betaH, iwae, vq, ae_big ...), no CPU baseline
 #   archcpu:A:B      the same with the CPU baseline legs (the oracle on the host cores)
 #   prof             rocprofv3 --kernel-trace --stats over a short VanillaVAE bench
@@ -63,7 +64,7 @@ pmc() {   # name bench-args...   (one counter group per run: rocprofv3 does not 
 }
 
 for step in "$@"; do
-  IFS=: read -r kind a1 a2 <<< "$step"
+  IFS=: read -r kind a1 a2 a3 <<< "$step"
   case $kind in
     tests) if [ -n "$a1" ]; then run tests_${a1//[^A-Za-z0-9]/_} 900 $PT -k "$a1"; else run tests 900 $PT; fi ;;
     tenv) run tenv_${a1//[=,]/_} 900 env ${a1//,/ } $PT -k "$a2" ;;
@@ -71,6 +72,7 @@ for step in "$@"; do
     bench) run bench 400 python3 -u bench.py ;;
     quick) run quick 300 python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --kernel-breakdown ;;
     qenv) run qenv_${a1//[=,]/_} 300 env ${a1//,/ } python3 -u bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-dropin ;;
+    aenv) run aenv_${a1//[=,]/_}_${a2}_${a3} 300 env ${a1//,/ } python3 -u bench.py --arch $a2 --batch $a3 --steps 100 --warmup 10 --no-cpu-baseline ;;
     arch) run arch_${a1}_${a2} 300 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --no-cpu-baseline --kernel-breakdown ;;
     archcpu) run archcpu_${a1}_${a2} 400 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --kernel-breakdown ;;
     prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;

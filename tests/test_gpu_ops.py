@@ -222,12 +222,17 @@ def test_linear_all(dtype):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("fused", [False, True])
-def test_head_fwd_bwd(dtype, fused):
-    """final Conv2d(32->3,k3,s1,p1)+Tanh and MSE vs autograd (vanilla_vae.py:73-75, :140);
-    fused: vae_head_bwd (data + filter in one pass, per-block partials summed from a workspace)."""
+@pytest.mark.parametrize("C,N", [(32, 2), (64, 2), (128, 2), (128, 9)])
+def test_head_fwd_bwd(dtype, fused, C, N):
+    """final Conv2d(C->3,k3,s1,p1)+Tanh and MSE vs autograd (vanilla_vae.py:73-75, :140;
+    autoencoder.py:84-86 with C = 128, configs/big_ae.yaml); fused: vae_head_bwd (data + filter in
+    one pass, per-block partials summed from a workspace).  C = 64 / 128 run the MFMA head kernels
+    in bf16 only (N = 9 at C = 128: 288 tiles, more than the persistent backward's 256 workgroups)."""
+    if C != 32 and dtype != torch.bfloat16:
+        pytest.skip("64/128-channel heads: bf16 MFMA kernels (fp32 plans take the conv-GEMM route)")
     L = _L()
     torch.manual_seed(6)
-    N, C, H = 2, 32, 64
+    H = 64
     y_prev = torch.randn(N, C, H, H).requires_grad_()
     gam = 0.8 + 0.4 * torch.rand(C); bet = torch.rand(C) * 0.2 - 0.1
     gp = gam.clone().requires_grad_(); bp = bet.clone().requires_grad_()
@@ -254,15 +259,36 @@ def test_head_fwd_bwd(dtype, fused):
     a.dw = dw.data_ptr(); a.db = db.data_ptr()
     if fused:
         ws = give_workspace(a, "vae_head_bwd")
+    lib = L.load()
+    lib.vae_launch_log(1)
     L.call("vae_head_fwd", ctypes.byref(a), _stream())
     if fused:
         L.call("vae_head_bwd", ctypes.byref(a), _stream())
     else:
         L.call("vae_head_bwd_data", ctypes.byref(a), _stream())
         L.call("vae_head_bwd_filter", ctypes.byref(a), _stream())
+    lib.vae_launch_log(0)
     torch.cuda.synchronize()
+    if dtype == torch.bfloat16:
+        need = lib.vae_launch_log_names(None, 0)
+        buf = ctypes.create_string_buffer(int(need))
+        lib.vae_launch_log_names(buf, need)
+        assert f"head_fwd_mfma<{C}>".encode() in buf.value, buf.value
+        assert f"head_bwd_mfma<{C}>".encode() in buf.value, buf.value
     t = tol(dtype)
-    assert rel(recon.cpu(), rec.detach()) < t
+    if dtype == torch.bfloat16:
+        # the kernel's operands are bf16 (stored y, the activation it stages, the weights), so its
+        # pre-tanh error grows as sqrt(9 C) of bf16 rounding (C = 128: up to 0.03 of max); against
+        # the same rounding emulated only the fp32 summation order differs
+        mean = y_prev.detach().mean((0, 2, 3)); var = y_prev.detach().var((0, 2, 3), unbiased=False)
+        ta = gam / torch.sqrt(var + 1e-5); tb = bet - mean * ta
+        z_b = y_prev.detach().to(torch.bfloat16).float() * ta.view(1, -1, 1, 1) + tb.view(1, -1, 1, 1)
+        act_b = F.leaky_relu(z_b, 0.01).to(torch.bfloat16).double()
+        w_b = w.detach().to(torch.bfloat16).double()
+        rec_b = torch.tanh(F.conv2d(act_b, w_b, b.detach().double(), padding=1)).float()
+        assert rel(recon.cpu(), rec_b) < 1e-3
+        assert abs(sse.sum().item() - ((rec_b - tgt) ** 2).sum().item()) < 1e-3 * ((rec_b - tgt) ** 2).sum().item()
+    assert rel(recon.cpu(), rec.detach()) < t * (C / 32) ** 0.5
     assert abs(sse.sum().item() / rec.numel() - loss.item()) < t * loss.item()
     assert rel(dw.permute(0, 3, 1, 2).cpu(), w.grad) < 5 * t
     assert rel(db.cpu(), b.grad) < 5 * t
