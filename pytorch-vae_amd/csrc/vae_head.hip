@@ -35,9 +35,10 @@ namespace {
 constexpr int HW = 64;                 // image width (one tile row)
 constexpr int NCO = 3;
 
-template <int HC>
+// HC: channels one workgroup stages (its LDS tile, fragments); ROWS: image rows per tile
+template <int HC, int ROWS_>
 struct HT {
-  static constexpr int ROWS = HC >= 128 ? 2 : 4;       // image rows per tile
+  static constexpr int ROWS = ROWS_;
   static constexpr int TR = ROWS + 2, TCOLS = HW + 2, TPIX = TR * TCOLS;   // tile with halo
   static constexpr int CH = HC / 8;                    // 16-byte channel chunks per pixel
   static constexpr int SW = CH >= 8 ? 7 : CH - 1;      // chunk XOR-swizzle mask
@@ -80,7 +81,8 @@ __device__ __forceinline__ rsrc_t rsrc(const void* p, uint32_t bytes) {
 // byte offset of (tile pixel, 16-byte channel chunk) in the act tile
 template <int HC>
 __device__ __forceinline__ int act_off(int trow, int tcol, int chunk) {
-  return (trow * HT<HC>::TCOLS + tcol) * (HC * 2) + ((chunk ^ (tcol & HT<HC>::SW)) << 4);
+  constexpr int SW = HC / 8 >= 8 ? 7 : HC / 8 - 1;
+  return (trow * (HW + 2) + tcol) * (HC * 2) + ((chunk ^ (tcol & SW)) << 4);
 }
 
 // XCD-aware order (a permutation of [0, nb)): the nb / 8 workgroups of XCD x = b % 8 take one
@@ -95,35 +97,41 @@ __device__ __forceinline__ float bf2f(uint32_t bits16) { return __uint_as_float(
 // Per-channel BN coefficients in LDS (from vae_bn_finalize's table when present).
 // Without a precomputed table the workgroup reduces the producer's replicated statistics itself
 // (tab_build; `update_running`: this workgroup also applies the running-statistic update).
-template <int HC>
-__device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq, bool update_running = false) {
-  if (xf.kind == VAE_X_BN_ACT && !xf.table && xf.channels == HC && bn_fast_ok(xf)) {
-    tab_build(xf, Tab{ta, tb, nullptr, tp, tq}, true, update_running);
-    return;
+// Channels [cb0, cb0 + HC) of a CT-channel input (CT > HC: a channel slice of the backward).
+template <int HC, int CT>
+__device__ void head_tables(const vae_xform& xf, float* ta, float* tb, float* tp, float* tq, int cb0,
+                            bool update_running = false) {
+  if constexpr (CT == HC) {
+    if (xf.kind == VAE_X_BN_ACT && !xf.table && xf.channels == HC && bn_fast_ok(xf)) {
+      tab_build(xf, Tab{ta, tb, nullptr, tp, tq}, true, update_running);
+      return;
+    }
   }
   for (int c = threadIdx.x; c < HC; c += blockDim.x) {
+    const int cg = cb0 + c;
     if (xf.kind != VAE_X_BN_ACT) { ta[c] = 1.f; tb[c] = 0.f; tp[c] = 0.f; tq[c] = 0.f; continue; }
     if (xf.table) {
-      ta[c] = xf.table[c]; tb[c] = xf.table[HC + c]; tp[c] = xf.table[2 * HC + c]; tq[c] = xf.table[3 * HC + c];
+      ta[c] = xf.table[cg]; tb[c] = xf.table[CT + cg]; tp[c] = xf.table[2 * CT + cg]; tq[c] = xf.table[3 * CT + cg];
     } else {
       float mean, invstd, var;
-      bn_moments(xf, c, mean, invstd, var);
-      ta[c] = xf.gamma[c] * invstd; tb[c] = xf.beta[c] - mean * ta[c];
+      bn_moments(xf, cg, mean, invstd, var);
+      ta[c] = xf.gamma[cg] * invstd; tb[c] = xf.beta[cg] - mean * ta[c];
       tp[c] = invstd; tq[c] = -mean * invstd;
       if (update_running && xf.running_mean) {     // (C = 128: 32 statistic replicas, no tab_build)
         const float m = xf.momentum;
         const float unb = xf.count > 1.f ? var * xf.count / (xf.count - 1.f) : var;
-        xf.running_mean[c] = (1.f - m) * xf.running_mean[c] + m * mean;
-        xf.running_var[c] = (1.f - m) * xf.running_var[c] + m * unb;
+        xf.running_mean[cg] = (1.f - m) * xf.running_mean[cg] + m * mean;
+        xf.running_var[cg] = (1.f - m) * xf.running_var[cg] + m * unb;
       }
     }
   }
 }
 
 // Raw y octets of the tile (halo included) -> registers; issued together (out of image: 0).
-template <int HC>
-__device__ __forceinline__ void tile_load(const HeadQ& q, rsrc_t ry, int n, int h0, u32x4 (&raw)[HT<HC>::OCT_PER_T]) {
-  using T = HT<HC>;
+template <int HC, int ROWS, int CT>
+__device__ __forceinline__ void tile_load(const HeadQ& q, rsrc_t ry, int n, int h0, int cb0,
+                                          u32x4 (&raw)[HT<HC, ROWS>::OCT_PER_T]) {
+  using T = HT<HC, ROWS>;
 #pragma unroll
   for (int j = 0; j < T::OCT_PER_T; ++j) {
     const int o = threadIdx.x + 256 * j;
@@ -131,16 +139,16 @@ __device__ __forceinline__ void tile_load(const HeadQ& q, rsrc_t ry, int n, int 
     const int trow = pix / T::TCOLS, tcol = pix - trow * T::TCOLS;
     const int hi = h0 + trow - 1, wi = tcol - 1;
     const bool ok = o < T::OCT && hi >= 0 && hi < q.h && wi >= 0 && wi < HW;
-    const uint32_t off = ok ? (uint32_t)((((n * q.h + hi) * HW + wi) * HC + ch * 8) * 2) : kOOB;
+    const uint32_t off = ok ? (uint32_t)((((n * q.h + hi) * HW + wi) * CT + cb0 + ch * 8) * 2) : kOOB;
     raw[j] = __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0);
   }
 }
 
 // act = lrelu(a*y + b) (0 outside the image) -> bf16 tile in LDS
-template <int HC>
-__device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (&raw)[HT<HC>::OCT_PER_T], char* tile,
+template <int HC, int ROWS>
+__device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (&raw)[HT<HC, ROWS>::OCT_PER_T], char* tile,
                                            const float* ta, const float* tb) {
-  using T = HT<HC>;
+  using T = HT<HC, ROWS>;
 #pragma unroll
   for (int j = 0; j < T::OCT_PER_T; ++j) {
     const int o = threadIdx.x + 256 * j;
@@ -167,9 +175,10 @@ __device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (
 }
 
 // ======================================================================= forward
-template <int HC>
+// One tile per workgroup (C <= 64: 1024 tiles at B = 64, all resident at once).
+template <int HC, int ROWS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_fwd_mfma(HeadQ q) {
-  using T = HT<HC>;
+  using T = HT<HC, ROWS>;
   __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float red[4];
@@ -180,7 +189,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
   const int n = ti / tiles_per_img, h0 = (ti - n * tiles_per_img) * T::ROWS;
   const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
   u32x4 raw[T::OCT_PER_T];
-  tile_load<HC>(q, ry, n, h0, raw);
+  tile_load<HC, ROWS, HC>(q, ry, n, h0, 0, raw);
   const int co = lane & 15, g = lane >> 4;
   // the epilogue's target pixels, in flight with the tile (no global load after the MFMAs)
   f32x4v tgv[T::GPW];
@@ -195,9 +204,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
   // cost ~72 vector-memory instructions per wave at C = 32)
   for (int i = threadIdx.x; i < T::NW; i += 256) wsb[i] = (__bf16)q.wt[i];
   const float bco = co < NCO ? q.bias[co] : 0.f;
-  head_tables<HC>(q.xf, ta, tb, tp, tq, blockIdx.x == 0);
+  head_tables<HC, HC>(q.xf, ta, tb, tp, tq, 0, blockIdx.x == 0);
   __syncthreads();
-  tile_store<HC>(q, h0, raw, tile, ta, tb);
+  tile_store<HC, ROWS>(q, h0, raw, tile, ta, tb);
   // B fragment of (tap t, K-step cc): W[co = lane&15][t][32 cc + 8 (lane>>4) .. +7] (zero for co >= 3);
   // held in registers while they fit (C <= 64), read from LDS per K-step otherwise
   constexpr int KS = 9 * T::CC;
@@ -253,6 +262,140 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
   if (threadIdx.x == 0) atomicAdd(q.sse + n, (red[0] + red[1]) + (red[2] + red[3]));
 }
 
+// C = 128: the taps move into N.  With the 3 outputs as N (the C <= 64 kernel) every MFMA used 3
+// of its 16 columns and every act element was read from LDS once per tap: 9 x 1 KB of A operand
+// per 16 pixels and 32 channels, LDS-bandwidth-bound at C = 128 (52 us at B = 64).  Here
+// out[p][co*9 + t] = sum_c act[p][c] W[co][t][c] runs over every tile pixel p (halo included):
+// N = 27 of 32 columns, K = C, each act element read once; then y[o][co] = sum_t out[o + d_t][co*9+t]
+// gathers the 9 shifted partial sums from LDS (fp32) before tanh / recon / SSE.
+// Grid-stride over tiles (tile_i = k * gridDim.x + XCD-ordered position), two workgroups per CU,
+// the next tile's raw y loaded while the current one computes.
+template <int HC, int ROWS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_fwd_stream(HeadQ q) {
+  using T = HT<HC, ROWS>;
+  constexpr int NPG = (T::TPIX + 15) / 16;          // 16-pixel groups over the whole tile
+  constexpr int OLD = 33;                           // out row stride (floats): conflict-free
+  static_assert(NPG * 16 * OLD * 4 <= T::TPIX * HC * 2, "out rows fit the tile area");
+  static_assert(T::NW * 2 <= T::TPIX * HC * 2, "bf16 weights fit the tile area");
+  __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];   // act; then out[p][33] fp32
+  __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
+  __shared__ float red[4];
+  __bf16* wsb = reinterpret_cast<__bf16*>(tile);    // W[co][tap][c] bf16, before the first tile
+  float* outl = reinterpret_cast<float*>(tile);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int tiles_per_img = q.h / T::ROWS;
+  const int bpos = q.xcd ? head_xcd_order((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
+  u32x4 raw[T::OCT_PER_T];
+  if (bpos < q.tiles) {
+    const int n0 = bpos / tiles_per_img;
+    tile_load<HC, ROWS, HC>(q, ry, n0, (bpos - n0 * tiles_per_img) * T::ROWS, 0, raw);
+  }
+  for (int i = threadIdx.x; i < T::NW; i += 256) wsb[i] = (__bf16)q.wt[i];
+  head_tables<HC, HC>(q.xf, ta, tb, tp, tq, 0, blockIdx.x == 0);
+  __syncthreads();
+  // B fragments (n-frag nf, K-step cc): column n = nf*16 + lane&15 = co*9 + t (n < 27), rows
+  // c = 32 cc + 8 (lane>>4) .. +7
+  bf16x8 bw[2][T::CC];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf) {
+    const int nn = nf * 16 + li, ok = nn < 27 ? 1 : 0, nc = ok ? nn : 0;
+#pragma unroll
+    for (int cc = 0; cc < T::CC; ++cc) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(&wsb[nc * HC + 32 * cc + 8 * g]);
+      bw[nf][cc] = ok ? v : bf16x8{};
+    }
+  }
+  // the gather's (pixel, co) items: idx = threadIdx.x + 256 k over ROWS*64 pixels x 3 channels;
+  // their biases loaded here — a global load inside the tile loop, issued after the next tile's
+  // prefetch, would make its wait drain the prefetch too (vmcnt counts in issue order)
+  constexpr int GI = (T::OWN * NCO + 255) / 256;
+  float bco[GI];
+#pragma unroll
+  for (int k = 0; k < GI; ++k) {
+    const int idx = threadIdx.x + 256 * k;
+    bco[k] = idx < T::OWN * NCO ? q.bias[idx / T::OWN] : 0.f;
+  }
+  for (int tile_i = bpos; tile_i < q.tiles; tile_i += gridDim.x) {
+    const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * T::ROWS;
+    float tgt[GI];
+#pragma unroll
+    for (int k = 0; k < GI; ++k) {
+      const int idx = threadIdx.x + 256 * k, co = idx / T::OWN, pix = idx - co * T::OWN;
+      tgt[k] = idx < T::OWN * NCO
+                   ? q.target[(((long)(n / q.samples) * NCO + co) * q.h + h0 + pix / HW) * HW + (pix % HW)]
+                   : 0.f;
+    }
+    __syncthreads();                      // the weights / previous tile's out rows are consumed
+    tile_store<HC, ROWS>(q, h0, raw, tile, ta, tb);
+    __syncthreads();
+    {
+      const int nx = tile_i + gridDim.x;
+      if (nx < q.tiles) {
+        const int n1 = nx / tiles_per_img;
+        tile_load<HC, ROWS, HC>(q, ry, n1, (nx - n1 * tiles_per_img) * T::ROWS, 0, raw);
+      }
+    }
+    // out = act x W over the tile's pixel groups grp = wave + 4 k
+    constexpr int GW = (NPG + 3) / 4;
+    f32x4v acc[GW][2];
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      acc[k][0] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      acc[k][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      const int grp = wave + 4 * k;
+      if (grp < NPG) {
+        int p = grp * 16 + li;
+        p = p < T::TPIX ? p : T::TPIX - 1;          // (rows past the tile: never gathered)
+        const int trow = p / T::TCOLS, tcol = p - trow * T::TCOLS;
+#pragma unroll
+        for (int cc = 0; cc < T::CC; ++cc) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(tile + act_off<HC>(trow, tcol, g + 4 * cc));
+          acc[k][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][cc], acc[k][0], 0, 0, 0);
+          acc[k][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][cc], acc[k][1], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();                      // every wave is done with the act tile
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      const int grp = wave + 4 * k;
+      if (grp < NPG) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = grp * 16 + 4 * g + i;
+          outl[p * OLD + li] = acc[k][0][i];
+          outl[p * OLD + 16 + li] = acc[k][1][i];
+        }
+      }
+    }
+    __syncthreads();
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < GI; ++k) {
+      const int idx = threadIdx.x + 256 * k;
+      if (idx < T::OWN * NCO) {
+        const int co = idx / T::OWN, pix = idx - co * T::OWN, row = pix / HW, col = pix - row * HW;
+        float v = bco[k];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int r = t / 3, s2 = t - 3 * r;
+          v += outl[((row + r) * T::TCOLS + col + s2) * OLD + co * 9 + t];
+        }
+        const float y = tanhf(v);
+        q.recon[(((long)n * NCO + co) * q.h + h0 + row) * HW + col] = y;
+        const float d = y - tgt[k];
+        sq = fmaf(d, d, sq);
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off);
+    if (lane == 0) red[wave] = sq;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(q.sse + n, (red[0] + red[1]) + (red[2] + red[3]));
+  }
+}
+
 // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group gives the address of row q, columns
 // 4p..4p+3; lane i receives column i of the 4 rows (row q in element q).
 typedef __bf16 __attribute__((ext_vector_type(4))) __attribute__((address_space(3))) lds_bf16x4;
@@ -266,9 +409,9 @@ __device__ __forceinline__ bf16x4v tr16_read(const char* generic_lds_addr) {
 // and the arithmetic: ld = (recon y, grad_recon or target)
 struct SeedLd { float y[2][NCO], t[2][NCO]; };
 
-template <int HC>
+template <int ROWS>
 __device__ __forceinline__ void seed_load(const HeadQ& q, int tile_i, SeedLd& ld) {
-  using T = HT<HC>;
+  using T = HT<32, ROWS>;
   const int tiles_per_img = q.h / T::ROWS;
   const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * T::ROWS;
 #pragma unroll
@@ -294,12 +437,18 @@ __device__ __forceinline__ float gseed(const HeadQ& q, int n, const SeedLd& ld, 
   return q.coef[n] * (y - ld.t[j][co]) * (1.f - y * y);   // 0 outside the image (y = t = 0)
 }
 
-// C = 32: registers capped for 2 workgroups per CU (the grid of 512 then runs two tiles in flight
-// per CU).  C >= 64: the LDS holds one workgroup per CU (C = 128: 130 KB), which keeps all 512
-// VGPRs of a SIMD for its wave.
-template <int HC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 64 ? 1 : 2))) head_bwd_mfma(HeadQ q) {
-  using T = HT<HC>;
+// One workgroup = one tile x HC of the CT input channels (CT / HC channel slices: the C = 128
+// head runs as two 64-channel slices, so that a workgroup's LDS — tile, raw-y copy, output
+// staging: 68 KB — leaves room for two per CU; as one 128-channel workgroup per CU it took 119 us
+// at B = 64).  Each slice computes the (cheap, 3-channel) seed itself; the data gradient, its
+// BatchNorm-backward sums and the weight gradient are per channel, so the slices never meet.
+// Registers capped for 2 workgroups per CU; ROWS = 4 at C = 64 keeps one (104 KB of LDS) and all
+// 512 VGPRs of a SIMD for its wave.
+template <int HC, int ROWS, int CT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 64 && ROWS >= 4 ? 1 : 2)))
+head_bwd_mfma(HeadQ q) {
+  using T = HT<HC, ROWS>;
+  constexpr int NSL = CT / HC;                                              // channel slices
   __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];
   __shared__ __attribute__((aligned(16))) uint2 gsA[T::TPIX];              // [pixel][co0..2, 0] bf16
   __shared__ __attribute__((aligned(16))) __bf16 gsT[4][T::OWN];           // [co][own pixel]
@@ -307,20 +456,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
   __shared__ __attribute__((aligned(16))) char ytile[T::OWN * HC * 2];     // raw y of the own pixels
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
   __shared__ float r1[4][HC], r2[4][HC], rdb[4][NCO];
-  __shared__ bf16x8 bdl[HT<HC>::NF > 4 ? 2 * HT<HC>::NF * 64 : 1];      // [ks][nf][lane] (C = 128)
-  // the fp32 weights pass through the output staging area before the first tile (27 C floats
-  // in 128 C bytes)
+  __shared__ bf16x8 bdl[T::NF > 2 ? 2 * T::NF * 64 : 1];                   // [ks][nf][lane] (HC >= 64)
+  // the fp32 weights of the slice pass through the output staging area before the first tile
+  // (27 HC floats in 128 HC bytes)
   float* wsh = reinterpret_cast<float*>(&gst[0][0]);
   static_assert(T::NW * 4 <= 4 * 16 * HC * 2, "weights fit the staging area");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int tiles_per_img = q.h / T::ROWS;
-  const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * HC * 2));
-  // tile_i = k * gridDim.x + bpos: at every step the workgroups of one XCD hold consecutive tiles
+  const rsrc_t ry = rsrc(q.x, (uint32_t)((long)q.n * q.h * HW * CT * 2));
+  // position bpos = slice * gsl + local, tile_i = local + k * gsl: at every step the workgroups of
+  // one XCD hold consecutive tiles of one slice (the host makes gridDim.x a multiple of 8 NSL)
   const int bpos = q.xcd ? head_xcd_order((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int gsl = (int)gridDim.x / NSL;
+  const int slice = bpos / gsl, local = bpos - slice * gsl, cb0 = slice * HC;
 
-  for (int i = threadIdx.x; i < T::NW; i += 256) wsh[i] = q.wt[i];
-  // filter accumulators: this wave's n-frags f = wave + 4*i (9 C / 16 n-frags of 16 over (tap, c))
+  for (int i = threadIdx.x; i < T::NW; i += 256) {
+    const int ct = i / HC, c = i - ct * HC;                                 // ct = co * 9 + tap
+    wsh[i] = q.wt[ct * CT + cb0 + c];
+  }
+  // filter accumulators: this wave's n-frags f = wave + 4*i (9 HC / 16 n-frags of 16 over (tap, c))
   f32x4v accw[T::NFW];
 #pragma unroll
   for (int i = 0; i < T::NFW; ++i) accw[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -328,21 +483,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
 #pragma unroll
   for (int nf = 0; nf < T::NF; ++nf) { s1[nf] = 0.f; s2[nf] = 0.f; }
 
-  head_tables<HC>(q.xf, ta, tb, tp, tq);
+  head_tables<HC, CT>(q.xf, ta, tb, tp, tq, cb0);
   // software pipeline: the raw y tile and the seed inputs of the next tile are loaded while
   // this tile's MFMAs run (one or two workgroups per CU leave few other waves to hide the latency)
   u32x4 raw[T::OCT_PER_T];
   SeedLd sld;
-  if (bpos < q.tiles) {
-    const int n0 = bpos / tiles_per_img;
-    tile_load<HC>(q, ry, n0, (bpos - n0 * tiles_per_img) * T::ROWS, raw);
-    seed_load<HC>(q, bpos, sld);
+  if (local < q.tiles) {
+    const int n0 = local / tiles_per_img;
+    tile_load<HC, ROWS, CT>(q, ry, n0, (local - n0 * tiles_per_img) * T::ROWS, cb0, raw);
+    seed_load<ROWS>(q, local, sld);
   }
   __syncthreads();
   // dgrad B fragments: B[k = tap*4 + co][n = c] = W[co][tap][c], k-step ks, n-frag nf — in
-  // registers up to C = 64; at C = 128 (64 more VGPRs than the wave has: 146 spilled) they are
-  // built once into LDS and read per use
-  constexpr bool BDREG = T::NF <= 4;
+  // registers at HC = 32; wider slices (in registers: 28 VGPRs spilled at HC = 64 under the
+  // two-workgroup cap) build them once into LDS and read them per use
+  constexpr bool BDREG = T::NF <= 2;
   bf16x8 bd[2][BDREG ? T::NF : 1];
   if constexpr (BDREG) {
 #pragma unroll
@@ -367,7 +522,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
       bdl[idx] = v;
     }
   }
-  for (int tile_i = bpos; tile_i < q.tiles; tile_i += gridDim.x) {
+  for (int tile_i = local; tile_i < q.tiles; tile_i += gsl) {
     const int n = tile_i / tiles_per_img, h0 = (tile_i - n * tiles_per_img) * T::ROWS;
     // gseed over the halo tile: threads walk pixels (2 per thread)
     float gv[2][NCO];
@@ -379,7 +534,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
       for (int c2 = 0; c2 < NCO; ++c2) gv[j][c2] = gseed(q, n, sld, j, c2);
     }
     __syncthreads();                    // previous tile's LDS reads done (and tables / weights read)
-    tile_store<HC>(q, h0, raw, tile, ta, tb);
+    tile_store<HC, ROWS>(q, h0, raw, tile, ta, tb);
     // raw y (pre-BN) of the own pixels for the data epilogue, from the same registers:
     // [own pixel][C] bf16, 16-byte chunks XOR-swizzled by the pixel
     if (q.data) {
@@ -412,11 +567,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
     }
     __syncthreads();
     {
-      const int nx = tile_i + gridDim.x;
+      const int nx = tile_i + gsl;
       if (nx < q.tiles) {
         const int n1 = nx / tiles_per_img;
-        tile_load<HC>(q, ry, n1, (nx - n1 * tiles_per_img) * T::ROWS, raw);
-        seed_load<HC>(q, nx, sld);
+        tile_load<HC, ROWS, CT>(q, ry, n1, (nx - n1 * tiles_per_img) * T::ROWS, cb0, raw);
+        seed_load<ROWS>(q, nx, sld);
       }
     }
 
@@ -470,11 +625,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
           }
         }
         __builtin_amdgcn_wave_barrier();
-        // 16 pixels x 2C B contiguous (NHWC): 16 B per lane per 1 KB
+        // 16 pixels x HC channels (NHWC, pixel stride CT): 16 B per lane per 1 KB
 #pragma unroll
         for (int j = 0; j < HC / 32; ++j) {
-          const u32x4 v = *reinterpret_cast<const u32x4*>(&gst[wave][lane * 8 + 512 * j]);
-          *reinterpret_cast<u32x4*>(q.dx + (((long)n * q.h + hh) * HW + c0) * HC + lane * 8 + 512 * j) = v;
+          const int e = lane * 8 + 512 * j, px = e / HC, c = e - px * HC;
+          const u32x4 v = *reinterpret_cast<const u32x4*>(&gst[wave][e]);
+          *reinterpret_cast<u32x4*>(q.dx + (((long)n * q.h + hh) * HW + c0 + px) * CT + cb0 + c) = v;
         }
         __builtin_amdgcn_wave_barrier();
       }
@@ -482,8 +638,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
 
     if (q.filter) {
       // ---- dW partials: M = co (rows 0..2 of 16), N = (tap, c), K = the own pixels
-      // (C = 128: one K-step at a time — unrolled, the scheduler hoisted all 144 transposed reads)
-      constexpr int KU = T::NF > 4 ? 1 : T::OWN / 32;
+      // (HC >= 64: one K-step at a time — unrolled, the scheduler hoisted every transposed read
+      // of the tile: 146 VGPRs spilled at HC = 128)
+      constexpr int KU = T::NF >= 4 ? 1 : T::OWN / 32;
 #pragma unroll KU
       for (int ks = 0; ks < T::OWN / 32; ++ks) {
         const int k0 = ks * 32 + 8 * g;                 // this lane group's 8 pixels
@@ -529,8 +686,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
   if (q.data && threadIdx.x < HC) {
     const int c = threadIdx.x;
     const long roff = q.sum_reps > 1 ? (long)(blockIdx.x % q.sum_reps) * q.sum_rstride : 0;
-    atomicAdd(q.dbeta + roff + c, (r1[0][c] + r1[1][c]) + (r1[2][c] + r1[3][c]));
-    atomicAdd(q.dgamma + roff + c, (r2[0][c] + r2[1][c]) + (r2[2][c] + r2[3][c]));
+    atomicAdd(q.dbeta + roff + cb0 + c, (r1[0][c] + r1[1][c]) + (r1[2][c] + r1[3][c]));
+    atomicAdd(q.dgamma + roff + cb0 + c, (r2[0][c] + r2[1][c]) + (r2[2][c] + r2[3][c]));
   }
 #pragma unroll
   for (int c2 = 0; c2 < NCO; ++c2) {
@@ -539,23 +696,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
     if (lane == 0) rdb[wave][c2] = v;
   }
   __syncthreads();
-  if (q.filter && threadIdx.x < NCO && q.db) {
+  // the bias gradient from slice 0 only (every slice summed the same seeds)
+  if (q.filter && threadIdx.x < NCO && q.db && slice == 0) {
     const float v = (rdb[0][threadIdx.x] + rdb[1][threadIdx.x]) + (rdb[2][threadIdx.x] + rdb[3][threadIdx.x]);
-    if (q.slab) q.slab[(long)blockIdx.x * T::SLAB_COLS + T::NW + threadIdx.x] = v;
+    if (q.slab) q.slab[(long)bpos * T::SLAB_COLS + T::NW + threadIdx.x] = v;
     else atomicAdd(q.db + threadIdx.x, v);
   }
   if (q.filter) {
-    // dW[co][tap][c]: lane li = column within the n-frag, rows 4g+i = co (g == 0, i < 3 real)
-    float* out = q.slab ? q.slab + (long)blockIdx.x * T::SLAB_COLS : q.dw;
+    // dW[co][tap][c]: lane li = column within the n-frag, rows 4g+i = co (g == 0, i < 3 real);
+    // slab rows are positions (a slice's rows contiguous), columns the slice's own (co, tap, c)
 #pragma unroll
     for (int i = 0; i < T::NFW; ++i) {
       const int f = wave + 4 * i;
       if (f >= T::NFR || g != 0) continue;
-      const int nn = f * 16 + li;                       // = tap*C + c
+      const int nn = f * 16 + li;                       // = tap*HC + c
+      const int tap = nn / HC, c = nn - tap * HC;
 #pragma unroll
       for (int e = 0; e < NCO; ++e) {
-        if (q.slab) out[e * 9 * HC + nn] = accw[i][e];
-        else atomicAdd(out + e * 9 * HC + nn, accw[i][e]);
+        if (q.slab) q.slab[(long)bpos * T::SLAB_COLS + e * 9 * HC + nn] = accw[i][e];
+        else atomicAdd(q.dw + (e * 9 + tap) * CT + cb0 + c, accw[i][e]);
       }
     }
   }
@@ -565,9 +724,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 
 // (columns < NW) and db (the NCO columns after): 16 columns x 16 row-parts per workgroup, each
 // part's loads issued together, parts combined in a fixed order (deterministic).
 constexpr int RR_COLS = 16, RR_PARTS = 16, RR_UNROLL = 8;
-template <int HC>
-__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, float* dw, float* db) {
-  using T = HT<HC>;
+template <int HC, int CT>
+__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, float* dw, float* db, int cb0) {
+  using T = HT<HC, 4>;
   __shared__ float red[RR_PARTS][RR_COLS];
   const int cl = threadIdx.x % RR_COLS, part = threadIdx.x / RR_COLS;
   const int c = blockIdx.x * RR_COLS + cl;
@@ -590,15 +749,17 @@ __global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int 
   float t = 0.f;
 #pragma unroll
   for (int i = 0; i < RR_PARTS; ++i) t += red[i][cl];
-  if (c < T::NW) dw[c] += t;
-  else if (db) db[c - T::NW] += t;
+  if (c < T::NW) {
+    const int ct = c / HC, cl = c - ct * HC;          // ct = co * 9 + tap
+    dw[ct * CT + cb0 + cl] += t;
+  } else if (db) {
+    db[c - T::NW] += t;
+  }
 }
-
-inline int head_rows(int c) { return c >= 128 ? HT<128>::ROWS : HT<32>::ROWS; }
 
 bool head_mfma_ok(const vae_head_args* a) {
   return a->dtype == VAE_BF16 && (a->c == 32 || a->c == 64 || a->c == 128) && a->w == HW && a->h > 0 &&
-         a->h % head_rows(a->c) == 0 && a->n > 0 &&
+         a->h % 4 == 0 && a->n > 0 &&
          ((uintptr_t)a->x & 15) == 0 && ((uintptr_t)a->recon & 15) == 0 && ((uintptr_t)a->target & 15) == 0 &&
          (a->x_xf.kind == VAE_X_BN_ACT || a->x_xf.kind == VAE_X_ACT || a->x_xf.kind == VAE_X_NONE);
 }
@@ -615,7 +776,7 @@ int head_xcd() {
 HeadQ head_q(const vae_head_args* a) {
   HeadQ q;
   memset(&q, 0, sizeof(q));
-  q.n = a->n; q.h = a->h; q.samples = a->samples > 0 ? a->samples : 1; q.tiles = a->n * (a->h / head_rows(a->c));
+  q.n = a->n; q.h = a->h; q.samples = a->samples > 0 ? a->samples : 1;   // (q.tiles: per kernel)
   q.xcd = head_xcd();
   q.x = static_cast<const __bf16*>(a->x); q.xf = a->x_xf;
   if (q.xf.channels <= 0) q.xf.channels = a->c;
@@ -627,20 +788,24 @@ HeadQ head_q(const vae_head_args* a) {
   return q;
 }
 
-template <int HC>
-int head_bwd_go(const vae_head_args* a, HeadQ q, int grid, hipStream_t st) {
-  using T = HT<HC>;
+template <int HC, int ROWS, int CT>
+int head_bwd_go(const vae_head_args* a, HeadQ q, int gsl_max, hipStream_t st) {
+  using T = HT<HC, ROWS>;
+  constexpr int NSL = CT / HC;
+  q.tiles = q.n * (q.h / ROWS);
+  const int gsl = q.tiles < gsl_max ? q.tiles : gsl_max;     // workgroups per channel slice
+  const int grid = gsl * NSL;
   const long need = (long)grid * T::SLAB_COLS * 4;
   float* ws = static_cast<float*>(a->workspace);
   if (q.filter && ws && !ws_fits(need, a->workspace_bytes, "head_bwd filter partials")) return VAE_E_BADARG;
   const bool slab = q.filter && ws;
   q.slab = slab ? ws : nullptr;
-  VAE_LAUNCH(head_bwd_mfma<HC>, dim3(grid), dim3(256), 0, st, q);
+  VAE_LAUNCH((head_bwd_mfma<HC, ROWS, CT>), dim3(grid), dim3(256), 0, st, q);
   int rc = check_launch("head_bwd_mfma");
-  if (rc || !q.filter) return rc;
-  if (slab) {
-    VAE_LAUNCH(reduce_rows_kernel<HC>, dim3((T::SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st, (const float*)ws,
-               grid, a->dw, a->db);
+  if (rc || !q.filter || !slab) return rc;
+  for (int sl = 0; sl < NSL && !rc; ++sl) {      // a slice's slab rows are contiguous positions
+    VAE_LAUNCH((reduce_rows_kernel<HC, CT>), dim3((T::SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st,
+               (const float*)ws + (long)sl * gsl * T::SLAB_COLS, gsl, a->dw, sl == 0 ? a->db : nullptr, sl * HC);
     rc = check_launch("reduce_rows");
   }
   return rc;
@@ -648,34 +813,40 @@ int head_bwd_go(const vae_head_args* a, HeadQ q, int grid, hipStream_t st) {
 
 }  // namespace
 
-// Entry points used by vae_misc.hip's C ABI for the bf16 MFMA path.
-int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
-  if (!head_mfma_ok(a)) return kHeadFallback;       // caller falls back to the VALU kernels
-  HeadQ q = head_q(a);
-  switch (a->c) {
-    case 32: VAE_LAUNCH(head_fwd_mfma<32>, dim3(q.tiles), dim3(256), 0, st, q); break;
-    case 64: VAE_LAUNCH(head_fwd_mfma<64>, dim3(q.tiles), dim3(256), 0, st, q); break;
-    default: VAE_LAUNCH(head_fwd_mfma<128>, dim3(q.tiles), dim3(256), 0, st, q); break;
-  }
-  return check_launch("head_fwd_mfma");
-}
-
 // Persistent grid of the backward.  C = 32, swept on MI355X (B=64 step): 128 -> 78.7 us,
 // 192 -> 61.7, 256 -> 45.6, 512 -> 50.5, 1024 -> 61.4 (more blocks means more filter partials to
 // reduce and more halo re-reads; fewer leaves CUs idle).  Re-swept with the tile-ahead loads:
 // 192 -> 50.4 us, 256 -> 38.5, 320 -> 55.6, 384 -> 49.8, 512 -> 43.9 (scripts/gpu_headgrid.sh).
 // r2: with the registers capped for 2 workgroups per CU (amdgpu_waves_per_eu(2)), 512 -> 37.2 us
 // (two tiles in flight per CU), 256 -> 45.1 (the cap's spills without the second workgroup).
-// C >= 64: one workgroup per CU (LDS), so 256.
-constexpr int kHeadGrid = 512, kHeadGridWide = 256;
-// VAE_HEAD_GRID overrides it (tuning sweeps only; read once)
-int head_grid(int c) {
+// C = 64 / 128: 64-channel slices of 2 image rows, two workgroups per CU — 512 workgroups, i.e.
+// 512 per slice (C = 64) or 256 per slice (C = 128).
+constexpr int kHeadGrid = 512;
+// VAE_HEAD_GRID overrides it (workgroups in all; tuning sweeps only; read once)
+int head_grid() {
   static const int g = [] {
     const char* e = getenv("VAE_HEAD_GRID");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 0;
+    return v > 0 ? v : kHeadGrid;
   }();
-  return g > 0 ? g : c == 32 ? kHeadGrid : kHeadGridWide;
+  return g;
+}
+
+// Entry points used by vae_misc.hip's C ABI for the bf16 MFMA path.
+int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {
+  if (!head_mfma_ok(a)) return kHeadFallback;       // caller falls back to the VALU kernels
+  HeadQ q = head_q(a);
+  switch (a->c) {
+    case 32: q.tiles = q.n * (q.h / 4); VAE_LAUNCH((head_fwd_mfma<32, 4>), dim3(q.tiles), dim3(256), 0, st, q); break;
+    case 64: q.tiles = q.n * (q.h / 4); VAE_LAUNCH((head_fwd_mfma<64, 4>), dim3(q.tiles), dim3(256), 0, st, q); break;
+    default: {
+      q.tiles = q.n * (q.h / 2);
+      const int grid = q.tiles < head_grid() ? q.tiles : head_grid();   // two workgroups per CU
+      VAE_LAUNCH((head_fwd_stream<128, 2>), dim3(grid), dim3(256), 0, st, q);
+      break;
+    }
+  }
+  return check_launch("head_fwd_mfma");
 }
 
 // data / filter: which halves of the backward to run.  The filter half writes per-block partials
@@ -685,11 +856,10 @@ int head_bwd_mfma_launch(const vae_head_args* a, bool data, bool filter, hipStre
   if (data && a->dx_epi.kind != VAE_X_BN_ACT) return kHeadFallback;   // the fused epilogue is BatchNorm+LReLU
   HeadQ q = head_q(a);
   q.data = data; q.filter = filter;
-  const int grid = q.tiles < head_grid(a->c) ? q.tiles : head_grid(a->c);
   switch (a->c) {
-    case 32: return head_bwd_go<32>(a, q, grid, st);
-    case 64: return head_bwd_go<64>(a, q, grid, st);
-    default: return head_bwd_go<128>(a, q, grid, st);
+    case 32: return head_bwd_go<32, 4, 32>(a, q, head_grid(), st);
+    case 64: return head_bwd_go<64, 2, 64>(a, q, head_grid(), st);
+    default: return head_bwd_go<64, 2, 128>(a, q, head_grid() / 2, st);
   }
 }
 

@@ -273,8 +273,10 @@ def test_head_fwd_bwd(dtype, fused, C, N):
         need = lib.vae_launch_log_names(None, 0)
         buf = ctypes.create_string_buffer(int(need))
         lib.vae_launch_log_names(buf, need)
-        assert f"head_fwd_mfma<{C}>".encode() in buf.value, buf.value
-        assert f"head_bwd_mfma<{C}>".encode() in buf.value, buf.value
+        fwd = f"head_fwd_stream<{C}," if C == 128 else f"head_fwd_mfma<{C},"
+        bwd = "head_bwd_mfma<64, 2, 128>" if C == 128 else f"head_bwd_mfma<{C},"
+        assert fwd.encode() in buf.value, buf.value
+        assert bwd.encode() in buf.value, buf.value
     t = tol(dtype)
     if dtype == torch.bfloat16:
         # the kernel's operands are bf16 (stored y, the activation it stages, the weights), so its
