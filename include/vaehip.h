@@ -209,8 +209,9 @@ typedef struct vae_linear_args {
   uint32_t* bn_counter;
 } vae_linear_args;
 
-/* Final layer of the decoder: Conv2d(C->3, k3, s1, p1) + Tanh (vanilla_vae.py:73-75) and the
- * reconstruction term of the ELBO (F.mse_loss, vanilla_vae.py:140) — VALU kernels. */
+/* Final layer of the decoder: Conv2d(C->3, k3, s1, p1) + Tanh (vanilla_vae.py:73-75,
+ * autoencoder.py:84-86) and the reconstruction term of the ELBO (F.mse_loss, vanilla_vae.py:140).
+ * bf16 with w = 64 and C = 32, 64 or 128: MFMA kernels (vae_head.hip); otherwise VALU kernels. */
 typedef struct vae_head_args {
   int32_t dtype;
   int32_t n, h, w, c;      /* input of the conv (NHWC, pre-activation, see x_xf) */

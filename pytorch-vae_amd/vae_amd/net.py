@@ -25,7 +25,9 @@ from . import _lib as L
 from .layout import Layout, default_init, reference_key_order, vanilla_layout
 
 SLOPE = 0.01         # nn.LeakyReLU default
-MAT_MIN_FLOPS = 4e9  # layers at least this large take materialised operands (StepPlan.big_layer)
+# layers at least this large take materialised operands (StepPlan.big_layer); VAE_MAT_MIN
+# overrides it (A/B sweeps only)
+MAT_MIN_FLOPS = float(os.environ.get("VAE_MAT_MIN", "4e9"))
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 
