@@ -22,6 +22,7 @@
 #   pmc:A:B          the same for --arch A --batch B
 #   kprobe           per-block phase probe (needs `make probe`)
 #   kbench[:ARGS]    per-launch microbench under a kernel trace (tools/kbench.py, ARGS comma-separated)
+#   headbench        the decoder-head kernels back to back (tools/headbench.py): fwd, bwd, bwd halves
 #   c3bench[:ENV]    the VQ-VAE image-tile kernels back to back (tools/c3bench.py), ENV e.g.
 #                    VAE_C3_DBG=5 (phase ablation: 1 no chunk loads, 2 no MFMAs, 4 no LDS stores)
 #   c3trace          tools/c3bench.py under rocprofv3 --kernel-trace --stats
@@ -77,6 +78,7 @@ for step in "$@"; do
     archcpu) run archcpu_${a1}_${a2} 400 python3 -u bench.py --arch $a1 --batch $a2 --steps 100 --warmup 10 --kernel-breakdown ;;
     prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;
     pmc) if [ -n "$a1" ]; then pmc pmc_$a1 --arch $a1 --batch $a2; else pmc pmc; fi ;;
+    headbench) run headbench 200 python3 -u tools/headbench.py ;;
     kprobe) run kprobe 200 env VAE_HIP_LIB=probe python3 -u tools/kprobe.py --out $O/${TAG}_kp.json ;;
     kbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
                -d $O/${TAG}_kb -o kb -- python3 $R/tools/kbench.py --out $O/${TAG}_kb_groups.json ${a1//,/ }) \
