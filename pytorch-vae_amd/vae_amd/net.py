@@ -407,12 +407,14 @@ class StepPlan:
         self._add(lst, "vae_bn_finalize", a)
 
     # ---- materialised transforms for the large layers (vaehip.h vae_bn_apply + vae_bgemm.hip)
-    def big_layer(self, flops: float) -> bool:
+    def big_layer(self, flops: float, cin: int, cout: int) -> bool:
         """A layer whose GEMMs take materialised (transform-free) operands: bf16 training, >= 4 GFLOP
-        per pass (the Autoencoder's wide layers; the VanillaVAE's are 0.6).  VAE_NO_MAT=1 keeps every
-        transform fused into its consumers (A/B timing)."""
+        per pass and >= 128 channels on both sides (the Autoencoder's wide layers, whose GEMMs run on
+        the 128 x 128 LDS-DMA tiles; the VanillaVAE's are 0.6 GFLOP, and IWAE's 32-channel final ConvT
+        reaches 6 GFLOP at B*S = 320 but stays on its own kernels: materialised it measured 1.10 vs
+        1.04 ms/step).  VAE_NO_MAT=1 keeps every transform fused into its consumers (A/B timing)."""
         return (self.net.dtype == torch.bfloat16 and self.training and flops >= MAT_MIN_FLOPS
-                and not os.environ.get("VAE_NO_MAT"))
+                and min(cin, cout) >= 128 and not os.environ.get("VAE_NO_MAT"))
 
     def mat_act(self, F, prefix: str, t: torch.Tensor, count: int):
         """lrelu(BN(t)) written once (vae_bn_apply: running statistics updated there, the forward's
@@ -513,7 +515,7 @@ class StepPlan:
             elif i == 0:
                 a.x_nchw_f32 = 1
                 a.x = self.x.data_ptr()
-            elif self.big_layer(2.0 * B * (sp // 2) ** 2 * h[i] * 9 * h[i - 1]):
+            elif self.big_layer(2.0 * B * (sp // 2) ** 2 * h[i] * 9 * h[i - 1], h[i - 1], h[i]):
                 a.x = self.mat_act(F, enc_pre[i - 1], self.enc[i - 1], cnt(self.enc[i - 1])).data_ptr()
             else:
                 a.x = self.enc[i - 1].data_ptr()
@@ -568,7 +570,7 @@ class StepPlan:
             cout = r[i + 1] if i < len(r) - 1 else r[-1]
             a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
             a.x = prev.data_ptr()
-            if prev_pre is not None and self.big_layer(2.0 * BS * sp * sp * cin * cout * 9):
+            if prev_pre is not None and self.big_layer(2.0 * BS * sp * sp * cin * cout * 9, cin, cout):
                 a.x = self.mat_act(F, prev_pre, prev, cnt(prev)).data_ptr()
             elif prev_pre is not None:
                 a.x_xf = self.bn_xf(prev_pre, L.X_BN_ACT, cnt(prev), running=True)
@@ -651,7 +653,7 @@ class StepPlan:
             self.bn_finalize(Bw, dec_pre[i], 1, cnt(dec_out[i]))
             dy_xf = self.bn_xf(dec_pre[i], L.X_BN_DY, cnt(dec_out[i]), aux=dec_out[i])
             dz = (self.mat_dz(Bw, dec_pre[i], g_dec_out[i], dec_out[i], cnt(dec_out[i]))
-                  if self.big_layer(2.0 * BS * sp * sp * cin * cout * 9) else None)
+                  if self.big_layer(2.0 * BS * sp * sp * cin * cout * 9, cin, cout) else None)
             if dz is not None:
                 dy_xf = L.Xform(kind=L.X_NONE, channels=cout)
             a = L.ConvArgs(dtype=T, n=BS, h=sp, w=sp, c=cin, k=cout, p=2 * sp, q=2 * sp, r=3, stride=2, pad=1)
@@ -740,7 +742,7 @@ class StepPlan:
             self.bn_finalize(Bw, enc_pre[i], 1, cnt(self.enc[i]))
             dy_xf = self.bn_xf(enc_pre[i], L.X_BN_DY, cnt(self.enc[i]), aux=self.enc[i])
             dz = (self.mat_dz(Bw, enc_pre[i], self.g_enc[i], self.enc[i], cnt(self.enc[i]))
-                  if i > 0 and self.big_layer(2.0 * B * (sp // 2) ** 2 * h[i] * 9 * cin) else None)
+                  if i > 0 and self.big_layer(2.0 * B * (sp // 2) ** 2 * h[i] * 9 * cin, cin, h[i]) else None)
             if dz is not None:
                 dy_xf = L.Xform(kind=L.X_NONE, channels=h[i])
             f = L.ConvArgs(dtype=T, n=B, h=sp, w=sp, c=cin, k=h[i], p=sp // 2, q=sp // 2, r=3, stride=2, pad=1)
