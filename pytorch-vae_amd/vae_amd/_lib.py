@@ -15,9 +15,10 @@ import torch  # noqa: F401  (must precede the library: one HIP runtime per proce
 
 LIB_NAME = "libvaehip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
-# diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe)
-if os.environ.get("VAE_HIP_LIB") == "probe":
-    LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_probe.so")
+# diagnostics: VAE_HIP_LIB=probe loads the phase-timestamp build (make -C pytorch-vae_amd/csrc probe);
+# any other value V loads libvaehip_V.so (a build-flag variant for A/B timing)
+if os.environ.get("VAE_HIP_LIB"):
+    LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_%s.so" % os.environ["VAE_HIP_LIB"])
 ABI_VERSION = 21
 
 F32, BF16 = 0, 1

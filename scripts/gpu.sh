@@ -79,6 +79,7 @@ for step in "$@"; do
     prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;
     pmc) if [ -n "$a1" ]; then pmc pmc_$a1 --arch $a1 --batch $a2; else pmc pmc; fi ;;
     headbench) run headbench 200 python3 -u tools/headbench.py ;;
+    hbenv) run hbenv_${a1//[=,]/_} 200 env ${a1//,/ } python3 -u tools/headbench.py ;;
     kprobe) run kprobe 200 env VAE_HIP_LIB=probe python3 -u tools/kprobe.py --out $O/${TAG}_kp.json ;;
     kbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
                -d $O/${TAG}_kb -o kb -- python3 $R/tools/kbench.py --out $O/${TAG}_kb_groups.json ${a1//,/ }) \
