@@ -84,7 +84,7 @@ class TrainStep:
     queued, so it runs on the communication stream while the rest of the backward computes."""
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
-                 nbuckets: int = 4, device_eps: Optional[int] = None):
+                 nbuckets: int = 4, device_eps: Optional[int] = None, force_buckets: bool = False):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -94,7 +94,9 @@ class TrainStep:
         self.world = dist.get_world_size(process_group) if (dist.is_available() and dist.is_initialized()) else 1
         self.use_graph = graph
         self.segments = []                      # (call range) of the backward per bucket
-        if self.world > 1:
+        # force_buckets: the bucketed path (segment graphs, one all-reduce per bucket, the buffer
+        # broadcast) at world size 1 too — how the one-GPU tests run the RCCL branch
+        if self.world > 1 or (force_buckets and self.world == 1 and dist.is_available() and dist.is_initialized()):
             raw = getattr(plan, "bwd_calls_raw", plan.bwd_calls)
             self.buckets = plan_buckets(raw, plan.grads, net.layout, nbuckets)
             if hasattr(plan, "batch_wgrads"):
@@ -133,7 +135,7 @@ class TrainStep:
             if p.loss_kind == L.LOSS_BETA_B:
                 p.num_iter.add_(1.0)
             p._run(p.fwd_calls[skip:], st)
-            if self.world > 1:
+            if self.comm is not None:
                 p.metrics.copy_(p.out)
         lo = 0 if k == 0 else self.buckets[k - 1][0]
         p._run(p.bwd_calls[lo:self.buckets[k][0]], st)
@@ -214,4 +216,4 @@ class TrainStep:
     def loss_terms(self):
         """[loss, Reconstruction_Loss, KLD|VQ_Loss] of the last step: the mean over ranks with more
         than one (what the reference logs, experiment.py:55), else this rank's."""
-        return (self.plan.metrics if self.world > 1 else self.plan.out)[:3].tolist()
+        return (self.plan.metrics if self.comm is not None else self.plan.out)[:3].tolist()
