@@ -6,7 +6,7 @@ the last bucket, rank 0's BatchNorm buffers broadcast).  Two ranks cannot share 
 RCCL, so the multi-rank arithmetic is covered by the gloo tests (test_gpu_dp.py, test_dp_gloo.py);
 this one checks that the RCCL calls run inside the step's stream order and leave the step's
 result unchanged: against the one-graph, collective-free path (fp32 parity mode, VanillaVAE B=16)
-the first step's gradients within 1e-5 relative norm (the bucketed plan batches its weight
+the first step's gradients within 1e-5 relative norm + 1e-6 (the bucketed plan batches its weight
 gradients per segment, so the summation order may differ; measured: a second step's gradients
 differ by up to 1.2e-4 as Adam amplifies that noise on near-zero gradients), the parameters after
 it within 1e-4, the loss terms of two steps within 1e-5."""
@@ -74,12 +74,13 @@ def _worker(port, q):
         q.put((traceback.format_exc(),) + (None,) * 6)
 
 
-def _rel(a, b):
-    """Relative norm of a - b; a gradient that is zero in exact arithmetic (a conv bias in front of
-    a BatchNorm: ~1e-8 of rounding either way) is measured against 1e-3 instead of its own norm."""
+def _err(a, b, rel):
+    """norm(a - b) against rel * norm(b) + 1e-6: the absolute term covers gradients that are zero in
+    exact arithmetic (a conv bias in front of a BatchNorm: 1e-8-sized rounding either way, their
+    difference norm ~1e-7 between the two summation orders); returns (error, bound)."""
     d = float(np.linalg.norm((a.astype(np.float64) - b.astype(np.float64)).ravel()))
     n = float(np.linalg.norm(b.astype(np.float64).ravel()))
-    return d / max(n, 1e-3)
+    return d, rel * n + 1e-6
 
 
 def test_rccl_bucketed_step_matches_one_graph_step():
@@ -92,8 +93,10 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     assert not isinstance(ga, str), ga
     assert nb >= 2
     for k in gb:                          # the first step's gradients
-        assert _rel(ga[k], gb[k]) <= 1e-5, (k, _rel(ga[k], gb[k]))
+        d, bound = _err(ga[k], gb[k], 1e-5)
+        assert d <= bound, (k, d, bound)
     for k in sb:                          # parameters / buffers after it (Adam amplifies the
         if sb[k].dtype.kind == "f":       # summation-order noise of near-zero gradients)
-            assert _rel(sa[k], sb[k]) <= 1e-4, (k, _rel(sa[k], sb[k]))
+            d, bound = _err(sa[k], sb[k], 1e-4)
+            assert d <= bound, (k, d, bound)
     np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-5, atol=0)
