@@ -95,8 +95,12 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     for k in gb:                          # the first step's gradients
         d, bound = _err(ga[k], gb[k], 1e-5)
         assert d <= bound, (k, d, bound)
-    for k in sb:                          # parameters / buffers after it (Adam amplifies the
-        if sb[k].dtype.kind == "f":       # summation-order noise of near-zero gradients)
+    # parameters / buffers after it (Adam amplifies the summation-order noise of near-zero
+    # gradients; a parameter whose gradient is zero in exact arithmetic — the conv biases in front
+    # of a BatchNorm — takes a noise-signed step of up to lr on either side, so it is not compared)
+    noise = {k for k in gb if float(np.linalg.norm(gb[k].astype(np.float64).ravel())) < 1e-6}
+    for k in sb:
+        if sb[k].dtype.kind == "f" and k not in noise:
             d, bound = _err(sa[k], sb[k], 1e-4)
             assert d <= bound, (k, d, bound)
     np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-5, atol=0)
