@@ -9,7 +9,8 @@ result unchanged: against the one-graph, collective-free path (fp32 parity mode,
 the first step's gradients within 1e-4 relative norm + 1e-6 (the bucketed plan batches its weight
 gradients per segment, so the fp32 summation order differs: measured up to 3.2e-5, decoder.3.0.weight;
 a second step's gradients differ by up to 1.2e-4 as Adam amplifies that noise on near-zero
-gradients), the parameters after it within 1e-3, the loss terms of two steps within 1e-4 — a
+gradients), the Adam update of every element whose gradient is clear of that noise equal, the
+BatchNorm buffers within 1e-4, the loss terms of two steps within 1e-4 — a
 broken exchange (a bucket missed, summed twice or raced by the next segment) is an O(1) error."""
 import os
 import socket
@@ -96,12 +97,22 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     for k in gb:                          # the first step's gradients
         d, bound = _err(ga[k], gb[k], 1e-4)
         assert d <= bound, (k, d, bound)
-    # parameters / buffers after it (Adam amplifies the summation-order noise of near-zero
-    # gradients; a parameter whose gradient is zero in exact arithmetic — the conv biases in front
-    # of a BatchNorm — takes a noise-signed step of up to lr on either side, so it is not compared)
-    noise = {k for k in gb if float(np.linalg.norm(gb[k].astype(np.float64).ravel())) < 1e-6}
+    # parameters after it: Adam's first step moves every element by lr * g / (|g| + eps), i.e. by
+    # lr * sign(g) wherever |g| >> eps, so the two runs must agree exactly on every element whose
+    # gradient is clear of the summation-order noise (elements near zero may take the step with
+    # the other sign; parameters whose gradient is zero in exact arithmetic — the conv biases in
+    # front of a BatchNorm — are all noise and not compared)
+    for k in gb:
+        g = np.abs(gb[k].astype(np.float64))
+        if g.max() < 1e-6:
+            continue
+        clear = g > 1e-3 * g.max()
+        assert clear.mean() > 0.2, (k, clear.mean())
+        dmax = float(np.abs(sa[k].astype(np.float64) - sb[k].astype(np.float64))[clear].max())
+        assert dmax <= 1e-6, (k, dmax)
+    # buffers (BatchNorm running statistics): the same batch statistics either way
     for k in sb:
-        if sb[k].dtype.kind == "f" and k not in noise:
-            d, bound = _err(sa[k], sb[k], 1e-3)
+        if k not in gb and sb[k].dtype.kind == "f":
+            d, bound = _err(sa[k], sb[k], 1e-4)
             assert d <= bound, (k, d, bound)
     np.testing.assert_allclose(np.array(ta), np.array(tb), rtol=1e-4, atol=0)
