@@ -3,7 +3,8 @@ DDP) on the one GPU a test box has: a world of one rank over the "nccl" backend 
 step forced onto its bucketed path (engine.TrainStep(force_buckets=True): backward HIP-graph
 segments per gradient bucket, one RCCL all-reduce launched after each, the loss terms riding in
 the last bucket, rank 0's BatchNorm buffers broadcast).  Two ranks cannot share a device under
-RCCL, so the multi-rank arithmetic is covered by the gloo tests (test_gpu_dp.py, test_dp_gloo.py);
+RCCL, so the multi-rank arithmetic is covered by the gloo tests (test_gpu_dp.py, test_dp_gloo.py; this file
+sorts last so that its RCCL process group initialises after every single-process test has run);
 this one checks that the RCCL calls run inside the step's stream order and leave the step's
 result unchanged: against the one-graph, collective-free path (fp32 parity mode, VanillaVAE B=16)
 the first step's gradients within 1e-4 relative norm + 1e-6 (the bucketed plan batches its weight
