@@ -7,8 +7,9 @@ RCCL, so the multi-rank arithmetic is covered by the gloo tests (test_gpu_dp.py,
 sorts last so that its RCCL process group initialises after every single-process test has run);
 this one checks that the RCCL calls run inside the step's stream order and leave the step's
 result unchanged: against the one-graph, collective-free path (fp32 parity mode, VanillaVAE B=16)
-the first step's gradients within 1e-4 relative norm + 1e-6 (the bucketed plan batches its weight
-gradients per segment, so the fp32 summation order differs: measured up to 3.2e-5, decoder.3.0.weight;
+the first step's gradients within 1e-3 relative norm + 1e-6 (the bucketed plan batches its weight
+gradients per segment and the weight-gradient atomics add in run-dependent order: measured 3.2e-5 to
+1.2e-4 between runs, decoder.1.0.weight / decoder.3.0.weight;
 a second step's gradients differ by up to 1.2e-4 as Adam amplifies that noise on near-zero
 gradients), the Adam update of every element whose gradient is clear of that noise within 1e-5
 (measured 1.2e-6 at a 1e-3 x max cut, decoder.1.0.weight; the step is lr = 5e-3), the
@@ -97,7 +98,7 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     assert not isinstance(ga, str), ga
     assert nb >= 2
     for k in gb:                          # the first step's gradients
-        d, bound = _err(ga[k], gb[k], 1e-4)
+        d, bound = _err(ga[k], gb[k], 1e-3)
         assert d <= bound, (k, d, bound)
     # parameters after it: Adam's first step moves every element by lr * g / (|g| + eps), i.e. by
     # lr * sign(g) wherever |g| >> eps, so the two runs must agree exactly on every element whose
