@@ -178,11 +178,6 @@ def kernel_costs(plan, dsz):
             fb = [conv_cost(f, r._obj, dsz) for f, r in ref.calls]
             out.append((fn, ref, sum(c[0] for c in fb), sum(c[1] for c in fb)))
             continue
-        if isinstance(ref, L.PairCall):             # one layer's data + weight gradient in one grid
-            dfn = "vae_conv2d_bwd_data" if ref.kind == L.LAYER_CONV2D else "vae_convT2d_bwd_data"
-            fb = [conv_cost(dfn, ref.data._obj, dsz), conv_cost(dfn.replace("_data", "_filter"), ref.filter._obj, dsz)]
-            out.append((fn, ref, sum(c[0] for c in fb), sum(c[1] for c in fb)))
-            continue
         a = ref._obj
         if isinstance(a, L.ConvArgs):
             f, b = conv_cost(fn, a, dsz)

@@ -118,8 +118,17 @@ __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, cons
 // The per-tap weight-gradient GEMM of workgroup `bid` of its problem, operand tiles at `lds`
 // (wgemm_lds_bytes) — called by wgemm_kernel (one problem per launch) and by wg_group_kernel
 // (several layers' weight gradients in one launch, vae_wgrad_batch.hip).
+// (clk: VAE_PROBE diagnostics — thread 0 records cycle counts after the prologue and the K loop)
+#ifdef VAE_PROBE
+#define WG_MARK(i) do { if (clk && threadIdx.x == 0) clk[i] = __builtin_readcyclecounter(); } while (0)
+#else
+#define WG_MARK(i) do { } while (0)
+#endif
+// nunits > 1 (the grouped launch, vae_wgrad_batch.hip): the workgroup runs work units bid0 ..
+// bid0 + nunits - 1 of its layer one after another, building the BatchNorm tables once.
 template <int BM, int BJ, int XU, int XV>
-__device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, char* lds) {
+__device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid0, char* lds,
+                                           unsigned long long* clk = nullptr, const int nunits = 1) {
   constexpr int KP = wg_kp<BM>();
   constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int CU = BM / 8, CV = BJ / 8;              // 16-byte chunks per pixel row
@@ -141,22 +150,29 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, cha
   const int wm = wave >> 1, wn = wave & 1;
   const int gm = (p.M + BM - 1) / BM, gj = (p.J + BJ - 1) / BJ;
   const int per_slice = gm * gj * p.R * p.R;
-  const int slice = bid / per_slice;
-  int t = bid - slice * per_slice;
-  const int tj = t % gj; t /= gj;
-  const int tmi = t % gm;
-  const int tap = t / gm;
-  const int r = (int)p.fd_r.div(tap), s = tap - r * p.R;
-  const int m0 = tmi * BM, j0 = tj * BJ;
   const long npix = (long)p.n * p.hu * p.wu;
-  const long k0 = (long)slice * p.kper;
-  const long k1 = min(npix, k0 + p.kper);
-  const int nsteps = (int)((k1 - k0 + KP - 1) / KP);
-
   // per-thread chunk coordinates (all of a thread's rows share the chunk column)
   const int cu = tid % CU, ru0 = tid / CU, cv = tid % CV, rv0 = tid / CV;
-  const int chu = m0 + cu * 8, chv = j0 + cv * 8;
-  const bool cu_ok = chu < p.M && ru0 < KP, cv_ok = chv < p.J && rv0 < KP;
+
+  // the work unit: K slice, tap, output tile (re-decoded per unit)
+  int slice, tap, r, s, m0, j0, chu, chv, nsteps;
+  long k0, k1;
+  bool cu_ok, cv_ok;
+  auto decode = [&](int bid) {
+    slice = bid / per_slice;
+    int t = bid - slice * per_slice;
+    const int tj = t % gj; t /= gj;
+    const int tmi = t % gm;
+    tap = t / gm;
+    r = (int)p.fd_r.div(tap); s = tap - r * p.R;
+    m0 = tmi * BM; j0 = tj * BJ;
+    k0 = (long)slice * p.kper;
+    k1 = min(npix, k0 + p.kper);
+    nsteps = (int)((k1 - k0 + KP - 1) / KP);
+    chu = m0 + cu * 8; chv = j0 + cv * 8;
+    cu_ok = chu < p.M && ru0 < KP; cv_ok = chv < p.J && rv0 < KP;
+  };
+  decode(bid0);
   const Src<__bf16> su = make_src<__bf16>(p.u, p.u_bytes, p.u_xf);
   const Src<__bf16> sv = make_src<__bf16>(p.v, p.v_bytes, p.v_xf);
 
@@ -215,18 +231,15 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, cha
   float* const scr = reinterpret_cast<float*>(Vs[0]);
   if constexpr (BU) tab_fill_pre(p.u_xf, pu, u_pre, tu, false, false, scr);
   if constexpr (BV) tab_fill_pre(p.v_xf, pv, v_pre, tv, false, false, scr);
-  if (bid == 0) {
+  if (bid0 == 0) {
     // the BatchNorm whose backward this call applies: dL/dgamma, dL/dbeta (+ conv bias) once
     const vae_xform& dyx = p.dy_is_v ? p.v_xf : p.u_xf;
     if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
   }
   __syncthreads();
+  WG_MARK(1);
 
   f32x4 acc[TM][TJ];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto store = [&](int buf, const Stage& st) {
 #pragma unroll
@@ -295,24 +308,37 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid, cha
     }
   };
 
-  // main loop (vae_cgemm.hpp: loads issued on every path, LDS work skipped past the slice)
-  int buf = 0;
-  for (int kb = 0; kb < nsteps; kb += NS) {
-#pragma unroll
-    for (int u = 0; u < NS; ++u) {
-      const bool live = kb + u < nsteps;
-      if (live) store(buf, ring[u]);
-      __syncthreads();
-      issue(kb + u + NS, ring[u]);
-      if (live) compute(buf);
-      buf ^= 1;
-    }
-  }
-  // D[m][j]: lane holds rows 4g + e of fragment i, column li of fragment j
   const int jst = p.jst > 0 ? p.jst : p.J;
   const long rowstride = (long)p.R * p.R * jst;
-  float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
-  wg_epilogue<TM, TJ>(p, part, acc, m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)tap * jst);
+  for (int ut = 0; ut < nunits; ++ut) {
+    if (ut > 0) {
+      decode(bid0 + ut);
+      __syncthreads();                                 // every wave is done with the LDS tiles
+#pragma unroll
+      for (int u = 0; u < NS; ++u) issue(u, ring[u]);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // main loop (vae_cgemm.hpp: loads issued on every path, LDS work skipped past the slice)
+    int buf = 0;
+    for (int kb = 0; kb < nsteps; kb += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) {
+        const bool live = kb + u < nsteps;
+        if (live) store(buf, ring[u]);
+        __syncthreads();
+        issue(kb + u + NS, ring[u]);
+        if (live) compute(buf);
+        buf ^= 1;
+      }
+    }
+    WG_MARK(2);
+    // D[m][j]: lane holds rows 4g + e of fragment i, column li of fragment j
+    float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;
+    wg_epilogue<TM, TJ>(p, part, acc, m0 + wm * WTM + 4 * g, j0 + wn * WTJ + li, rowstride, (long)tap * jst);
+  }
 }
 
 template <int BM, int BJ, int XU, int XV>
@@ -352,7 +378,8 @@ template <int BM, int BJ, int RR> constexpr int wgemm_taps_lds_bytes() {
 }
 
 template <int BM, int BJ, int XU, int XV, int RR>
-__device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid, char* lds) {
+__device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid, char* lds,
+                                                unsigned long long* clk = nullptr) {
   constexpr int TAPS = RR * RR;
   constexpr int CU = BM / 8, CV = BJ / 8;
   constexpr int RPU = 256 / CU, RPV = 256 / CV;
@@ -457,6 +484,7 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
     if (dyx.kind == VAE_X_BN_DY && (p.db || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.db);
   }
   __syncthreads();
+  WG_MARK(1);
 
   f32x4 acc[TAPS][TM][TJ];
 #pragma unroll
@@ -551,6 +579,7 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
       if constexpr (NB == 2) buf ^= 1;
     }
   }
+  WG_MARK(2);
   const int jst = p.jst > 0 ? p.jst : p.J;
   const long rowstride = (long)TAPS * jst;
   float* const part = p.slab ? p.slab + (long)slice * p.slab_ld : nullptr;

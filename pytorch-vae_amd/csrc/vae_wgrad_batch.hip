@@ -11,6 +11,9 @@
 // call, so the results are those of the calls made one after another.
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
+
 #include "vae_launch.hpp"
 #include "vae_wgrad.hpp"
 #include "vae_wgemm.hpp"
@@ -19,99 +22,123 @@ using namespace vae;
 
 namespace {
 
-constexpr int kWgGroupMax = 6;
+constexpr int kWg3Max = 10;     // layers of one grouped launch (kernel arguments: 8 KB measured to
+                                // launch fine, tools/ubench/kernarg.hip; the group is ~6.5 KB)
 
-// XCD-aware order within each layer of a grouped launch: workgroups are dealt round-robin over the
-// 8 XCDs (block b runs on XCD b % 8; speed only, never correctness), so a layer's local index is
-// remapped to give each XCD a contiguous range of that layer — its K slices (pixel ranges,
-// slice-outermost) then share an L2 instead of every XCD fetching every layer's operands from the
-// fabric (VanillaVAE mixed launch: 86 -> 69 MB of FETCH/WRITE traffic at the same 49.5-50 us,
-// r4_v5 / r4n PMC).  Per layer, not over the whole grid: a grid-wide remap gave whole
-// (unequal-cost) layers to single XCDs and measured 4.7 us slower despite 35 MB less traffic (r4m).
-// Mixed launch only: the all-taps 32x32 group measured slower with it (39.6 -> 45.2 us).
-__device__ __forceinline__ int wg_xcd_order(int b, int nb) {
-  const int q = nb >> 3, r = nb & 7, x = b & 7, loc = b >> 3;
-  return x * q + min(x, r) + loc;
-}
+// VAE_PROBE builds (tools/wgprobe.py): one record per workgroup {layer << 32 | local item, wall
+// start, wall end, XCD, prologue / K-loop / total cycles, HW_ID} in the probe buffer (vae_probe_set)
+#ifdef VAE_PROBE
+#define WG_PROBE_BEGIN() const unsigned long long wg_w0 = threadIdx.x == 0 ? wall_clock64() : 0; \
+  unsigned long long wclk[4] = {__builtin_readcyclecounter(), 0, 0, 0}; unsigned long long* clkp = wclk
+#define WG_PROBE_END(layer, lbid, tag) do { \
+    unsigned long long* pr_ = gk->probe; \
+    const unsigned long long slot_ = blockIdx.x; \
+    if (pr_ && threadIdx.x == 0 && slot_ < pr_[1]) { \
+      unsigned long long* r_ = pr_ + 8 + slot_ * 8; \
+      r_[0] = ((unsigned long long)(layer) << 32) | (unsigned)(lbid); \
+      r_[1] = wg_w0; r_[2] = wall_clock64(); r_[3] = (tag); r_[4] = wclk[1] - wclk[0]; r_[5] = wclk[2] - wclk[0]; \
+      r_[6] = __builtin_readcyclecounter() - wclk[0]; \
+      r_[7] = __builtin_amdgcn_s_getreg((23 << 0) | (0 << 6) | (31 << 11)); \
+    } } while (0)
+#else
+#define WG_PROBE_BEGIN() unsigned long long* clkp = nullptr
+#define WG_PROBE_END(layer, lbid, tag) do { } while (0)
+#endif
 
-struct WgGroup {
+// One launch for every weight gradient of a backward segment.  The work items (layer, K slice,
+// output tile) are listed layer by layer, slice-major, and cut into 8 contiguous ranges of equal
+// estimated cost, one per XCD: workgroups are dealt round-robin over the XCDs (block b runs on
+// XCD b % 8 — speed only, never correctness), so workgroup b runs item xs[b % 8] + b / 8.  An
+// XCD then streams a contiguous pixel range of its layers (the shallow layers' slices) or a
+// contiguous range of output tiles (the deep layers'), and the tiles and taps that re-read the
+// same pixels hit its own L2 instead of the fabric.  No atomics: a layer split into K slices
+// writes each slice's partial tile to its slab (plain stores) and wg3_reduce adds the slices in
+// slice order; a single-slice layer adds its tile into dW itself — the result does not depend on
+// scheduling (deterministic, bit-identical run to run).
+constexpr int kWg3Items = 1024;  // work items of one launch (kernel-argument list, 2 bytes each)
+
+struct Wg3Group {
   int n;
-  int start[kWgGroupMax + 1];      // first workgroup of each layer; start[n] = total
-  int var[kWgGroupMax];            // body variant: 2 * dy_is_v + (x operand BatchNorm+LeakyReLU)
-  WgParams p[kWgGroupMax];
+  int xs[9];                       // XCD x runs list entries [xs[x], xs[x+1])
+  int var[kWg3Max];                // body: 0-3 32 x 32 all-taps, 4-7 64 x 64 per tap, 8-11 64 x 128 per tap
+  int tpi[kWg3Max];                // work units (slice, tap, tile) per item, run one after another
+  int units[kWg3Max];              // work units of the layer
+  WgParams p[kWg3Max];
+  unsigned short item[kWg3Items];  // layer << 12 | the layer's work item (slice * tiles + tile)
+  unsigned long long* probe;       // VAE_PROBE builds: per-workgroup records (else NULL)
 };
-static_assert(sizeof(WgGroup) <= 3584, "kernel argument block");
+static_assert(sizeof(Wg3Group) <= 7680, "kernel argument block");
 
-template <int T, int RR, int XU, int XV>
-__device__ __forceinline__ void wg_group_body(const WgParams& p, int bid, char* lds) {
-  if constexpr (RR > 0) wgemm_taps_body<T, T, XU, XV, RR>(p, bid, lds);
-  else wgemm_body<T, T, XU, XV>(p, bid, lds);
+constexpr int wg3_max(int a, int b) { return a > b ? a : b; }
+constexpr int wg3_lds() {
+  return wg3_max(wgemm_taps_lds_bytes<32, 32, 3>(), wg3_max(wgemm_lds_bytes<64, 64>(), wgemm_lds_bytes<64, 128>()));
 }
 
-template <int T, int RR> constexpr int wg_group_lds() {
-  if constexpr (RR > 0) return wgemm_taps_lds_bytes<T, T, RR>();
-  else return wgemm_lds_bytes<T, T>();
-}
-
-// The dy operand carries the BatchNorm backward (BN_DY), the other one is the layer input with
-// no transform or its BatchNorm+LeakyReLU (the VanillaVAE family and the Autoencoder).
-template <int T, int RR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(T >= 128 ? 2 : 1)))
-wg_group_kernel(const WgGroup g) {
-  __shared__ __attribute__((aligned(16))) char lds[wg_group_lds<T, RR>()];
-  // The group is read in place from the kernel-argument segment (scalar loads at a uniform
-  // dynamic offset): indexing the by-value parameter with a runtime layer index makes the
-  // compiler copy all of it to scratch first (2.5 KB per workgroup, measured 10x slower).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wg3_kernel(const Wg3Group g) {
+  __shared__ __attribute__((aligned(16))) char lds[wg3_lds()];
+  // read in place from the kernel-argument segment (scalar loads at a uniform dynamic offset):
+  // indexing the by-value parameter with a runtime layer index copies all of it to scratch
   (void)g;
-  const WgGroup* gk = (const WgGroup*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
-  const int b = (int)blockIdx.x;
-  const int n = gk->n;
+  const Wg3Group* gk = (const Wg3Group*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int x = (int)(blockIdx.x & 7u), loc = (int)(blockIdx.x >> 3);
+  const int e = gk->xs[x] + loc;
+  if (e >= gk->xs[x + 1]) return;
+  const int it = gk->item[e];
+  const int i = __builtin_amdgcn_readfirstlane(it >> 12);
+  const int bid = __builtin_amdgcn_readfirstlane((it & 4095) * gk->tpi[i]);
+  const int nu = min(gk->tpi[i], gk->units[i] - bid);
+  const WgParams& p = gk->p[i];
+  WG_PROBE_BEGIN();
+  switch (gk->var[i]) {
+    case 0: wgemm_taps_body<32, 32, VAE_X_BN_DY, VAE_X_NONE, 3>(p, bid, lds, clkp); break;
+    case 1: wgemm_taps_body<32, 32, VAE_X_BN_DY, VAE_X_BN_ACT, 3>(p, bid, lds, clkp); break;
+    case 2: wgemm_taps_body<32, 32, VAE_X_NONE, VAE_X_BN_DY, 3>(p, bid, lds, clkp); break;
+    case 3: wgemm_taps_body<32, 32, VAE_X_BN_ACT, VAE_X_BN_DY, 3>(p, bid, lds, clkp); break;
+    case 4: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds, clkp, nu); break;
+    case 5: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds, clkp, nu); break;
+    case 6: wgemm_body<64, 64, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
+    case 7: wgemm_body<64, 64, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
+    case 8: wgemm_body<64, 128, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds, clkp, nu); break;
+    case 9: wgemm_body<64, 128, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds, clkp, nu); break;
+    case 10: wgemm_body<64, 128, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
+    default: wgemm_body<64, 128, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
+  }
+  WG_PROBE_END(i, bid, x);
+}
+
+// dw[e] += Σ_s slab[s][e] for the sliced layers of a launch, slices summed in order (one thread
+// per element; consecutive threads read consecutive words of every slice).
+struct Wg3Reduce {
+  int n;
+  long start[kWg3Max + 1];         // element prefix over the sliced layers
+  const float* slab[kWg3Max];
+  float* dw[kWg3Max];
+  int slices[kWg3Max];
+};
+
+__global__ void __launch_bounds__(256) wg3_reduce(const Wg3Reduce r) {
+  const Wg3Reduce* rk = (const Wg3Reduce*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)r;
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= rk->start[rk->n]) return;
   int i = 0;
 #pragma unroll
-  for (int j = 1; j < kWgGroupMax; ++j) i = (j < n && b >= gk->start[j]) ? j : i;
-  i = __builtin_amdgcn_readfirstlane(i);
-  const int bid = b - gk->start[i];   // (the per-layer XCD order measured 39.6 -> 45.2 us here, r4n)
-  const WgParams& p = gk->p[i];
-  switch (gk->var[i]) {
-    case 0: wg_group_body<T, RR, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
-    case 1: wg_group_body<T, RR, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds); break;
-    case 2: wg_group_body<T, RR, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds); break;
-    default: wg_group_body<T, RR, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds); break;
-  }
-}
-
-// The 64 x 64 and 128 x 128 classes in ONE grid (per layer: var[i] = 4 * (tile == 128) + variant):
-// launched one after the other, each class ran a round of one workgroup per CU on its own (the
-// VanillaVAE's 25 + 30 us, profiles/r4_v1_kstats.json); in one grid they share the round.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wg_group_mixed_kernel(const WgGroup g) {
-  __shared__ __attribute__((aligned(16))) char lds[wgemm_lds_bytes<128, 128>()];
-  (void)g;
-  const WgGroup* gk = (const WgGroup*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
-  const int b = (int)blockIdx.x;
-  const int n = gk->n;
-  int i = 0;
+  for (int j = 1; j < kWg3Max; ++j) i = (j < rk->n && e >= rk->start[j]) ? j : i;
+  const long o = e - rk->start[i];
+  const long cols = rk->start[i + 1] - rk->start[i];
+  const float* sl = rk->slab[i] + o;
+  const int S = rk->slices[i];
+  float acc = 0.f;
+  int s = 0;
+  for (; s + 8 <= S; s += 8) {
+    float v[8];
 #pragma unroll
-  for (int j = 1; j < kWgGroupMax; ++j) i = (j < n && b >= gk->start[j]) ? j : i;
-  i = __builtin_amdgcn_readfirstlane(i);
-  const int bid = wg_xcd_order(b - gk->start[i], gk->start[i + 1] - gk->start[i]);
-  const WgParams& p = gk->p[i];
-  switch (gk->var[i]) {
-    case 0: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
-    case 1: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds); break;
-    case 2: wgemm_body<64, 64, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds); break;
-    case 3: wgemm_body<64, 64, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds); break;
-    case 4: wgemm_body<128, 128, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds); break;
-    case 5: wgemm_body<128, 128, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds); break;
-    case 6: wgemm_body<128, 128, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds); break;
-    default: wgemm_body<128, 128, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds); break;
+    for (int u = 0; u < 8; ++u) v[u] = sl[(long)(s + u) * cols];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
   }
-}
-
-// group classes: 0 = 32 x 32 tiles with all 3x3 taps per workgroup, 1 = 64 x 64, 2 = 128 x 128
-constexpr int kClasses = 3;
-inline int wg_class(const WgPlan& w) {
-  if (w.T == 32) return w.taps == 3 ? 0 : -1;
-  return w.taps ? -1 : (w.T == 64 ? 1 : 2);
+  for (; s < S; ++s) acc += sl[(long)s * cols];
+  rk->dw[i][o] += acc;
 }
 
 inline int wg_variant(const WgParams& p) {
@@ -120,16 +147,6 @@ inline int wg_variant(const WgParams& p) {
   if (dy.kind != VAE_X_BN_DY) return -1;
   if (x.kind != VAE_X_NONE && x.kind != VAE_X_BN_ACT) return -1;
   return 2 * p.dy_is_v + (x.kind == VAE_X_BN_ACT ? 1 : 0);
-}
-
-inline int group_launch(int cls, const WgGroup& g, size_t lds, hipStream_t st) {
-  const dim3 grid((unsigned)g.start[g.n]);
-  switch (cls) {
-    case 0: VAE_LAUNCH((wg_group_kernel<32, 3>), grid, dim3(256), lds, st, g); break;
-    case 1: VAE_LAUNCH((wg_group_kernel<64, 0>), grid, dim3(256), lds, st, g); break;
-    default: VAE_LAUNCH((wg_group_kernel<128, 0>), grid, dim3(256), lds, st, g); break;
-  }
-  return check_launch("wg_group");
 }
 
 // workspace a single call of item i needs (the thread's query state is saved around it)
@@ -143,156 +160,239 @@ inline long item_need(int kind, const vae_conv_args* a) {
   return rc ? -1 : (long)((b + 255) / 256 * 256);
 }
 
+// A grouped layer before its slices are chosen: body, tiles, K-steps and the estimated time of one
+// K-step (us, one workgroup, measured with tools/wgprobe.py on the VanillaVAE B=64 batch: the
+// 64-wide per-tap bodies are latency-bound at ~0.6 us per 32-pixel step; the all-taps body holds
+// one step in flight and pays about a round trip plus its bytes per 64-pixel step).
+struct Wg3Layer {
+  int idx;                 // batch item
+  WgParams p;
+  int var;                 // Wg3Group.var
+  int KP;                  // pixels per K-step of the body
+  long tiles, steps;       // output tiles per slice; K-steps over all pixels
+  double step_us;
+  long cols;               // dW elements (M * R * R * jst)
+  long slices, tpi;
+};
+
+// fixed parts of a work item (us, tools/wgprobe.py): its first round trip (tables + first K-steps,
+// queued behind every other workgroup's), a unit's refill when an item runs several, the epilogue
+constexpr double kWg3PrologueUs = 6.0, kWg3RefillUs = 2.0, kWg3EpilogueUs = 3.0;
+
+inline bool wg3_layer(const WgParams& w0, int idx, Wg3Layer* L) {
+  const int var = wg_variant(w0);
+  if (var < 0 || w0.R != 3) return false;
+  const int mn = w0.M < w0.J ? w0.M : w0.J;
+  WgParams p = w0;
+  p.fd_wu = make_fastdiv(p.wu);
+  p.fd_hu = make_fastdiv(p.hu);
+  p.fd_r = make_fastdiv(p.R);
+  const long npix = (long)p.n * p.hu * p.wu;
+  p.u_bytes = (uint32_t)(npix * p.M * 2);
+  p.v_bytes = (uint32_t)((long)p.n * p.hv * p.wv * p.J * 2);
+  const bool du = p.u_xf.kind == VAE_X_BN_DY, dv = p.v_xf.kind == VAE_X_BN_DY;
+  L->idx = idx;
+  const int jst = p.jst > 0 ? p.jst : p.J;
+  L->cols = (long)p.M * p.R * p.R * jst;
+  if (mn < 64) {                                       // 32 x 32 tiles, all 9 taps per workgroup
+    L->var = var;
+    L->KP = wgt_kp<32, 32>();
+    L->tiles = (long)((p.M + 31) / 32) * ((p.J + 31) / 32);
+    const int cu = p.M < 32 ? p.M : 32, cv = p.J < 32 ? p.J : 32;
+    const double bytes = (double)L->KP * 2.0 * (cu * (du ? 2 : 1) + 9.0 * cv * (dv ? 2 : 1));
+    L->step_us = 1.2 + bytes / 51200.0;
+  } else if (p.J >= 128) {                             // 64 x 128 tiles, one tap per workgroup
+    L->var = 8 + var;
+    L->KP = wg_kp<64>();
+    L->tiles = (long)((p.M + 63) / 64) * ((p.J + 127) / 128) * p.R * p.R;
+    L->step_us = 0.95;
+  } else {                                             // 64 x 64 tiles, one tap per workgroup
+    L->var = 4 + var;
+    L->KP = wg_kp<64>();
+    L->tiles = (long)((p.M + 63) / 64) * ((p.J + 63) / 64) * p.R * p.R;
+    L->step_us = 0.65;
+  }
+  L->steps = (npix + L->KP - 1) / L->KP;
+  L->p = p;
+  return true;
+}
+
 }  // namespace
 
 extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
                                          void* workspace, int64_t workspace_bytes, void* stream) {
   if (n < 0 || (n > 0 && (!kinds || !items))) return fail(VAE_E_BADARG, "conv_bwd_filter_batch: null arrays");
-  hipStream_t st = (hipStream_t)stream;
-  // every item's own workspace, back to back (the grouped layers run concurrently)
-  long total = 0;
-  long off[64];
   if (n > 64) return fail(VAE_E_BADARG, "conv_bwd_filter_batch: %d items > 64", n);
+  hipStream_t st = (hipStream_t)stream;
+  // which items group: bf16 3x3 weight gradients with a BN-backward dy (the VanillaVAE family and
+  // the Autoencoder); the rest run as their own calls, each with a workspace region of its own
+  Wg3Layer lay[kWg3Max];
+  int nl = 0;
+  bool grouped[64];
   for (int i = 0; i < n; ++i) {
     const vae_conv_args* a = items[i];
     if (!a || (kinds[i] != VAE_LAYER_CONV2D && kinds[i] != VAE_LAYER_CONVT2D))
       return fail(VAE_E_BADARG, "conv_bwd_filter_batch: item %d", i);
-    const long need = item_need(kinds[i], a);
-    if (need < 0) return VAE_E_BADARG;                        // (the item's own error message)
-    off[i] = total;
-    total += need;
-  }
-  if (!ws_fits(total, workspace ? workspace_bytes : 0, "conv_bwd_filter_batch")) return VAE_E_BADARG;
-  auto region = [&](int i) -> void* {
-    const long need = (i + 1 < n ? off[i + 1] : total) - off[i];
-    return need > 0 ? static_cast<char*>(workspace) + off[i] : nullptr;
-  };
-  auto region_bytes = [&](int i) -> long { return (i + 1 < n ? off[i + 1] : total) - off[i]; };
-
-  WgPlan plans[64];
-  int cls[64];
-  for (int i = 0; i < n; ++i) {
-    const vae_conv_args* a = items[i];
-    const bool tr = kinds[i] == VAE_LAYER_CONVT2D;
-    cls[i] = -1;
+    grouped[i] = false;
     WgParams w;
     bool closed = false;
     const bool valid = geom_ok(a, "conv_bwd_filter_batch") && a->dy && a->x && a->dw &&
                        xf_ok(a->dy_xf, "conv_bwd_filter_batch.dy") && xf_ok(a->x_xf, "conv_bwd_filter_batch.x");
-    if (valid && conv_wg_params(a, tr, &w, &closed) && (!a->db || closed) && wg_variant(w) >= 0) {
-      if (int rc = wg2_plan(w, querying() ? workspace : region(i), region_bytes(i), &plans[i])) return rc;
-      cls[i] = wg_class(plans[i]);
-    }
-    if (cls[i] < 0) {
-      // not groupable: the call on its own (validation and error messages included)
-      vae_conv_args c = *a;
-      c.workspace = querying() ? workspace : region(i);
-      c.workspace_bytes = region_bytes(i);
-      const int rc = tr ? vae_convT2d_bwd_filter(&c, stream) : vae_conv2d_bwd_filter(&c, stream);
-      if (rc) return rc;
-    }
-  }
-  // Grouped 64 x 64 / 128 x 128 layers (deep, few pixels, large dW): their K slices were sized
-  // for ~2 workgroups per CU each, and every slice adds its whole dW tile with fp32 atomics (the
-  // 3x3 128-channel layers: 8 slices x 1.2 MB).  In a group the layers fill the chip together, so
-  // each takes its share of one round of workgroups (one per CU), in proportion to its MACs:
-  // fewer slices, and a single slice accumulates with plain stores (WgParams.own).
-  static const int group_slots = tune_env("VAE_WG_GROUP_SLOTS", kCUs);
-  // the 32 x 32 all-taps class (wide, few-channel layers: thousands of pixels per dW element)
-  // gets its own round (measured, VanillaVAE B=64: 0 = each layer's standalone split 127 us for
-  // the batch, 256 -> 103 us, 512 -> 107, 768 -> 126); VAE_WG_GROUP_SLOTS0=0 keeps the
-  // standalone plans
-  static const int group_slots0 = tune_env("VAE_WG_GROUP_SLOTS0", kCUs);
-  // When a class's output tiles alone exceed that round (the Autoencoder's 1024-2048-channel
-  // layers: thousands of 128 x 128 tiles), the round-share would leave the long-K layers (its
-  // 64 x 64-pixel ConvT: 65536 pixels, 9 tiles) a handful of workgroups each running hundreds of
-  // K-steps behind everything else; there the K slices are sized instead so that every workgroup
-  // of the class runs about the same number of K-steps (the class's work over its tile count,
-  // >= 16 steps of 32 pixels).
-  // VAE_WG_SHARE=steps: shares in proportion to tile-steps (output tiles x 32-pixel K-steps)
-  // instead of MACs.  Measured slower (VanillaVAE B=64: 0.5498 vs 0.5416 ms/step, the batch 102.8
-  // vs 94 us): the first conv's K-steps (8 of its 32 tile columns real) cost a quarter of its
-  // class-mates', so the MAC shares were the balanced ones.
-  static const bool share_macs = !(getenv("VAE_WG_SHARE") && !strcmp(getenv("VAE_WG_SHARE"), "steps"));
-  for (int c = group_slots0 > 0 ? 0 : 1; c < kClasses; ++c) {
-    const int gs = c == 0 ? group_slots0 : group_slots;
-    double macs = 0.0;
-    long tiles_sum = 0, work = 0;
-    for (int i = 0; i < n; ++i)
-      if (cls[i] == c) {
-        macs += (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
-        const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
-        const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;
-        tiles_sum += tiles;
-        work += tiles * ks;
-      }
-    if (macs <= 0.0) continue;
-    const bool balance = c > 0 && tiles_sum > gs;
-    long kt = balance ? (work + tiles_sum - 1) / tiles_sum : 0;
-    if (kt < 16) kt = 16;
-    for (int i = 0; i < n; ++i) {
-      if (cls[i] != c) continue;
-      const double m = (double)plans[i].cols * ((double)plans[i].p.n * plans[i].p.hu * plans[i].p.wu);
-      long slots = (long)(gs * m / macs + 0.5);
-      if (!share_macs && work > 0) {
-        const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
-        const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;
-        slots = (long)((double)gs * (double)(tiles * ks) / (double)work + 0.5);
-      }
-      if (balance) {
-        const long tiles = (long)plans[i].blocks / (plans[i].split > 0 ? plans[i].split : 1);
-        const long ks = ((long)plans[i].p.n * plans[i].p.hu * plans[i].p.wu + 31) / 32;
-        slots = tiles * ((ks + kt - 1) / kt);
-      }
-      if (slots < 1) slots = 1;
-      WgParams w = plans[i].p;
-      w.slab = nullptr;
-      // (balanced slices add into dw with atomics: their counts were not in the item's workspace)
-      void* wsi = balance ? nullptr : (querying() ? workspace : region(i));
-      if (int rc = wg2_plan(w, wsi, balance ? 0 : region_bytes(i), &plans[i], slots)) return rc;
-      if (wg_class(plans[i]) != c) return fail(VAE_E_UNSUPPORTED, "conv_bwd_filter_batch: replanned class");
-    }
-  }
-  // one launch per tile class (chunks of kWgGroupMax layers); classes 1 and 2 in one grid when
-  // their layers fit one group (VAE_WG_MIXED=0: a launch each)
-  static const bool mixed_ok = !(getenv("VAE_WG_MIXED") && !strcmp(getenv("VAE_WG_MIXED"), "0"));
-  int n12 = 0;
-  for (int i = 0; i < n; ++i) n12 += (cls[i] == 1 || cls[i] == 2) ? 1 : 0;
-  const bool mixed = mixed_ok && n12 <= kWgGroupMax && n12 > 0;
-  for (int c = 0; c < kClasses; ++c) {
-    if (mixed && c == 2) continue;                       // (launched with class 1)
-    WgGroup g;
-    memset(&g, 0, sizeof(g));
-    size_t lds = 0;
-    for (int i = 0; i <= n; ++i) {
-      const bool take = i < n && (cls[i] == c || (mixed && c == 1 && cls[i] == 2));
-      if (take) {
-        const WgPlan& w = plans[i];
-        g.p[g.n] = w.p;
-        g.var[g.n] = wg_variant(w.p) + (mixed && cls[i] == 2 ? 4 : 0);
-        g.start[g.n + 1] = g.start[g.n] + (int)w.blocks;
-        g.n++;
-        const bool bu = w.p.u_xf.kind == VAE_X_BN_ACT || w.p.u_xf.kind == VAE_X_BN_DY;
-        const bool bv = w.p.v_xf.kind == VAE_X_BN_ACT || w.p.v_xf.kind == VAE_X_BN_DY;
-        const size_t l = (size_t)((bu ? 3 * tab_stride(w.p.u_xf.channels) : 0) +
-                                  (bv ? 3 * tab_stride(w.p.v_xf.channels) : 0)) * 4;
-        lds = l > lds ? l : lds;
-      }
-      if (g.n > 0 && (g.n == kWgGroupMax || i == n)) {
-        if (mixed && c == 1) {
-          VAE_LAUNCH(wg_group_mixed_kernel, dim3((unsigned)g.start[g.n]), dim3(256), lds, st, g);
-          if (int rc = check_launch("wg_group_mixed")) return rc;
-        } else if (int rc = group_launch(c, g, lds, st)) {
-          return rc;
-        }
-        memset(&g, 0, sizeof(g));
-        lds = 0;
+    if (nl < kWg3Max && valid && conv_wg_params(a, kinds[i] == VAE_LAYER_CONVT2D, &w, &closed) && (!a->db || closed)) {
+      const bool bu = w.u_xf.kind == VAE_X_BN_ACT || w.u_xf.kind == VAE_X_BN_DY;
+      const bool bv = w.v_xf.kind == VAE_X_BN_ACT || w.v_xf.kind == VAE_X_BN_DY;
+      const long tab = 4l * ((bu ? 3 * tab_stride(w.u_xf.channels) : 0) + (bv ? 3 * tab_stride(w.v_xf.channels) : 0));
+      if (tab + wg3_lds() <= 80 * 1024 && wg3_layer(w, i, &lay[nl])) {
+        grouped[i] = true;
+        ++nl;
       }
     }
   }
-  for (int i = 0; i < n; ++i)
-    if (cls[i] >= 0)
-      if (int rc = wg2_reduce(plans[i], st)) return rc;
+  // workspace: the standalone items' regions, then the grouped layers' slabs
+  long off[64], total = 0;
+  for (int i = 0; i < n; ++i) {
+    off[i] = total;
+    if (grouped[i]) continue;
+    const long need = item_need(kinds[i], items[i]);
+    if (need < 0) return VAE_E_BADARG;                        // (the item's own error message)
+    total += need;
+  }
+  // K slices and units per item: the kernel holds two workgroups per CU (512 slots), so the plan
+  // aims at one round of at most 512 items of about equal time T: a layer whose unit (one K slice
+  // of one tile) takes longer than T is cut into more K slices; a layer of many short units (the
+  // deep layers: hundreds of output tiles over few pixels) runs several units per item.  T is the
+  // smallest time for which the items fit the round.
+  long slab_off[kWg3Max];
+  const long total0 = total;
+  auto plan_at = [&](double T) -> long {
+    total = total0;
+    long items = 0;
+    for (int l = 0; l < nl; ++l) {
+      Wg3Layer& L = lay[l];
+      const double body = T - kWg3PrologueUs - kWg3EpilogueUs;
+      long sl = (long)ceil(L.steps * L.step_us / (body > 0.5 ? body : 0.5));
+      if (sl < 1) sl = 1;
+      if (sl > L.steps) sl = L.steps;
+      const long ksteps = (L.steps + sl - 1) / sl;
+      L.p.kper = (int)(ksteps * L.KP);
+      const long npix = (long)L.p.n * L.p.hu * L.p.wu;
+      L.slices = (npix + L.p.kper - 1) / L.p.kper;
+      L.tpi = 1;
+      if (L.slices == 1) {
+        const double unit = ksteps * L.step_us + kWg3EpilogueUs;
+        long t = (long)((T - kWg3PrologueUs + kWg3RefillUs) / (unit + kWg3RefillUs));
+        L.tpi = t < 1 ? 1 : (t > L.tiles ? L.tiles : t);
+      }
+      L.p.slab = nullptr;
+      L.p.slab_ld = L.cols;
+      L.p.own = L.slices == 1 ? 1 : 0;
+      slab_off[l] = total;
+      if (L.slices > 1) total += (L.slices * L.cols * 4 + 255) / 256 * 256;
+      const long li = (L.slices * L.tiles + L.tpi - 1) / L.tpi;
+      items += li > 4096 ? (long)kWg3Items + 1 : li;
+    }
+    return items;
+  };
+  {
+    double lo = 1.0, hi = 1.0;
+    while (plan_at(hi) > 2 * kCUs && hi < 1e6) hi *= 2.0;
+    for (int it = 0; it < 24; ++it) {
+      const double mid = 0.5 * (lo + hi);
+      if (plan_at(mid) > 2 * kCUs) lo = mid; else hi = mid;
+    }
+    if (nl && plan_at(hi) > kWg3Items) return fail(VAE_E_UNSUPPORTED, "conv_bwd_filter_batch: work items");
+  }
+  if (!ws_fits(total, workspace ? workspace_bytes : 0, "conv_bwd_filter_batch")) return VAE_E_BADARG;
+  auto region = [&](long o) -> void* { return querying() ? workspace : static_cast<char*>(workspace) + o; };
+  for (int i = 0; i < n; ++i) {
+    if (grouped[i]) continue;
+    vae_conv_args c = *items[i];
+    const long need = item_need(kinds[i], items[i]);
+    c.workspace = need > 0 ? region(off[i]) : nullptr;
+    c.workspace_bytes = need;
+    const int rc = kinds[i] == VAE_LAYER_CONVT2D ? vae_convT2d_bwd_filter(&c, stream) : vae_conv2d_bwd_filter(&c, stream);
+    if (rc) return rc;
+  }
+  if (nl == 0) return VAE_OK;
+  // the item list: layers in order, each layer's items slice-major, cut into 8 runs of equal
+  // estimated time (XCD x takes run x: contiguous pixel ranges / tile ranges of its layers); within
+  // a run the longer items go first (the XCD dispatches its workgroups in list order, so the short
+  // items fill the slots the long ones leave)
+  Wg3Group g;
+  memset(&g, 0, sizeof(g));
+#ifdef VAE_PROBE
+  g.probe = vae_probe_buffer();
+#endif
+  g.n = nl;
+  struct It { unsigned short code; float us; };
+  static thread_local It list[kWg3Items];
+  double total_us = 0.0;
+  int ni = 0;
+  for (int l = 0; l < nl; ++l) {
+    Wg3Layer& L = lay[l];
+    if (L.slices > 1) L.p.slab = static_cast<float*>(region(slab_off[l]));
+    g.p[l] = L.p;
+    g.var[l] = L.var;
+    g.tpi[l] = (int)L.tpi;
+    g.units[l] = (int)(L.slices * L.tiles);
+    const long npix = (long)L.p.n * L.p.hu * L.p.wu;
+    const long nitems = (L.slices * L.tiles + L.tpi - 1) / L.tpi;
+    for (long it = 0; it < nitems; ++it) {
+      double us = kWg3PrologueUs;
+      for (long u = it * L.tpi; u < (it + 1) * L.tpi && u < L.slices * L.tiles; ++u) {
+        const long sl = u / L.tiles;
+        const long px = (sl + 1) * L.p.kper < npix ? L.p.kper : npix - sl * L.p.kper;
+        us += (double)(px + L.KP - 1) / L.KP * L.step_us + kWg3EpilogueUs + (u > it * L.tpi ? kWg3RefillUs : 0.0);
+      }
+      list[ni++] = It{(unsigned short)((l << 12) | (int)it), (float)us};
+      total_us += us;
+    }
+  }
+  {
+    // (an XCD holds 64 workgroups at once: a run of more items would start a second round there)
+    constexpr int kPerXcd = 2 * kCUs / 8;
+    int e = 0;
+    for (int x = 0; x < 8; ++x) {
+      g.xs[x] = e;
+      double cum = 0.0;
+      int cnt = 0;
+      while (e < ni && cnt < kPerXcd && (x == 7 || cum < total_us / 8.0 || ni - e > (7 - x) * kPerXcd)) {
+        cum += list[e++].us;
+        ++cnt;
+      }
+    }
+    g.xs[8] = ni;
+    if (e < ni) return fail(VAE_E_UNSUPPORTED, "conv_bwd_filter_batch: %d items over 8 XCD runs", ni);
+    for (int r = 0; r < 8; ++r)
+      std::stable_sort(list + g.xs[r], list + g.xs[r + 1], [](const It& a, const It& b) { return a.us > b.us; });
+    for (int e = 0; e < ni; ++e) g.item[e] = list[e].code;
+  }
+  int per = 0;
+  for (int x = 0; x < 8; ++x) per = g.xs[x + 1] - g.xs[x] > per ? g.xs[x + 1] - g.xs[x] : per;
+  size_t lds = 0;
+  for (int l = 0; l < nl; ++l) {
+    const WgParams& w = g.p[l];
+    const bool bu = w.u_xf.kind == VAE_X_BN_ACT || w.u_xf.kind == VAE_X_BN_DY;
+    const bool bv = w.v_xf.kind == VAE_X_BN_ACT || w.v_xf.kind == VAE_X_BN_DY;
+    const size_t t = (size_t)((bu ? 3 * tab_stride(w.u_xf.channels) : 0) + (bv ? 3 * tab_stride(w.v_xf.channels) : 0)) * 4;
+    lds = t > lds ? t : lds;
+  }
+  VAE_LAUNCH(wg3_kernel, dim3((unsigned)(8 * per)), dim3(256), lds, st, g);
+  if (int rc = check_launch("wg3")) return rc;
+  Wg3Reduce r;
+  memset(&r, 0, sizeof(r));
+  for (int l = 0; l < nl; ++l) {
+    if (lay[l].slices <= 1) continue;
+    r.slab[r.n] = g.p[l].slab;
+    r.dw[r.n] = g.p[l].dw;
+    r.slices[r.n] = (int)lay[l].slices;
+    r.start[r.n + 1] = r.start[r.n] + lay[l].cols;
+    r.n++;
+  }
+  if (r.n > 0) {
+    VAE_LAUNCH(wg3_reduce, dim3((unsigned)((r.start[r.n] + 255) / 256)), dim3(256), 0, st, r);
+    if (int rc = check_launch("wg3_reduce")) return rc;
+  }
   return VAE_OK;
 }
 

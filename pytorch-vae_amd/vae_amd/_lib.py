@@ -200,8 +200,6 @@ _SIGS = {
     "vae_head_workspace_size": [POINTER(HeadArgs), c_int32, POINTER(ctypes.c_size_t)],
     "vae_conv_bwd_filter_batch": [c_int32, c_void_p, c_void_p, c_void_p, c_int64, c_void_p],
     "vae_conv_bwd_filter_batch_workspace_size": [c_int32, c_void_p, c_void_p, POINTER(ctypes.c_size_t)],
-    "vae_conv_bwd_pair": [c_int32, POINTER(ConvArgs), POINTER(ConvArgs), c_void_p, c_int64, c_void_p],
-    "vae_conv_bwd_pair_workspace_size": [c_int32, POINTER(ConvArgs), POINTER(ConvArgs), POINTER(ctypes.c_size_t)],
     "vae_step_begin_ex": [POINTER(StepBeginArgs), c_void_p],
     "vae_latent_fc_fwd": [POINTER(LatentArgs), c_void_p],
     "vae_latent_dec_fwd": [POINTER(LatentArgs), c_void_p],
@@ -326,31 +324,6 @@ class FilterBatch:
              self.workspace_bytes, stream)
         for fn, args in self.after:
             call(fn, *args, stream)
-
-
-class PairCall:
-    """Argument block of one vae_conv_bwd_pair call: a Conv2d / ConvTranspose2d block's
-    bwd_data and bwd_filter calls (each with its ConvArgs, the same dy) as one call — on the bf16
-    conv-GEMM paths one grid of data- and weight-gradient workgroups (vaehip.h)."""
-
-    KINDS = {"vae_conv2d_bwd_data": LAYER_CONV2D, "vae_convT2d_bwd_data": LAYER_CONVT2D}
-
-    def __init__(self, data_fn, data_ref, filter_ref):
-        self.kind = self.KINDS[data_fn]
-        self.data, self.filter = data_ref, filter_ref
-        self.workspace, self.workspace_bytes = None, 0
-
-    @property
-    def args(self):
-        return [self.data._obj, self.filter._obj]
-
-    def workspace_size(self) -> int:
-        out = ctypes.c_size_t(0)
-        call("vae_conv_bwd_pair_workspace_size", self.kind, self.data, self.filter, ctypes.byref(out))
-        return int(out.value)
-
-    def __call__(self, stream):
-        call("vae_conv_bwd_pair", self.kind, self.data, self.filter, self.workspace, self.workspace_bytes, stream)
 
 
 def recon_loss_args(kind: int, n: int, c: int, h: int, w: int, *, mask=None, window=None, levels: int = 5,

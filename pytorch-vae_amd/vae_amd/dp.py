@@ -109,14 +109,19 @@ class _MeanWork:
 
     def __init__(self, work, t: torch.Tensor, world: int):
         self.work, self.t, self.world = work, t, world
+        self.scaled = False
 
     def wait(self):
-        self.work.wait()
-        self.t.div_(self.world)
+        if not self.scaled:
+            self.work.wait()
+            self.t.div_(self.world)
+            self.scaled = True
         return True
 
     def is_completed(self):
-        return self.work.is_completed()
+        """True only once wait() has applied the 1/world scale: before that the tensor holds the
+        rank SUM, not the mean (a poller must call wait() before reading it)."""
+        return self.scaled
 
 
 def allreduce_mean(t: torch.Tensor, group=None, async_op: bool = False):

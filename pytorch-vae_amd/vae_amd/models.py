@@ -188,7 +188,8 @@ class _HipReconLoss(torch.autograd.Function):
             mask = cfg["mask"].to(recons.device, torch.float32).contiguous()
             a = L.recon_loss_args(L.RLOSS_CENTER, n, c, h, w, mask=mask)
         else:
-            a = L.recon_loss_args(L.RLOSS_MSSIM, n, c, h, w, window=cfg["window"])
+            a = L.recon_loss_args(L.RLOSS_MSSIM, n, c, h, w, window=cfg["window"], levels=cfg.get("levels", 5),
+                                  normalize=cfg.get("normalize", True))
         grad = torch.empty_like(recons)
         out = torch.zeros(3, dtype=torch.float32, device=recons.device)
         ws = torch.empty(max(1, L.recon_loss_workspace(a) // 4), dtype=torch.float32, device=recons.device)
@@ -639,6 +640,12 @@ class Autoencoder(_HipVAE):
             return {'loss': g[0], 'Reconstruction_Loss': g[1], 'KLD': zero, 'feature_loss': zero}
         cfg = (self._recon_loss_cfg(recons.device) if recons.is_cuda and recons.dim() == 4
                and recons.shape[2] * recons.shape[3] <= 4096 and recons.shape[2:] == input.shape[2:] else None)
+        if cfg is not None and cfg["kind"] == "mssim":
+            # the kernel's pyramid halves exactly (vaehip.h vae_recon_loss); other plane sizes (the
+            # reference's avg_pool2d floors them, mssim_vae.py) take the torch MS-SSIM below
+            step = 1 << (cfg.get("levels", 5) - 1)
+            if recons.shape[2] % step or recons.shape[3] % step:
+                cfg = None
         if cfg is not None and (cfg["kind"] != "center" or tuple(cfg["mask"].shape) == tuple(recons.shape[2:])):
             recons_loss = _HipReconLoss.apply(recons, input, cfg)  # vae_recon_loss (HIP forward + seed)
         elif self.center_focus_sigma is not None:

@@ -157,11 +157,6 @@ class StepPlan:
         # the weight-gradient call's first workgroup writes dL/dgamma, dL/dbeta and the conv
         # bias gradient (closed form).  Eval mode keeps vae_bn_finalize (running statistics).
         self.bn_in_consumer = bn_in_consumer and training
-        # persist_tables (VAE_PERSIST=1, off by default): the forward's BN_ACT tables written once
-        # (vae_xform.table_out) and loaded by the backward's consumers of the same statistics.
-        # Measured slower (VanillaVAE B=64 0.5724 vs 0.5395 ms/step) and, in the fp32 parity mode,
-        # off against the oracle (encoder gradients) — kept as an experiment, not on the path
-        self.persist_tables = os.environ.get("VAE_PERSIST") == "1"
         self.S = samples if loss == "iwae" else 1
         self.loss_kind = {"vanilla": L.LOSS_VANILLA, "betaH": L.LOSS_BETA_H, "betaB": L.LOSS_BETA_B,
                           "iwae": L.LOSS_IWAE}[loss]
@@ -343,15 +338,6 @@ class StepPlan:
         if table:
             t = self.bntab[prefix]
             xf.table = t.data_ptr() + (4 * 4 * C if kind == L.X_BN_DY else 0)
-        elif kind == L.X_BN_ACT and self.bn_in_consumer and self.persist_tables:
-            # the forward's consumer of this BatchNorm (the one updating the running statistics)
-            # writes the table it builds; every later BN_ACT use of the step (the backward's
-            # activation-backward epilogues and weight-gradient operands) loads it instead of
-            # reducing the replicated statistics again (vaehip.h vae_xform.table_out)
-            if running:
-                xf.table_out = self.bntab[prefix].data_ptr()
-            else:
-                xf.table = self.bntab[prefix].data_ptr()
         if aux is not None:
             xf.aux = aux.data_ptr()
         if running:
@@ -975,15 +961,10 @@ def batch_filter_calls(calls, ends, splits=()):
 
     for end in ends:
         deferred = []
-        paired = pair_calls(calls, lo, end)
         for i in range(lo, end):
             if i in splits and deferred:
                 emit(deferred, True)
                 deferred = []
-            if i in paired:
-                if paired[i] is not None:
-                    out.append(paired[i])
-                continue
             fn, ref = calls[i]
             if fn in DEFERRED_FNS:
                 deferred.append((fn, ref))
@@ -995,47 +976,6 @@ def batch_filter_calls(calls, ends, splits=()):
     return out, new_ends
 
 
-PAIR_FN = "vae_conv_bwd_pair"
-_PAIRS = {"vae_conv2d_bwd_data": "vae_conv2d_bwd_filter", "vae_convT2d_bwd_data": "vae_convT2d_bwd_filter"}
-
-
-def pair_calls(calls, lo, end):
-    """A BatchNorm'd conv / convT block's bwd_data and bwd_filter calls (adjacent in the raw
-    backward, same dy) as one vae_conv_bwd_pair call at the data call's position: on the bf16
-    conv-GEMM paths its weight gradient runs in the data gradient's grid instead of in the
-    segment's grouped batch.  Returns {raw index: (PAIR_FN, PairCall) at the data call's index,
-    None at the filter call's}.  Off by default (VAE_PAIR=1 turns it on): measured slower — the
-    VanillaVAE step 0.660 vs 0.5435 ms/step (B=64, graph-replayed; profiles/r4_v2_pair_sweep.txt):
-    each layer's weight gradient alone in its pair grid took longer than its share of the grouped
-    batch (its slices add whole tiles into dW with atomics), the 64 x 32 data tiles lost a third of
-    their occupancy to the pair's register budget, and the first conv's weight gradient, left alone,
-    took 96 us."""
-    if os.environ.get("VAE_PAIR", "0") != "1":
-        return {}
-    out = {}
-    i = lo
-    while i + 1 < end:
-        (f0, r0), (f1, r1) = calls[i], calls[i + 1]
-        pair = None
-        if _PAIRS.get(f0) == f1:
-            pair = (i, r0, i + 1, r1, f0)
-        elif _PAIRS.get(f1) == f0:
-            pair = (i + 1, r1, i, r0, f1)
-        if pair is not None:
-            di, dref, fi, fref, dfn = pair
-            d, f = dref._obj, fref._obj
-            if (d.dy == f.dy and d.dtype == L.BF16 and d.dy_xf.kind == L.X_BN_DY and f.dy_xf.kind == L.X_BN_DY
-                    and not d.bn_finalize and not f.split_k):
-                out[di] = (PAIR_FN, L.PairCall(dfn, dref, fref))
-                out[fi] = None
-                i += 2
-                continue
-        i += 1
-    return out
-
-
-# Weight-gradient calls: nothing later in the backward reads their output (only the optimizer),
-# so they run on a side stream, concurrent with the data-gradient chain that is the critical path.
 def size_workspaces(plan, call_lists):
     """Give a plan's calls their workspace: each call's need is queried from the library
     (vaehip.h vae_*_workspace_size, which runs the call's own planning without launching), and
@@ -1049,7 +989,7 @@ def size_workspaces(plan, call_lists):
     sized = []
     for calls in call_lists:
         for fn, ref in calls:
-            if fn in (BATCH_FN, PAIR_FN):
+            if fn == BATCH_FN:
                 arg = ref
                 b = ref.workspace_size()
             elif fn not in L.WS_QUERY:
@@ -1101,7 +1041,7 @@ def run_calls(plan, calls, stream):
 def call_one(fn, arg, stream):
     """One entry of a plan's call list (struct argument, scalar-argument tuple or a batch of
     weight-gradient calls) on `stream`."""
-    if fn in (BATCH_FN, PAIR_FN):
+    if fn == BATCH_FN:
         arg(stream)
     elif isinstance(arg, tuple):
         L.call(fn, *arg, stream)

@@ -305,9 +305,8 @@ class BN:
         return bf(F.leaky_relu(z, SLOPE).float())
 
 
-def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed=3, slab=False):
-    """slab: give the call its queried workspace — K slices write partials to it and a fixed-order
-    slab reduction adds them into dw (vae_wgemm.hpp wg_slab_reduce); else fp32 atomics into dw."""
+def prep_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed=3):
+    """One bf16 weight-gradient call's arguments (kernel-side operands) and its fp64 reference."""
     L = _L()
     g = torch.Generator().manual_seed(seed)
     if transposed:
@@ -338,7 +337,7 @@ def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, see
               torch.sqrt(yst.double().var((0, 2, 3), unbiased=False, keepdim=True) + 1e-5))
         dgam, dbet = (gst.double() * xh).sum((0, 2, 3)), gst.double().sum((0, 2, 3))
     else:
-        dyp, dgam, dbet = gst, None, None
+        dyp, dgam, dbet, db_exact = gst, None, None, None
     w0 = torch.zeros(wshape, dtype=torch.float64, requires_grad=True)
     if transposed:
         out = F.conv_transpose2d(act.double(), w0, None, stride=stride, padding=pad,
@@ -359,6 +358,37 @@ def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, see
         a.db = db.data_ptr()
     a.dw = dw.data_ptr()
     fn = "vae_convT2d_bwd_filter" if transposed else "vae_conv2d_bwd_filter"
+    return dict(a=a, fn=fn, want=want, dw=dw, db=db, dgo=dgo, dbo=dbo, db_exact=db_exact, dyp=dyp, dgam=dgam,
+                dbet=dbet, keep=(xd, yd, gd, bnx, bny), R=R, untransformed=(x_kind == L.X_NONE and dy_kind == L.X_NONE))
+
+
+def check_wgrad(w):
+    """The call's dW (and closed-form bias / BN affine gradients) against the fp64 reference."""
+    torch.cuda.synchronize()
+    dw, want, R = w["dw"], w["want"], w["R"]
+    assert relmax(dw.cpu(), want) < 2e-3
+    if w["untransformed"]:
+        # untransformed operands are exact bf16 in the fp64 reference: only fp32 accumulation order
+        # separates the two, so the whole tensor must agree to ~1e-6 (a dropped or doubled K slice,
+        # tap or row block shows here long before it moves the max-abs bar)
+        d = dw.cpu().double() - want
+        err = float(d.norm() / want.norm())
+        if not err < 1e-4:
+            per_tap = [float(d[:, r, s_].norm() / want[:, r, s_].norm()) for r in range(R) for s_ in range(R)]
+            raise AssertionError(f"weight gradient rel-norm error {err:.3e}; per tap {per_tap}")
+    if w["db_exact"] is not None:
+        # closed form A*Σg + B*Σy + C*M (vaehip.h bn_args): exact up to fp32 cancellation
+        assert float((w["db"].cpu().double() - w["db_exact"]).abs().max()) < \
+            1e-6 * float(w["dyp"].double().abs().sum((0, 2, 3)).max())
+        assert relmax(w["dgo"].cpu(), w["dgam"]) < 1e-5 and relmax(w["dbo"].cpu(), w["dbet"]) < 1e-5
+
+
+def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed=3, slab=False):
+    """slab: give the call its queried workspace — K slices write partials to it and a fixed-order
+    slab reduction adds them into dw (vae_wgemm.hpp wg_slab_reduce); else fp32 atomics into dw."""
+    L = _L()
+    w = prep_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, seed)
+    a, fn = w["a"], w["fn"]
     import os
     old_env = os.environ.get("VAE_WG_SLAB_MIN")
     if slab:                      # the slab path from 2 K slices on (in the net: >= 384, vae_wgemm.hpp)
@@ -372,21 +402,7 @@ def run_wgrad(transposed, N, cin, cout, hw, stride, R, pad, x_kind, dy_kind, see
                 os.environ.pop("VAE_WG_SLAB_MIN", None)
             else:
                 os.environ["VAE_WG_SLAB_MIN"] = old_env
-    torch.cuda.synchronize()
-    assert relmax(dw.cpu(), want) < 2e-3
-    if x_kind == L.X_NONE and dy_kind == L.X_NONE:
-        # untransformed operands are exact bf16 in the fp64 reference: only fp32 accumulation order
-        # separates the two, so the whole tensor must agree to ~1e-6 (a dropped or doubled K slice,
-        # tap or row block shows here long before it moves the max-abs bar)
-        d = dw.cpu().double() - want
-        err = float(d.norm() / want.norm())
-        if not err < 1e-4:
-            per_tap = [float(d[:, r, s_].norm() / want[:, r, s_].norm()) for r in range(R) for s_ in range(R)]
-            raise AssertionError(f"weight gradient rel-norm error {err:.3e}; per tap {per_tap}")
-    if dy_kind == L.X_BN_DY:
-        # closed form A*Σg + B*Σy + C*M (vaehip.h bn_args): exact up to fp32 cancellation
-        assert float((db.cpu().double() - db_exact).abs().max()) < 1e-6 * float(dyp.double().abs().sum((0, 2, 3)).max())
-        assert relmax(dgo.cpu(), dgam) < 1e-5 and relmax(dbo.cpu(), dbet) < 1e-5
+    check_wgrad(w)
 
 
 WGRAD = [  # N, cin, cout, hw (conv input), stride, R, pad
@@ -453,3 +469,39 @@ def test_cgemm_fwd_table_built_in_kernel():
     var_u = y.double().var((0, 2, 3), unbiased=True)
     assert relmax(rm.cpu(), 0.1 * mean) < 1e-4
     assert relmax(rv.cpu() - 0.9, 0.1 * var_u) < 1e-4
+
+
+# the VanillaVAE backward's nine weight gradients (B = 16): convT decoder, conv encoder, padded RGB
+BATCH = [(True, 16, 64, 32, 16, 2, 3, 1), (True, 16, 128, 64, 8, 2, 3, 1), (True, 16, 256, 128, 4, 2, 3, 1),
+         (True, 16, 512, 256, 2, 2, 3, 1), (False, 16, 256, 512, 4, 2, 3, 1), (False, 16, 128, 256, 8, 2, 3, 1),
+         (False, 16, 64, 128, 16, 2, 3, 1), (False, 16, 32, 64, 32, 2, 3, 1), (False, 16, 8, 32, 64, 2, 3, 1)]
+
+
+def test_wgrad_batch_matches_reference_and_is_deterministic():
+    """vae_conv_bwd_filter_batch (one XCD-partitioned grid, K-slice partials in slabs reduced in slice
+    order): every layer's dW / bias / BN affine gradients against fp64, and two runs bit-identical."""
+    L = _L()
+    ws = []
+    for seed, (tr, N, cin, cout, hw, s_, R, pad) in enumerate(BATCH):
+        xk = L.X_BN_ACT if (tr and cin != 512) or (not tr and cin != 8) else L.X_NONE
+        ws.append(prep_wgrad(tr, N, cin, cout, hw, s_, R, pad, xk, L.X_BN_DY, seed=10 + seed))
+    n = len(ws)
+    kinds = (ctypes.c_int32 * n)(*[L.LAYER_CONVT2D if w["fn"].startswith("vae_convT") else L.LAYER_CONV2D for w in ws])
+    items = (ctypes.c_void_p * n)(*[ctypes.addressof(w["a"]) for w in ws])
+    need = ctypes.c_size_t(0)
+    L.call("vae_conv_bwd_filter_batch_workspace_size", n, kinds, items, ctypes.byref(need))
+    wsb = torch.empty(max(16, need.value), dtype=torch.uint8, device="cuda")
+    results = []
+    for rep in range(2):
+        for w in ws:
+            for t in ("dw", "db", "dgo", "dbo"):
+                w[t].zero_()
+        L.call("vae_conv_bwd_filter_batch", n, kinds, items, wsb.data_ptr(), wsb.numel(),
+               torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        results.append([w["dw"].clone() for w in ws] + [w["db"].clone() for w in ws])
+        if rep == 0:
+            for w in ws:
+                check_wgrad(w)
+    for a, b in zip(*results):
+        assert torch.equal(a, b)
