@@ -93,12 +93,6 @@ typedef struct vae_xform {
    * When set, consumers load it instead of reducing the statistics themselves, and running
    * statistics / dgamma_out / dbeta_out are left to vae_bn_finalize. */
   const float* table;
-  /* BN_ACT, training: the consumer that updates the running statistics (the forward's first
-   * consumer of the BatchNorm, its first workgroup) also writes the BN_ACT table it built here,
-   * planar [4][C] as above — the backward's later consumers of the same statistics (activation-
-   * backward epilogues, weight-gradient operands) then take it as `table` instead of reducing the
-   * replicated statistics again in every workgroup.  NULL: not written. */
-  float* table_out;
 } vae_xform;
 
 /* One BatchNorm's per-step finalisation, run once between the kernel that produces its
@@ -425,19 +419,6 @@ int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const vae_conv_ar
                               void* workspace, int64_t workspace_bytes, void* stream);
 int vae_conv_bwd_filter_batch_workspace_size(int32_t n, const int32_t* kinds, const vae_conv_args* const* items,
                                              size_t* bytes);
-/* --- one layer's data and weight gradients in one call -----------------------------------
- * The backward of one Conv2d / ConvTranspose2d block (models/vanilla_vae.py:25-75 under
- * experiment.py:45-86's loss.backward()): `data` holds what vae_conv2d_bwd_data /
- * vae_convT2d_bwd_data would get, `filter` what the matching *_bwd_filter call would get (same dy
- * and dy_xf).  The results equal the two calls made one after the other.  Both GEMMs read the same
- * BatchNorm-backward gradient, so on the bf16 conv-GEMM paths they run as ONE grid: data-gradient
- * tiles and weight-gradient K slices side by side (the weight gradient of a latency-bound small
- * layer fills the CUs its data gradient leaves idle).  Other shapes run the two calls in turn.
- * `workspace` serves both (they run in order on `stream`): vae_conv_bwd_pair_workspace_size. */
-int vae_conv_bwd_pair(int32_t kind, const vae_conv_args* data, const vae_conv_args* filter, void* workspace,
-                      int64_t workspace_bytes, void* stream);
-int vae_conv_bwd_pair_workspace_size(int32_t kind, const vae_conv_args* data, const vae_conv_args* filter,
-                                     size_t* bytes);
 /* --- the bookkeeping of one training step (experiment.py:45-86 training_step after the loss):
  * one launch instead of a dozen small tensor ops.
  *   terms[0..nterms) = src_terms[0..nterms)                 (the logged loss terms)

@@ -33,6 +33,8 @@ namespace vae {
 namespace {
 
 constexpr int BG_M = 128, BG_N = 128, BG_K = 64, BG_T = 256;
+// work (FLOP) from which a transform-free layer takes the LDS-DMA GEMMs instead of the conv GEMM
+constexpr double kBgMinFlops = 4e9;
 constexpr int BG_TILE = BG_M * BG_K * 2;              // bytes of one operand tile (16 KB)
 constexpr int BG_STAGE = 2 * BG_TILE;                 // A + B
 // A ring of NSTG stages with NSTG - 1 K-steps in flight: NSTG = 2 at two workgroups per CU (64 KB
@@ -471,9 +473,7 @@ int bgemm_go(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
   const long tiles = (long)((p.M + BG_M - 1) / BG_M) * (p.N / BG_N) * p.nphase;
   // ring depth (bg_ops): two stages at two workgroups per CU for grids of >= two rounds of CUs,
   // else four stages at one per CU, K split until the tiles cover the CUs (>= 4 K-steps a slice)
-  // (VAE_BG_NSTG=2/4 forces one)
-  static const int nstg_env = tune_env("VAE_BG_NSTG", 0);
-  const int nstg = nstg_env == 2 || nstg_env == 4 ? nstg_env : (tiles >= 2l * kCUs ? 2 : 4);
+  const int nstg = tiles >= 2l * kCUs ? 2 : 4;
   const int wgpercu = nstg == 2 ? 2 : 1;
   int split = 1;
   if (tiles < (long)wgpercu * kCUs) {
@@ -505,8 +505,7 @@ int bgemm_go(GemmParams p, void* ws, long ws_bytes, hipStream_t st) {
 // K-steps that stay inside one tap, 128-column tiles, no residual, work large enough to pay for a
 // 128 x 128 tile (>= 1 GFLOP), packed NHWC alignment.
 bool bgemm_ok(const GemmParams& p, int am, int em) {
-  static const bool off = getenv("VAE_NO_BGEMM") != nullptr;
-  if (off || (am != A_CONV && am != A_CONVT) || (em != E_STORE && em != E_BNBWD)) return false;
+  if ((am != A_CONV && am != A_CONVT) || (em != E_STORE && em != E_BNBWD)) return false;
   if (p.a_xf.kind != VAE_X_NONE || p.g_nchw || p.ones_col >= 0 || p.residual || p.out_f32) return false;
   if (p.gc % BG_K || p.N % BG_N || p.out_ld % 8 || p.b_ld % 8) return false;
   if (((uintptr_t)p.a_ptr | (uintptr_t)p.b_ptr | (uintptr_t)p.out) & 15) return false;
@@ -520,8 +519,7 @@ bool bgemm_ok(const GemmParams& p, int am, int em) {
     }
   }
   const double flops = 2.0 * p.M * p.N * (double)kmax * p.nphase;      // (upper bound over phases)
-  static const double minf = tune_env("VAE_BG_MINGF", 0) > 0 ? tune_env("VAE_BG_MINGF", 0) * 1e9 : 4e9;
-  return flops >= minf;
+  return flops >= kBgMinFlops;
 }
 
 int bgemm_launch(const GemmParams& p, int am, int em, void* ws, long ws_bytes, hipStream_t st) {
@@ -530,17 +528,15 @@ int bgemm_launch(const GemmParams& p, int am, int em, void* ws, long ws_bytes, h
 }
 
 // Weight gradients on the LDS-DMA pipeline: transform-free operands (the materialised activation
-// and BatchNorm-backward gradient), 128-multiple channel counts, work >= 4 GFLOP (VAE_BG_MINGF).
+// and BatchNorm-backward gradient), 128-multiple channel counts, work >= 4 GFLOP (kBgMinFlops).
 bool bwg_ok(const WgParams& p) {
-  static const bool off = getenv("VAE_NO_BWG") != nullptr;
-  if (off || p.u_xf.kind != VAE_X_NONE || p.v_xf.kind != VAE_X_NONE || p.jst || p.db) return false;
+  if (p.u_xf.kind != VAE_X_NONE || p.v_xf.kind != VAE_X_NONE || p.jst || p.db) return false;
   if (p.M % 128 || p.J % 128 || p.M <= 0 || p.J <= 0) return false;
   if (((uintptr_t)p.u | (uintptr_t)p.v) & 15) return false;
   const long npix = (long)p.n * p.hu * p.wu;
   if (npix * p.M * 2 >= (1l << 31) || (long)p.n * p.hv * p.wv * p.J * 2 >= (1l << 31)) return false;
   const double flops = 2.0 * p.M * p.J * p.R * p.R * (double)npix;
-  static const double minf = tune_env("VAE_BG_MINGF", 0) > 0 ? tune_env("VAE_BG_MINGF", 0) * 1e9 : 4e9;
-  return flops >= minf;
+  return flops >= kBgMinFlops;
 }
 
 int bwg_launch(WgParams p, hipStream_t st) {
@@ -553,13 +549,12 @@ int bwg_launch(WgParams p, hipStream_t st) {
   const long tiles = (long)(p.M / 128) * (p.J / 128) * p.R * p.R;
   const long ksteps = (npix + BW_KP - 1) / BW_KP;
   // two stages at two workgroups per CU, K slices: one round of workgroups (floor: no overflow
-  // round), >= 8 K-steps each.  (Four stages at one per CU, VAE_BWG_NSTG=4, halves the slices the
-  // small-tile layers split into and measured slower: VQ-VAE encoder.1 72.6 -> 88.7 us, big_ae's
+  // round), >= 8 K-steps each.  (Four stages at one per CU halves the slices the small-tile
+  // layers split into and measured slower: VQ-VAE encoder.1 72.6 -> 88.7 us, big_ae's
   // weight-gradient batch 486 -> 512 us.)
-  static const int nstg_env = tune_env("VAE_BWG_NSTG", 0);
-  const int nstg = nstg_env == 4 ? 4 : 2;
-  const int wgpercu = nstg == 2 ? 2 : 1;
-  static const int mink = tune_env("VAE_BWG_MINK", 8);
+  const int nstg = 2;
+  const int wgpercu = 2;
+  constexpr int mink = 8;
   const long slots = (long)wgpercu * kCUs;
   long split = slots / tiles;
   if (split > ksteps / mink) split = ksteps / mink;

@@ -1020,10 +1020,7 @@ inline bool al16(const void* ptr) { return ((uintptr_t)ptr & 15u) == 0; }
 
 }  // namespace
 
-bool c3_enabled() {
-  static const bool on = !getenv("VAE_NO_C3");
-  return on;
-}
+bool c3_enabled() { return true; }
 
 bool c3_shape_ok(int n, int h, int w, int p, int q, int r, int stride, int pad, int C, int N) {
   return n > 0 && h == 16 && w == 16 && p == 16 && q == 16 && r == 3 && stride == 1 && pad == 1 && C % 32 == 0 &&
@@ -1041,23 +1038,14 @@ int c3_launch(const C3Args& a, hipStream_t st) {
   p.o_bytes = (uint32_t)((long)a.n * 256 * a.N * 2);
   p.a_slope = a.a_slope; p.aux_slope = a.aux_slope;
   p.a_act = a.a_act; p.flip = a.flip; p.C = a.C; p.N = a.N;
-  static const int dbg = getenv("VAE_C3_DBG") ? atoi(getenv("VAE_C3_DBG")) : 0;
-  p.dbg = dbg;
-  // VAE_C3_BN=64: two 256-thread workgroups per CU (A/B timing: 65 vs 48 us forward, slower)
-  static const int bn = (getenv("VAE_C3_BN") && atoi(getenv("VAE_C3_BN")) == 64) ? 64 : 128;
-  const unsigned grid = (unsigned)(a.n * (a.N / bn));
-  // VAE_C3_V1=1: the register-staged whole-chunk kernel (A/B timing)
-  static const bool v1 = getenv("VAE_C3_V1") != nullptr;
+  p.dbg = 0;
+  const unsigned grid = (unsigned)(a.n * (a.N / 128));
   // An activated input (LeakyReLU of the stored tensor) stays on the register-staged kernel, which
-  // applies it once per element as it stages the patch: c3d_kernel<1> applies it to the A fragments
-  // (once per element and tap, VALU-bound) — 66-71 vs 35 us per call at B=128
-  // (profiles/r4_v3_vq_breakdown.txt); VAE_C3D_ACT=1 keeps it (A/B timing)
-  static const bool d_act = getenv("VAE_C3D_ACT") != nullptr;
-  if (bn == 128 && !v1 && a.C % 32 == 0 && (!a.a_act || d_act)) {
-    if (a.a_act) VAE_LAUNCH(c3d_kernel<1>, dim3(grid), dim3(512), 0, st, p);
-    else VAE_LAUNCH(c3d_kernel<0>, dim3(grid), dim3(512), 0, st, p);
-  } else if (bn == 128) VAE_LAUNCH(c3_kernel<128>, dim3(grid), dim3(512), 0, st, p);
-  else VAE_LAUNCH(c3_kernel<64>, dim3(grid), dim3(256), 0, st, p);
+  // applies it once per element as it stages the patch (the LDS-DMA kernel would apply it to the A
+  // fragments once per element and tap: 66-71 vs 35 us per call at B=128,
+  // profiles/r4_v3_vq_breakdown.txt); untransformed inputs take the LDS-DMA kernel
+  if (!a.a_act) VAE_LAUNCH(c3d_kernel<0>, dim3(grid), dim3(512), 0, st, p);
+  else VAE_LAUNCH(c3_kernel<128>, dim3(grid), dim3(512), 0, st, p);
   return check_launch("c3");
 }
 
@@ -1090,12 +1078,9 @@ int c3w_launch(const C3WArgs& a, void* ws, long ws_bytes, hipStream_t st) {
   p.v_act = a.v_act; p.v_slope = a.v_slope;
   p.n = a.n; p.M = a.M; p.J = a.J;
   const unsigned grid = (unsigned)(groups * (a.M / W3_BM) * (a.J / W3_BC));
-  static const bool v1 = getenv("VAE_C3_V1") != nullptr;
-  // (an activated V operand: the register-staged kernel, as c3_launch — c3wd_kernel<1> took
-  // 114-131 vs 50 us per call; VAE_C3D_ACT=1 keeps it)
-  static const bool d_act = getenv("VAE_C3D_ACT") != nullptr;
-  if (v1 || (a.v_act && !d_act)) VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
-  else if (a.v_act) VAE_LAUNCH(c3wd_kernel<1>, dim3(grid), dim3(W3_NT), 0, st, p);
+  // (an activated V operand: the register-staged kernel, as c3_launch — the LDS-DMA kernel took
+  // 114-131 vs 50 us per call)
+  if (a.v_act) VAE_LAUNCH(c3w_kernel, dim3(grid), dim3(W3_NT), 0, st, p);
   else VAE_LAUNCH(c3wd_kernel<0>, dim3(grid), dim3(W3_NT), 0, st, p);
   if (int rc = check_launch("c3w")) return rc;
   VAE_LAUNCH(c3w_reduce, dim3((unsigned)((cols / 4 + 255) / 256)), dim3(256), 0, st, (const float*)p.slab, cols, groups,

@@ -119,9 +119,7 @@ template <int BM, int BN, int XA> constexpr int cg_waves_per_eu() {
   return (BM >= 128 && BN >= 128) ? 2 : ((BM == 64 && BN == 32 && XA == VAE_X_BN_DY) ? 3 : 1);
 }
 
-// The tile work of workgroup `bid` (operand tiles / epilogue tile at `smem`, CgSmem<...NBUF>::BYTES)
-// — run by cgemm_kernel (one problem per launch) and by the paired data + weight gradient launch
-// (vae_bwd_pair.hip), whose other workgroups run a weight-gradient body in the same LDS.
+// The tile work of workgroup `bid` (operand tiles / epilogue tile at `smem`, CgSmem<...NBUF>::BYTES).
 template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
 __device__ __forceinline__ void cgemm_body(const GemmParams& p, const int bid, char* smem) {
   using WG = CgWaves<BM, BN>;
@@ -587,15 +585,6 @@ __device__ __forceinline__ void cgemm_body(const GemmParams& p, const int bid, c
 }
 
 template <int BM, int BN, int BK, int OR> constexpr int cg_nbuf() { return OR == 2 ? 1 : 2; }
-
-// A layer's weight gradient riding on this thread's next conv-GEMM launch (vae_conv_bwd_pair,
-// vae_bwd_pair.hip): set around the layer's data-gradient call.  The cgemm launch site offers
-// its grid to pair_cg_launch, which launches data- and weight-gradient workgroups as ONE grid when
-// that pair is instantiated and returns false otherwise (the weight gradient then runs alone).
-struct PairRider;
-PairRider*& pair_rider();
-bool pair_cg_launch(const GemmParams& p, unsigned nb, int bm, int bn, int am, int xa, int em, int orr, size_t lds,
-                    hipStream_t st);
 
 template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg_waves_per_eu<BM, BN, XA>())))

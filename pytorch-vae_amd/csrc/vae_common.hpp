@@ -289,17 +289,6 @@ __device__ __forceinline__ void bn_finalize_block(const vae_bn_args& a, int cg0,
   }
 }
 
-// The BN_ACT table of channel ch written to x.table_out (vaehip.h: by the consumer that updates
-// the running statistics, for the backward's consumers of the same statistics)
-__device__ __forceinline__ void tab_persist(const vae_xform& x, int ch, float a, float b, float invstd, float mean) {
-  if (!x.table_out) return;
-  const int C = x.channels;
-  x.table_out[ch] = a;
-  x.table_out[C + ch] = b;
-  x.table_out[2 * C + ch] = invstd;
-  x.table_out[3 * C + ch] = -mean * invstd;
-}
-
 // ---------------------------------------------------------------- per-channel transform tables
 // Views into LDS, sized by the real channel count of each transform (rounded up to 4 so vector
 // reads of 4 consecutive channels stay 16-byte aligned):
@@ -421,7 +410,6 @@ __device__ __forceinline__ void tab_pre_finish(const vae_xform& x, const TabPre<
         x.running_mean[ch] = (1.f - m) * x.running_mean[ch] + m * mean;
         x.running_var[ch] = (1.f - m) * x.running_var[ch] + m * unb;
       }
-      if (update_running) tab_persist(x, ch, sc, be - mean * sc, invstd, mean);
     } else {
       const float A = g * invstd;
       const float mg = tot[j][3] * inv_m, mgx = tot[j][2] * inv_m;

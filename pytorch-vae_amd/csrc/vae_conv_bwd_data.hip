@@ -77,8 +77,7 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
       }
     }
   }
-  if (S == 1 && a->dtype == VAE_BF16 && a->c % 8 == 0 && a->k % 8 == 0 && a->workspace &&
-      !getenv("VAE_NO_DGRAD_FLIP")) {
+  if (S == 1 && a->dtype == VAE_BF16 && a->c % 8 == 0 && a->k % 8 == 0 && a->workspace) {
     // stride 1: dx = conv(dy, W') with W'[c][r][s][k] = W[k][R-1-r][R-1-s][c] and pad R-1-P — the
     // forward conv path (k-contiguous weight rows, packed im2col gather of dy) instead of the
     // phase-gather with k-strided weights.  W' lives at the end of the workspace.

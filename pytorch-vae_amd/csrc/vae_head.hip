@@ -764,14 +764,8 @@ bool head_mfma_ok(const vae_head_args* a) {
          (a->x_xf.kind == VAE_X_BN_ACT || a->x_xf.kind == VAE_X_ACT || a->x_xf.kind == VAE_X_NONE);
 }
 
-// XCD-aware tile order (VAE_HEAD_XCD=0 turns it off: A/B sweeps only; read once)
-int head_xcd() {
-  static const int v = [] {
-    const char* e = getenv("VAE_HEAD_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
+// XCD-aware tile order
+int head_xcd() { return 1; }
 
 HeadQ head_q(const vae_head_args* a) {
   HeadQ q;
@@ -822,15 +816,7 @@ int head_bwd_go(const vae_head_args* a, HeadQ q, int gsl_max, hipStream_t st) {
 // C = 64 / 128: 64-channel slices of 2 image rows, two workgroups per CU — 512 workgroups, i.e.
 // 512 per slice (C = 64) or 256 per slice (C = 128).
 constexpr int kHeadGrid = 512;
-// VAE_HEAD_GRID overrides it (workgroups in all; tuning sweeps only; read once)
-int head_grid() {
-  static const int g = [] {
-    const char* e = getenv("VAE_HEAD_GRID");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : kHeadGrid;
-  }();
-  return g;
-}
+int head_grid() { return kHeadGrid; }
 
 // Entry points used by vae_misc.hip's C ABI for the bf16 MFMA path.
 int head_fwd_mfma_launch(const vae_head_args* a, hipStream_t st) {

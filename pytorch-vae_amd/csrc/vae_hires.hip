@@ -483,7 +483,6 @@ constexpr int kHiresBwdGrid = 256;
 // The shapes these kernels take (checked on the host; the caller falls back otherwise):
 // bf16, 32 -> 32 channels, 32x32 -> 64x64, k3 s2 p1 (op1), 16-byte aligned NHWC tensors.
 bool hires_convT_ok(const vae_conv_args* a) {
-  if (getenv("VAE_NO_HIRES")) return false;
   return a->dtype == VAE_BF16 && a->c == HC && a->k == HC && a->h == HIN && a->w == HIN && a->p == HOUT &&
          a->q == HOUT && a->r == 3 && a->stride == 2 && a->pad == 1 && a->n > 0 && !a->x_nchw_f32 &&
          ((uintptr_t)a->x & 15) == 0 && (a->x_xf.kind == VAE_X_NONE || a->x_xf.kind == VAE_X_ACT ||
@@ -523,7 +522,7 @@ int hires_convT_bwd_launch(const vae_conv_args* a, hipStream_t st) {
     return kHeadFallback;
   if (a->x_xf.kind == VAE_X_BN_ACT && (a->x_xf.table || !bn_fast_ok(a->x_xf))) return kHeadFallback;
   const int tiles = a->n * (HIN / IR);
-  static const int gmax = tune_env("VAE_HIRES_GRID", kHiresBwdGrid);     // (sweeps)
+  const int gmax = kHiresBwdGrid;
   const int grid = tiles < gmax ? tiles : gmax;
   const long need = (long)grid * NW * 4;
   if (!a->workspace && !querying()) return kHeadFallback;

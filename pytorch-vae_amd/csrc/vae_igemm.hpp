@@ -201,7 +201,6 @@ __device__ __forceinline__ void tab_fill(const vae_xform& x, Tab t, bool epi, bo
         x.running_mean[ch] = (1.f - m) * x.running_mean[ch] + m * mean;
         x.running_var[ch] = (1.f - m) * x.running_var[ch] + m * unb;
       }
-      if (update_running) tab_persist(x, ch, sc, x.beta[ch] - mean * sc, invstd, mean);
     } else {
       const float inv_m = 1.0f / x.count;
       const float A = g * invstd;

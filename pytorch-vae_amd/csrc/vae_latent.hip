@@ -132,7 +132,6 @@ __device__ __forceinline__ BnCoef bn_coef(const vae_xform& x, int c, bool update
     x.running_mean[c] = (1.f - m) * x.running_mean[c] + m * mean;
     x.running_var[c] = (1.f - m) * x.running_var[c] + m * unb;
   }
-  if (update_running) tab_persist(x, c, k.a, k.b, invstd, mean);
   return k;
 }
 

@@ -304,14 +304,12 @@ inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
 template <int AM, int BMD, int EM>
 inline bool fgemm_ok(const GemmParams& p, int esize_a, int esize_b) {
   if constexpr (BMD != B_NK || AM == A_KM || EM == E_ACC) return false;
-  if (getenv("VAE_NO_FGEMM")) return false;
   if (p.g_nchw || p.ones_col >= 0) return false;
   // Measured (profiles/r1_v2_kernel_breakdown.txt): direct fragments win on the deep-K Linear
   // shapes (fc_mu||fc_var 9.7 -> 4.0 us) but lose on the conv / convT ones, whose blocks run two
-  // residency rounds of latency-bound phases; those stay on the LDS-staged kernel unless asked.
-  if ((AM == A_CONV || AM == A_CONVT) && !getenv("VAE_FGEMM_CONV")) return false;
+  // residency rounds of latency-bound phases; those stay on the LDS-staged kernel.
   if (AM == A_CONV || AM == A_CONVT) {
-    if (p.gc % 32) return false;
+    return false;
   } else {
     if (p.K % 32 || p.a_ld % 8) return false;
   }
@@ -501,7 +499,6 @@ inline int flip_weights_launch(const __bf16* w, __bf16* wf, int K, int R, int C,
 // 16-byte aligned tensors, k-contiguous weight rows, and a transform / epilogue pair the kernel
 // is instantiated for.  VAE_NO_CGEMM=1 keeps everything on the generic kernel (A/B timing).
 inline bool cg_ok(const GemmParams& p, int em) {
-  if (getenv("VAE_NO_CGEMM")) return false;
   if (p.g_nchw || p.ones_col >= 0 || p.gc % 8 || p.N % 8 || p.out_ld % 8 || p.b_ld % 8) return false;
   if (!aligned(p.a_ptr, 16) || !aligned(p.b_ptr, 16) || !aligned(p.out, 16)) return false;
   const int k = p.a_xf.kind;
@@ -521,16 +518,12 @@ inline bool cg_ok(const GemmParams& p, int em) {
 
 struct CgTile { int bm, bn; };
 
-// Launch-shape tunables (read once): VAE_CG_MINWG — workgroups per CU a tile must give before a
-// smaller one is tried (default 2); VAE_CG_SPLITWG — split K while a launch has fewer than this
-// many workgroups per CU (default 1); VAE_WG_WGPERCU — the weight-gradient GEMM's K-slice target.
-inline int tune_env(const char* name, int dflt) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : 0;
-  return v > 0 ? v : dflt;
-}
-inline int cg_minwg() { static const int v = tune_env("VAE_CG_MINWG", 2); return v; }
-inline int cg_splitwg() { static const int v = tune_env("VAE_CG_SPLITWG", 1); return v; }
+// Launch shape: a tile must give every CU this many workgroups before a smaller one is tried, and
+// K is split while a launch has fewer than kCgSplitWg workgroups per CU (swept in round 5,
+// profiles/r5_notes.md: 1 / 3 / 4 and 2 / 3 measured slower on the VanillaVAE step)
+constexpr int kCgMinWg = 2, kCgSplitWg = 1;
+inline int cg_minwg() { return kCgMinWg; }
+inline int cg_splitwg() { return kCgSplitWg; }
 
 // Largest tile that still gives every CU ~2 workgroups; split-K (slabs + igemm_finalize) when
 // even the smallest leaves the chip half empty and K is deep.
@@ -556,7 +549,6 @@ inline void cg_launch_tile(const GemmParams& p, CgTile t, hipStream_t st) {
 #define VAE_CG_CASE(BM_, BN_) \
   if (t.bm == BM_ && t.bn == BN_) { \
     const unsigned nb = (unsigned)(((p.M + BM_ - 1) / BM_) * ((p.N + BN_ - 1) / BN_) * p.nphase * p.ksplit); \
-    if (pair_rider() && pair_cg_launch(p, nb, BM_, BN_, AM, XA, EM, OR, lds, st)) return; \
     VAE_LAUNCH((cgemm_kernel<BM_, BN_, cg_bk<BM_, BN_>(), AM, XA, EM, OR>), dim3(nb), dim3(256), lds, st, p); \
     return; \
   }
@@ -593,8 +585,7 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   const CgTile t = cg_pick(p.M, p.N, p.nphase, cg_table_bytes(p, EM));
   const int bk = t.bm >= 128 ? 64 : 128;
   // tile order (vae_cgemm.hpp): m fastest when the weights outweigh the gathered input tensor
-  static const bool mf_off = getenv("VAE_NO_MFAST") != nullptr;
-  p.m_fast = (!mf_off && (long)p.b_bytes > (long)p.a_bytes) ? 1 : 0;
+  p.m_fast = (long)p.b_bytes > (long)p.a_bytes ? 1 : 0;
   int kmax = p.K;
   if (AM == A_CONVT) {
     kmax = 0;
@@ -622,10 +613,6 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
   const bool one = kps <= ns;
 #define VAE_CG_XA(XA_) (!one ? cg_launch_tile<AM, XA_, EM, 0>(p, t, st) \
                               : kps <= 2 ? cg_launch_tile<AM, XA_, EM, 2>(p, t, st) : cg_launch_tile<AM, XA_, EM, 1>(p, t, st))
-#ifdef VAE_PROBE
-  // diagnostics only (probe build): time the launch without the A-operand transform
-  if (getenv("VAE_PROBE_NOXF")) { VAE_CG_XA(VAE_X_NONE); return check_launch("cgemm"); }
-#endif
   switch (p.a_xf.kind) {
     case VAE_X_NONE: VAE_CG_XA(VAE_X_NONE); break;
     case VAE_X_ACT: VAE_CG_XA(VAE_X_ACT); break;

@@ -314,10 +314,7 @@ int p1_launch(const P1Args& a, hipStream_t st) {
   p.a_slope = a.a_slope; p.res_slope = a.res_slope; p.aux_slope = a.aux_slope;
   p.a_act = a.a_act; p.res_act = a.res_act; p.M = (int)a.M; p.C = a.C; p.N = a.N;
   const unsigned grid = (unsigned)((a.M / P1_BM) * (a.N / P1_BN));
-  // VAE_P1_V1=1: the register-staged kernel (A/B timing)
-  static const bool v1 = getenv("VAE_P1_V1") != nullptr;
-  if (v1) VAE_LAUNCH(p1_kernel, dim3(grid), dim3(P1_NT), 0, st, p);
-  else if (a.a_act) VAE_LAUNCH(p1d_kernel<1>, dim3(grid), dim3(P1_NT), 0, st, p);
+  if (a.a_act) VAE_LAUNCH(p1d_kernel<1>, dim3(grid), dim3(P1_NT), 0, st, p);
   else VAE_LAUNCH(p1d_kernel<0>, dim3(grid), dim3(P1_NT), 0, st, p);
   return check_launch("p1");
 }

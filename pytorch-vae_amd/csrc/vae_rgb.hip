@@ -469,7 +469,6 @@ bool geom_ok_rgb(const vae_conv_args* a) {
 
 // the wide side: [n][32][32][128] bf16, the RGB side [n][64][64][8] bf16
 bool rgb_geom(const vae_conv_args* a, bool transposed) {
-  if (getenv("VAE_NO_RGB")) return false;
   if (a->dtype != VAE_BF16 || a->r != 4 || a->stride != 2 || a->pad != 1 || a->n <= 0 || a->x_nchw_f32) return false;
   if (transposed) return a->c == RG_C && a->h == RG_H && a->w == RG_H && a->k == RG_CP && a->p == 2 * RG_H && a->q == 2 * RG_H;
   return a->k == RG_C && a->c == RG_CP && a->h == 2 * RG_H && a->w == 2 * RG_H && a->p == RG_H && a->q == RG_H;

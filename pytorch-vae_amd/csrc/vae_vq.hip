@@ -321,9 +321,7 @@ int vq_fwd_launch(const vae_vq_args* a, hipStream_t st) {
   // measured at B=128 (32768 rows, 512 codes, dim 64): 64 rows 39.0 us, 128 rows 42.6 us — twice
   // the workgroups (two per CU) hide the chunk barriers and the epilogue better than the second
   // row block's reuse of each codebook fragment saves
-  static const int rb = [] { const char* e = getenv("VAE_VQF_RB"); return e && atoi(e) == 2 ? 2 : 1; }();
-  if (rb == 1) vq_fwd_launch_rb<D, 1>(a, st);
-  else vq_fwd_launch_rb<D, 2>(a, st);
+  vq_fwd_launch_rb<D, 1>(a, st);
   return check_launch("vq_fwd");
 }
 

@@ -620,7 +620,7 @@ static __global__ void __launch_bounds__(256) wg_slab_reduce(const float* slab, 
 // ------------------------------------------------------------------ host
 inline bool wg2_ok(int dtype, const vae_xform& ux, const vae_xform& vx, long u_elems, long v_elems, int M, int J,
                    const void* u, const void* v) {
-  if (dtype != VAE_BF16 || getenv("VAE_NO_WGEMM")) return false;
+  if (dtype != VAE_BF16) return false;
   if (M % 8 || J % 8) return false;
   if (u_elems * 2 >= (1l << 31) || v_elems * 2 >= (1l << 31)) return false;
   if (((uintptr_t)u & 15) || ((uintptr_t)v & 15)) return false;
@@ -691,7 +691,7 @@ struct WgPlan {
 // Plan one layer (tile, K slices, partial slab in `ws` when it pays); launches nothing.
 // slots_req > 0: the workgroups this layer should take (a share of a grouped launch) instead of
 // ~2 per CU of its own.
-inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots_req = 0) {
+inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots_req = 0, int slab_min = kWgSlabMin) {
   p.fd_wu = make_fastdiv(p.wu);
   p.fd_hu = make_fastdiv(p.hu);
   p.fd_r = make_fastdiv(p.R);
@@ -701,8 +701,6 @@ inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots
   // tile: square, the largest whose both sides fit the channel counts
   const int mn = p.M < p.J ? p.M : p.J;
   int T = mn >= 128 ? 128 : (mn >= 64 ? 64 : 32);
-  static const int t1 = tune_env("VAE_WG_T1X1", 0);            // tile override for 1x1 kernels (sweeps)
-  if (p.R == 1 && (t1 == 64 || t1 == 32) && t1 < T) T = t1;
   // wide BatchNorm tables (the Autoencoder's 2048-4096 channels) and the operand tiles share the LDS
   {
     const bool bu = p.u_xf.kind == VAE_X_BN_ACT || p.u_xf.kind == VAE_X_BN_DY;
@@ -720,25 +718,21 @@ inline int wg2_plan(WgParams p, void* ws, long ws_bytes, WgPlan* out, long slots
   // with fp32 atomics — measured on the VQ-VAE residual 1x1 (M = J = 256, 32768 pixels): 128
   // slices 44.4 us, 64 slices 32.7 us, 32 slices 32.5 us, 16 slices 48.7 us; the 3x3 layers and
   // VanillaVAE's are slower with the higher floor)
-  static const int wgpercu = tune_env("VAE_WG_WGPERCU", 2);
-  static const int mink_env = tune_env("VAE_WG_MINK", 0);
-  const int mink = mink_env > 0 ? mink_env : (p.R == 1 ? 16 : 4);
-  const long slots = slots_req > 0 ? slots_req : (long)wgpercu * kCUs;
+  const int mink = p.R == 1 ? 16 : 4;
+  const long slots = slots_req > 0 ? slots_req : 2l * kCUs;
   long split = (slots + tiles - 1) / tiles;
   if (split > ksteps / mink) split = ksteps / mink;
   // one round of workgroups: ceil(slots / tiles) slices overfill the slots by up to tiles - 1
   // workgroups, which then run as a second round on a few CUs (VQ-VAE 3x3: 36 tiles x 15 slices
   // = 540 workgroups for 512 slots) — take floor(slots / tiles) slices instead
-  if (tiles * split > slots && tiles <= slots && !getenv("VAE_WG_NOQUANT")) split = slots / tiles;
+  if (tiles * split > slots && tiles <= slots) split = slots / tiles;
   if (split < 1) split = 1;
   p.kper = (int)(((ksteps + split - 1) / split) * 32);
   split = (npix + p.kper - 1) / p.kper;
   const long cols = (long)p.M * p.R * p.R * p.J;
-  const int slab_min = tune_env("VAE_WG_SLAB_MIN", kWgSlabMin);      // read per call (tests lower it)
   p.slab = nullptr;
   p.slab_ld = cols;
-  if (split >= slab_min && split * cols * 4 <= kWgSlabMaxBytes && (ws || querying()) && cols % 4 == 0 && !p.jst &&
-      !getenv("VAE_NO_WG_SLAB")) {
+  if (split >= slab_min && split * cols * 4 <= kWgSlabMaxBytes && (ws || querying()) && cols % 4 == 0 && !p.jst) {
     if (!ws_fits(split * cols * 4, ws_bytes, "wgemm K-slice partials")) return VAE_E_BADARG;
     p.slab = static_cast<float*>(ws);
   }

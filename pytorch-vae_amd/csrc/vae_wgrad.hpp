@@ -222,10 +222,10 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WgradParams p) {
 // 405 -> 142 us, M = J = 256, 32768 pixels) but loses on the VanillaVAE ones (32-64 channels, or
 // 256-1024 pixels: one block's fixed costs over few K-steps), which stay on the igemm path.
 inline bool wgrad_ok(int dtype, const vae_xform& ux, const vae_xform& vx, long u_elems, long v_elems, int M, int J) {
-  if (dtype != VAE_BF16 || getenv("VAE_NO_WGRAD2")) return false;
+  if (dtype != VAE_BF16) return false;
   if (M % 8 || J % 8) return false;
   // (J == 8, the padded RGB ends, measured slower too: 536 -> 692 us on the VQ output ConvT)
-  if (!getenv("VAE_WGRAD2_ALL") && (M < 64 || J < 64 || u_elems / M < 8192)) return false;
+  if (M < 64 || J < 64 || u_elems / M < 8192) return false;
   auto xf_ok2 = [](const vae_xform& x) {
     if (x.kind == VAE_X_BN_ACT || x.kind == VAE_X_BN_DY) return x.table != nullptr;
     return x.kind == VAE_X_NONE || x.kind == VAE_X_ACT;

@@ -37,7 +37,7 @@ class Xform(ctypes.Structure):
                 ("beta", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("aux", c_void_p),
                 ("running_mean", c_void_p), ("running_var", c_void_p),
                 ("reps", c_int32), ("rstride", c_int32), ("dgamma_out", c_void_p), ("dbeta_out", c_void_p),
-                ("table", c_void_p), ("table_out", c_void_p)]
+                ("table", c_void_p)]
 
 
 class BnArgs(ctypes.Structure):

@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_struct_sizes_match_header_layout():
     # field order mirrors vaehip.h; a mismatch would shift every pointer after it
-    assert ctypes.sizeof(L.Xform) == 6 * 4 + 10 * 8 + 2 * 4 + 4 * 8      # ... dgamma_out, dbeta_out, table, table_out
+    assert ctypes.sizeof(L.Xform) == 6 * 4 + 10 * 8 + 2 * 4 + 3 * 8      # ... dgamma_out, dbeta_out, table
     assert L.ConvArgs.wt.offset > L.ConvArgs.x_xf.offset
 
 

@@ -2,7 +2,8 @@
 32 -> 32 channels, 32x32 -> 64x64, k3 s2 p1 op1) on its dedicated kernels (vae_hires.hip),
 through the C ABI, against PyTorch fp32 on the CPU: the output, the next BatchNorm's producer
 statistics (Σ(y - bias), Σ(y - bias)^2 over the replicas), the running-statistic update of the
-input BatchNorm, and the generic conv-GEMM path (VAE_NO_HIRES) on the same inputs.  bf16 operands:
+input BatchNorm.  (The generic conv-GEMM path these shapes used to have a switch for is covered at
+other shapes by test_gpu_cgemm.py.)  bf16 operands:
 the tolerance is the bf16 one of the other op tests (2e-2 of the max) — the kernels accumulate in
 fp32 and the statistics come from the fp32 accumulators."""
 import ctypes
@@ -32,12 +33,8 @@ def _fwd_args(L, st, wd, wtd, bd, out, sums, reps):
     return a
 
 
-def _run_fwd(monkeypatch, generic: bool):
+def _run_fwd():
     from vae_amd import _lib as L
-    if generic:
-        monkeypatch.setenv("VAE_NO_HIRES", "1")
-    else:
-        monkeypatch.delenv("VAE_NO_HIRES", raising=False)
     torch.manual_seed(4)
     y_prev = torch.randn(N, C, H, H) * 1.5 + 0.3
     st = BNState(y_prev, seed=1, dtype=torch.bfloat16)
@@ -62,9 +59,8 @@ def _run_fwd(monkeypatch, generic: bool):
     return to_nchw(out), ref, sums.sum(1).cpu(), (ref - b.view(1, -1, 1, 1)), (rm.cpu(), rv.cpu()), st
 
 
-@pytest.mark.parametrize("generic", [False, True])
-def test_final_convT_fwd(monkeypatch, generic):
-    out, ref, sums, pre, (rm, rv), st = _run_fwd(monkeypatch, generic)
+def test_final_convT_fwd():
+    out, ref, sums, pre, (rm, rv), st = _run_fwd()
     assert rel(out, ref) < TOL
     ps = pre.double()
     s1, s2 = ps.sum(dim=(0, 2, 3)), (ps * ps).sum(dim=(0, 2, 3))
@@ -78,22 +74,11 @@ def test_final_convT_fwd(monkeypatch, generic):
     torch.testing.assert_close(rv.double(), 0.9 + 0.1 * var * cnt / (cnt - 1), rtol=1e-4, atol=1e-6)
 
 
-def test_final_convT_fwd_hires_matches_generic(monkeypatch):
-    a = _run_fwd(monkeypatch, False)
-    b = _run_fwd(monkeypatch, True)
-    assert rel(a[0], b[0]) < 1e-2          # both bf16 outputs of the same fp32-accumulated sums
-    torch.testing.assert_close(a[2], b[2], rtol=1e-4, atol=1e-2)
-
-
-def _bwd_case(monkeypatch, generic: bool):
+def _bwd_case():
     """Both gradients of final_layer.0 through vae_convT2d_bwd against torch autograd on the CPU:
     act = lrelu(BN_x(x)), y = conv_transpose2d(act, W, b), z = BN_y(y); upstream g = dL/dz."""
     from vae_amd import _lib as L
     from gpu_util import give_workspace
-    if generic:
-        monkeypatch.setenv("VAE_NO_HIRES", "1")
-    else:
-        monkeypatch.delenv("VAE_NO_HIRES", raising=False)
     bf = lambda t: t.to(torch.bfloat16).float()
     torch.manual_seed(6)
     x = bf(torch.randn(N, C, H, H) * 1.3 + 0.2)
@@ -155,9 +140,8 @@ def _bwd_case(monkeypatch, generic: bool):
     return out, ref
 
 
-@pytest.mark.parametrize("generic", [False, True])
-def test_final_convT_bwd_both_gradients(monkeypatch, generic):
-    out, ref = _bwd_case(monkeypatch, generic)
+def test_final_convT_bwd_both_gradients():
+    out, ref = _bwd_case()
     for k in ("dx", "dw", "es"):
         assert rel(out[k], ref[k]) < TOL, (k, rel(out[k], ref[k]))
     for k in ("dgo", "dbo"):                               # the BN affine gradients (fp32 sums)

@@ -104,9 +104,11 @@ def _bn(kind, c):
     return x
 
 
-def test_filter_batch_workspace_is_the_sum_of_its_items():
-    """vae_conv_bwd_filter_batch runs its layers concurrently, so every item gets its own
-    workspace: the batch's need is the sum of the items' (256-byte rounded) needs."""
+def test_filter_batch_workspace():
+    """vae_conv_bwd_filter_batch: the bf16 3x3 layers with a BN-backward dy run as one grid whose
+    K-sliced layers write partial slabs (the batch's own workspace); any other item runs as its own
+    call with a region of its own, so a batch of those needs the sum of the items' needs.  A short
+    workspace fails in planning."""
     fin = _conv(64, 32, 32, 32)                  # final_layer ConvT 32 -> 32, 32x32 -> 64x64
     fin.p = fin.q = 64
     fin.dy = fin.dw = FAKE
@@ -114,12 +116,19 @@ def test_filter_batch_workspace_is_the_sum_of_its_items():
     enc = _conv(64, 16, 64, 128)                 # encoder.2 conv 64 -> 128
     enc.dy = enc.dw = FAKE
     enc.x_xf, enc.dy_xf = _bn(L.X_BN_ACT, 64), _bn(L.X_BN_DY, 128)
-    n1 = _need("vae_convT2d_bwd_filter", fin)
-    n2 = _need("vae_conv2d_bwd_filter", enc)
-    assert n1 > 0                                # 512 K slices x 9216 dW words: slab partials
     b = L.FilterBatch([("vae_convT2d_bwd_filter", ctypes.byref(fin)), ("vae_conv2d_bwd_filter", ctypes.byref(enc))])
-    r = lambda v: (v + 255) // 256 * 256
-    assert b.workspace_size() == r(n1) + r(n2)
+    need = b.workspace_size()
+    assert need > 0 and need % 256 == 0           # K-slice partial slabs of the grouped grid
     lib = L.load()
-    rc = lib.vae_conv_bwd_filter_batch(2, b.kinds, b.items, FAKE, r(n1) + r(n2) - 4, None)
+    rc = lib.vae_conv_bwd_filter_batch(2, b.kinds, b.items, FAKE, need - 4, None)
     assert rc == -1 and b"workspace" in lib.vae_last_error()
+    # fp32 items do not group: each keeps its standalone plan and region
+    f32 = []
+    for a in (fin, enc):
+        c = L.ConvArgs.from_buffer_copy(a)
+        c.dtype = L.F32
+        f32.append(c)
+    n1, n2 = _need("vae_convT2d_bwd_filter", f32[0]), _need("vae_conv2d_bwd_filter", f32[1])
+    b32 = L.FilterBatch([("vae_convT2d_bwd_filter", ctypes.byref(f32[0])), ("vae_conv2d_bwd_filter", ctypes.byref(f32[1]))])
+    r = lambda v: (v + 255) // 256 * 256
+    assert b32.workspace_size() == r(n1) + r(n2)
