@@ -294,8 +294,30 @@ def pmc_traffic(kernels, digest, arch="vanilla"):
     per = {k: d["kernels"][r].get("hbm_bytes_per_launch") for k, r in rows.items()}
     if any(v is None for v in per.values()):
         return None, f"{os.path.relpath(path, REPO)}: no FETCH_SIZE/WRITE_SIZE for every kernel"
-    return {"bytes": sum(per.values()), "bytes_per_kernel": per, "file": os.path.relpath(path, REPO),
-            "digest": d.get("digest"), "head": d.get("head")}, None
+    # the same summary's SQ / TCC counters of each kernel (tools/pmc_summary.py): MFMA busy
+    # (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x CUs), wave-cycle fraction parked in waits
+    # (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and the L2 hit rate (TCC_HIT / (TCC_HIT + TCC_MISS))
+    counters = {k: {c: d["kernels"][r].get(c) for c in ("mfma_busy", "wait_frac", "l2_hit")} for k, r in rows.items()}
+    return {"bytes": sum(per.values()), "bytes_per_kernel": per, "counters": counters,
+            "file": os.path.relpath(path, REPO), "digest": d.get("digest"), "head": d.get("head")}, None
+
+
+def step_traffic(calls, digest, arch="vanilla"):
+    """HBM bytes of one whole step from the PMC summary of this build: per call, the per-launch
+    bytes of its kernels (a kernel shared by several calls contributes its average once per call,
+    so the sum over the step's calls is the step total).  (None, reason) when any kernel is missing."""
+    kernels = [k for ks in calls for k in ks]
+    path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest)
+    if path is None:
+        return None, rows
+    total = 0.0
+    for ks in calls:
+        for k in ks:
+            v = d["kernels"][_row_of(k, d["kernels"])].get("hbm_bytes_per_launch")
+            if v is None:
+                return None, f"{os.path.relpath(path, REPO)}: no FETCH_SIZE/WRITE_SIZE for {k[1]}"
+            total += v
+    return {"bytes": int(total), "file": os.path.relpath(path, REPO)}, None
 
 
 def rocprof_times(kernels, digest, arch="vanilla"):
@@ -602,6 +624,13 @@ def main():
                  "frac": round(attain_us / (ms * 1e3), 4),
                  "mfma_frac": round(step_flops / (ms * 1e-3) / (peak_tf * 1e12), 4),
                  "step_gflop": round(step_flops / 1e9, 3)}
+    # the whole step's counter traffic against its algorithmic bytes
+    step_bytes = sum(r[3] for r in rows)
+    st_tr, why_st = step_traffic([call_kernels(f_, r_) for (_, f_, _, _), r_ in zip(rows, rows_ref)], digest, args.arch)
+    step_roof["algorithmic_bytes"] = int(step_bytes)
+    step_roof["traffic"] = st_tr["bytes"] if st_tr else None
+    step_roof["traffic_ratio"] = round(st_tr["bytes"] / step_bytes, 3) if st_tr and step_bytes else None
+    step_roof["traffic_source"] = st_tr["file"] if st_tr else {"missing": why_st}
     dropin = dropin_eager = None
     if world == 1 and not args.no_dropin and args.arch not in AE_WIDTHS:
         dropin = dropin_leg(args, dtype, steps=max(20, min(args.steps, 100)))

@@ -67,6 +67,7 @@ __device__ __forceinline__ int bg_slot(int row, int c) { return c ^ ((row >> 1) 
 
 template <int AM, int EM, int NSTG>
 __global__ void __launch_bounds__(BG_T, NSTG >= 4 ? 1 : 2) bgemm_kernel(const GemmParams p) {
+  kernarg_prefetch<(sizeof(GemmParams) < 1024 ? sizeof(GemmParams) : 1024)>();
   static_assert(NSTG >= 2 && NSTG <= 4, "bg_wait_newer counts up to three steps in flight");
   extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object (see header)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -337,6 +338,7 @@ __device__ __forceinline__ bf16x8 bw_cat(wgm_bf16x4 lo, wgm_bf16x4 hi) {
 
 template <int NSTG>
 __global__ void __launch_bounds__(BG_T, NSTG >= 4 ? 1 : 2) bwg_kernel(const WgParams p) {
+  kernarg_prefetch<(sizeof(WgParams) < 1024 ? sizeof(WgParams) : 1024)>();
   static_assert(NSTG >= 2 && NSTG <= 4, "bg_wait_newer counts up to three steps in flight");
   extern __shared__ __attribute__((aligned(16))) char smem[];      // the ONLY LDS object
   const int tid = threadIdx.x, lane = tid & 63;

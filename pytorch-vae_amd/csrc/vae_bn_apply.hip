@@ -32,6 +32,7 @@ __device__ __forceinline__ float lo16(uint32_t w) { return __uint_as_float(w << 
 __device__ __forceinline__ float hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 __global__ void __launch_bounds__(BA_T) bn_apply_kernel(const BnApply q) {
+  kernarg_prefetch<(sizeof(BnApply) < 1024 ? sizeof(BnApply) : 1024)>();
   extern __shared__ float tab[];                    // [3][tab_stride(C)] + scratch [1024]
   const int ts = tab_stride(q.C);
   const int kind = q.xf.kind;

@@ -76,6 +76,7 @@ __device__ __forceinline__ uint32_t lrelu_pk(uint32_t w, float slope) {
 
 template <int BN>
 __global__ void __launch_bounds__(BN * 4) c3_kernel(const C3Params p) {
+  kernarg_prefetch<(sizeof(C3Params) < 1024 ? sizeof(C3Params) : 1024)>();
   using T = C3T<BN>;
   constexpr int C3_NT = T::NT, C3_AP = T::AP, C3_BP = T::BP, C3_LDC = T::LDC, C3_BN = BN;
   __shared__ __attribute__((aligned(16))) char smem[T::LDS];
@@ -292,6 +293,7 @@ __device__ __forceinline__ bf16x8 lrelu8(bf16x8 v, float slope) {
 
 template <int ACT>
 __global__ void __launch_bounds__(512) c3d_kernel(const C3Params p) {
+  kernarg_prefetch<(sizeof(C3Params) < 1024 ? sizeof(C3Params) : 1024)>();
   __shared__ __attribute__((aligned(16))) char smem[D3_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -508,6 +510,7 @@ struct W3Params {
 };
 
 __global__ void __launch_bounds__(W3_NT) c3w_kernel(const W3Params p) {
+  kernarg_prefetch<(sizeof(W3Params) < 1024 ? sizeof(W3Params) : 1024)>();
   __shared__ __attribute__((aligned(16))) char smem[W3_U_BYTES + W3_V_BYTES];
   char* const Us = smem;
   char* const Vs = smem + W3_U_BYTES;
@@ -694,6 +697,7 @@ __device__ __forceinline__ w3_bf16x4 w3d_tr(uint32_t lds_addr) {
 
 template <int VACT>
 __global__ void __launch_bounds__(W3_NT) c3wd_kernel(const W3Params p) {
+  kernarg_prefetch<(sizeof(W3Params) < 1024 ? sizeof(W3Params) : 1024)>();
   __shared__ __attribute__((aligned(16))) char smem[W3D_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -891,6 +895,7 @@ struct W1Params {
 };
 
 __global__ void __launch_bounds__(W1_NT) c1w_kernel(const W1Params p) {
+  kernarg_prefetch<(sizeof(W1Params) < 1024 ? sizeof(W1Params) : 1024)>();
   __shared__ __attribute__((aligned(16))) char smem[2 * 256 * W3_URS];
   char* const Us = smem;
   char* const Vs = smem + 256 * W3_URS;

@@ -589,6 +589,7 @@ template <int BM, int BN, int BK, int OR> constexpr int cg_nbuf() { return OR ==
 template <int BM, int BN, int BK, int AM, int XA, int EM, int OR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(cg_waves_per_eu<BM, BN, XA>())))
 cgemm_kernel(const GemmParams p) {
+  kernarg_prefetch<sizeof(GemmParams)>();
   __shared__ __attribute__((aligned(16))) char smem[CgSmem<BM, BN, BK, cg_nbuf<BM, BN, BK, OR>()>::BYTES];
   cgemm_body<BM, BN, BK, AM, XA, EM, OR>(p, (int)blockIdx.x, smem);
 }

@@ -90,6 +90,50 @@ inline void log_launch(const void* k) {
   } while (0)
 namespace vae {
 
+// ---------------------------------------------------------------- kernel-argument prefetch
+// A kernel reads its (up to 1 KB) argument block with scalar loads where each field is first
+// used, and every branch on a field waits for it: the prologue becomes a chain of dependent
+// scalar-cache misses before the first operand load goes out (host-resident kernel arguments made
+// the conv GEMMs 5-11 us slower per launch, profiles/r5_notes.md).  Touching every 64-byte line
+// of the block first puts all of them in flight at once; the later loads then hit the scalar cache.
+// (Reads only; nothing is written through the scalar cache.)
+// Lines 1..N-1 of the block (line 0 is read at entry anyway), one asm statement with its own
+// wait: no prefetch load is still in flight when the compiler reuses its registers.
+template <int BYTES>
+__device__ __forceinline__ void kernarg_prefetch() {
+  const void* k = (const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  unsigned d1, d2, d3, d4, d5, d6, d7;
+  // (only lines inside the block: 15, 7, 3 or 1 of them by its size.  Early-clobber outputs: a
+  // destination must not share the base-address registers, which later loads of the block still read)
+  if constexpr (BYTES > 960) {
+    unsigned e1, e2, e3, e4, e5, e6, e7, e8;
+    asm volatile(
+        "s_load_dword %0, %15, 64\n s_load_dword %1, %15, 128\n s_load_dword %2, %15, 192\n"
+        " s_load_dword %3, %15, 256\n s_load_dword %4, %15, 320\n s_load_dword %5, %15, 384\n"
+        " s_load_dword %6, %15, 448\n s_load_dword %7, %15, 512\n s_load_dword %8, %15, 576\n"
+        " s_load_dword %9, %15, 640\n s_load_dword %10, %15, 704\n s_load_dword %11, %15, 768\n"
+        " s_load_dword %12, %15, 832\n s_load_dword %13, %15, 896\n s_load_dword %14, %15, 960\n"
+        " s_waitcnt lgkmcnt(0)"
+        : "=&s"(d1), "=&s"(d2), "=&s"(d3), "=&s"(d4), "=&s"(d5), "=&s"(d6), "=&s"(d7), "=&s"(e1), "=&s"(e2), "=&s"(e3),
+          "=&s"(e4), "=&s"(e5), "=&s"(e6), "=&s"(e7), "=&s"(e8)
+        : "s"(k));
+  } else if constexpr (BYTES > 448) {
+    asm volatile(
+        "s_load_dword %0, %7, 64\n s_load_dword %1, %7, 128\n s_load_dword %2, %7, 192\n"
+        " s_load_dword %3, %7, 256\n s_load_dword %4, %7, 320\n s_load_dword %5, %7, 384\n"
+        " s_load_dword %6, %7, 448\n s_waitcnt lgkmcnt(0)"
+        : "=&s"(d1), "=&s"(d2), "=&s"(d3), "=&s"(d4), "=&s"(d5), "=&s"(d6), "=&s"(d7)
+        : "s"(k));
+  } else if constexpr (BYTES > 192) {
+    asm volatile("s_load_dword %0, %3, 64\n s_load_dword %1, %3, 128\n s_load_dword %2, %3, 192\n"
+                 " s_waitcnt lgkmcnt(0)"
+                 : "=&s"(d1), "=&s"(d2), "=&s"(d3)
+                 : "s"(k));
+  } else if constexpr (BYTES > 64) {
+    asm volatile("s_load_dword %0, %1, 64\n s_waitcnt lgkmcnt(0)" : "=&s"(d1) : "s"(k));
+  }
+}
+
 // ---------------------------------------------------------------- scalar conversion
 __device__ __forceinline__ float ld_f(const float* p) { return *p; }
 __device__ __forceinline__ float ld_f(const __bf16* p) { return (float)(*p); }

@@ -99,6 +99,7 @@ template <int BM, int BN> struct FgEpi {
 // k-steps of 32 inside one tap (gathered C % 32 == 0; dense K % 32 == 0), 16-B aligned rows.
 template <class T, class TA, int BM, int BN, int AM, int EM, bool DYA>
 __global__ void __launch_bounds__(256) fgemm_kernel(const GemmParams p) {
+  kernarg_prefetch<(sizeof(GemmParams) < 1024 ? sizeof(GemmParams) : 1024)>();
   constexpr int TM = BM / 16, TN = BN / 16;
   constexpr bool EPI_TBL = (EM == E_BNBWD);
   constexpr int EPR = FgEpi<BM, BN>::EPR;

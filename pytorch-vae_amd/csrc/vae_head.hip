@@ -178,6 +178,7 @@ __device__ __forceinline__ void tile_store(const HeadQ& q, int h0, const u32x4 (
 // One tile per workgroup (C <= 64: 1024 tiles at B = 64, all resident at once).
 template <int HC, int ROWS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_fwd_mfma(HeadQ q) {
+  kernarg_prefetch<(sizeof(HeadQ) < 1024 ? sizeof(HeadQ) : 1024)>();
   using T = HT<HC, ROWS>;
   __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];
   __shared__ float ta[HC], tb[HC], tp[HC], tq[HC];
@@ -272,6 +273,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) h
 // the next tile's raw y loaded while the current one computes.
 template <int HC, int ROWS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) head_fwd_stream(HeadQ q) {
+  kernarg_prefetch<(sizeof(HeadQ) < 1024 ? sizeof(HeadQ) : 1024)>();
   using T = HT<HC, ROWS>;
   constexpr int NPG = (T::TPIX + 15) / 16;          // 16-pixel groups over the whole tile
   constexpr int OLD = 33;                           // out row stride (floats): conflict-free
@@ -447,6 +449,7 @@ __device__ __forceinline__ float gseed(const HeadQ& q, int n, const SeedLd& ld, 
 template <int HC, int ROWS, int CT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HC >= 64 && ROWS >= 4 ? 1 : 2)))
 head_bwd_mfma(HeadQ q) {
+  kernarg_prefetch<(sizeof(HeadQ) < 1024 ? sizeof(HeadQ) : 1024)>();
   using T = HT<HC, ROWS>;
   constexpr int NSL = CT / HC;                                              // channel slices
   __shared__ __attribute__((aligned(16))) char tile[T::TPIX * HC * 2];

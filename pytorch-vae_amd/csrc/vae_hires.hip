@@ -45,6 +45,7 @@ __device__ __forceinline__ int band_off(int trow, int tcol, int chunk) {
 }
 
 __global__ void __launch_bounds__(256) hires_convT_fwd_kernel(const HiresF q) {
+  kernarg_prefetch<(sizeof(HiresF) < 1024 ? sizeof(HiresF) : 1024)>();
   __shared__ __attribute__((aligned(16))) char band[TROWS * TCOLS * HC * 2];
   __shared__ __attribute__((aligned(16))) __bf16 stage[4][2 * HOUT * HC];    // per wave: its 2 output rows
   __shared__ float tabs[3 * (HC + 8)];
@@ -219,6 +220,7 @@ __device__ __forceinline__ hr_bf16x4 hr_tr_read(const char* generic_lds_addr) {
 }
 
 __global__ void __launch_bounds__(256) hires_convT_bwd_kernel(const HiresB q) {
+  kernarg_prefetch<(sizeof(HiresB) < 1024 ? sizeof(HiresB) : 1024)>();
   __shared__ __attribute__((aligned(16))) char dyt[DROWS * 2 * DIDX * HC * 2];     // dY' (bf16)
   __shared__ __attribute__((aligned(16))) char actt[IR * HIN * HC * 2];            // act of the tile
   __shared__ __attribute__((aligned(16))) char yt[IR * HIN * HC * 2];              // raw x of the tile

@@ -844,6 +844,7 @@ template <int PER> constexpr int ring_stages() { return PER <= 2 ? 4 : (PER <= 4
 // DYA / DYB: the A / B operand may carry a BN_DY transform (its aux tensor is loaded).
 template <class T, class TA, class TB, int BM, int BN, int AM, int BMD, int EM, bool VA, bool VB, bool DYA, bool DYB>
 __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
+  kernarg_prefetch<(sizeof(GemmParams) < 1024 ? sizeof(GemmParams) : 1024)>();
   constexpr int BK = bk_of<T>();
   constexpr int LDK = BK + (sizeof(T) == 4 ? 4 : 8);        // padded LDS row (elements)
   using WG = WaveGrid<BM, BN>;
@@ -1205,6 +1206,7 @@ constexpr int FIN_RPT = 2;
 constexpr int FIN_ROWS = 16 * FIN_RPT;
 template <class T, int EM, bool V4>
 __global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
+  kernarg_prefetch<(sizeof(GemmParams) < 1024 ? sizeof(GemmParams) : 1024)>();
   constexpr bool EPI_TBL = (EM == E_BNBWD);
   __shared__ float r1[16][64], r2[16][64];
   extern __shared__ float tabs[];

@@ -140,6 +140,7 @@ __device__ __forceinline__ BnCoef bn_coef(const vae_xform& x, int c, bool update
 // (one pixel's channels c0..c0+127 of the NHWC map: x_xf.channels % 128 == 0)
 constexpr int FC_BK = 128, FC_LD = FC_BK + 8;
 __global__ void __launch_bounds__(256) latent_fc_fwd_kernel(const vae_latent_args a) {
+  kernarg_prefetch<(sizeof(vae_latent_args) < 1024 ? sizeof(vae_latent_args) : 1024)>();
   __shared__ __attribute__((aligned(16))) __bf16 As[64 * FC_LD];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[32 * FC_LD];
   __shared__ float ta[FC_BK], tb[FC_BK];
@@ -204,6 +205,7 @@ __global__ void __launch_bounds__(256) latent_fc_fwd_kernel(const vae_latent_arg
 // wave w: rows 16*(w&1).., columns 32*(w>>1)..
 template <int D>
 __global__ void __launch_bounds__(256) latent_dec_fwd_kernel(const vae_latent_args a) {
+  kernarg_prefetch<(sizeof(vae_latent_args) < 1024 ? sizeof(vae_latent_args) : 1024)>();
   constexpr int LD = D + 8, KC = D / 8;                       // 16-byte chunks per row
   constexpr int NA = 32 * KC / 256, NB = 64 * KC / 256;       // chunks per thread: z rows, W2 rows
   __shared__ __attribute__((aligned(16))) __bf16 As[32 * LD];
@@ -296,6 +298,7 @@ constexpr int DB_BK = 256, DB_LD = DB_BK + 8;
 constexpr int WR_BK = 64, WR_LD = WR_BK + 8;                  // K chunk over batch rows
 template <int D>
 __global__ void __launch_bounds__(256) latent_dec_bwd_kernel(const vae_latent_args a, int nA) {
+  kernarg_prefetch<(sizeof(vae_latent_args) < 1024 ? sizeof(vae_latent_args) : 1024)>();
   constexpr int SMEM_A = (64 + 16) * DB_LD * 2, SMEM_B = (64 + 64) * WR_LD * 2;
   __shared__ __attribute__((aligned(16))) char smem[SMEM_A > SMEM_B ? SMEM_A : SMEM_B];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -428,6 +431,7 @@ __global__ void __launch_bounds__(256) latent_dec_bwd_kernel(const vae_latent_ar
 //           [nA, ...) dW1 / db1 tiles: 64 fc outputs x 128 in_features, K = batch rows
 template <int D>
 __global__ void __launch_bounds__(256) latent_fc_bwd_kernel(const vae_latent_args a, int nA) {
+  kernarg_prefetch<(sizeof(vae_latent_args) < 1024 ? sizeof(vae_latent_args) : 1024)>();
   constexpr int D2 = 2 * D, LDA = D2 + 8;
   constexpr int SMEM_A = (32 + 64) * LDA * 2, SMEM_B = (64 + 128) * WR_LD * 2;
   __shared__ __attribute__((aligned(16))) char smem[SMEM_A > SMEM_B ? SMEM_A : SMEM_B];

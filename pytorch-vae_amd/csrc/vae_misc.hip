@@ -450,7 +450,8 @@ int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
 }
 
 // ------------------------------------------------------------------ BatchNorm finalisation
-__global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) { bn_finalize_block(a, blockIdx.x, gridDim.x); }
+__global__ void __launch_bounds__(256) bn_finalize_kernel(vae_bn_args a) {
+  kernarg_prefetch<(sizeof(vae_bn_args) < 1024 ? sizeof(vae_bn_args) : 1024)>(); bn_finalize_block(a, blockIdx.x, gridDim.x); }
 
 // Eval-mode BatchNorm: the forward table from the running statistics (torch eval semantics:
 // (y - running_mean) / sqrt(running_var + eps) * gamma + beta).
@@ -481,6 +482,7 @@ __global__ void reparam_kernel(int rows, int samples, int D, const float* mulv, 
 
 // ---------------------------------------------------------------------------- ELBO
 __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
+  kernarg_prefetch<(sizeof(vae_elbo_args) < 1024 ? sizeof(vae_elbo_args) : 1024)>();
   __shared__ float kld_row[1024];
   __shared__ float red[4][4];
   const int B = a.batch, S = a.samples > 0 ? a.samples : 1, D = a.latent;
@@ -804,6 +806,7 @@ extern "C" int vae_cast_bf16(int64_t n, const float* src, void* dst, void* strea
 // ------------------------------------------------------------------ training-step record
 namespace {
 __global__ void __launch_bounds__(256) step_record_kernel(const vae_record_args a) {
+  kernarg_prefetch<(sizeof(vae_record_args) < 1024 ? sizeof(vae_record_args) : 1024)>();
   __shared__ float pv[1024];
   __shared__ float rv[2][256];
   __shared__ int ri[2][256];
@@ -892,6 +895,7 @@ struct SwapBatch {
 };
 
 __global__ void __launch_bounds__(256) swap_axes_kernel(const SwapBatch sb) {
+  kernarg_prefetch<(sizeof(SwapBatch) < 1024 ? sizeof(SwapBatch) : 1024)>();
   __shared__ float t[32][33];
   int i = 0;
   while (i + 1 < sb.count && (int)blockIdx.x >= sb.tiles0[i + 1]) ++i;

@@ -206,6 +206,7 @@ constexpr int P1D_LDS = 2 * P1D_STAGE > P1_EPI ? 2 * P1D_STAGE : P1_EPI;
 
 template <int ACT>
 __global__ void __launch_bounds__(P1_NT, 2) p1d_kernel(const P1Params p) {
+  kernarg_prefetch<(sizeof(P1Params) < 1024 ? sizeof(P1Params) : 1024)>();
   __shared__ __attribute__((aligned(16))) char smem[P1D_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -105,6 +105,7 @@ constexpr int RL_LDS = 2 * RL_PYR + (RL_PYR - RL_MAXHW) + 6 * RL_MAXHW;
 
 template <bool BWD>
 __global__ void __launch_bounds__(RL_T) mssim_plane_kernel(const vae_recon_loss_args a) {
+  kernarg_prefetch<(sizeof(vae_recon_loss_args) < 1024 ? sizeof(vae_recon_loss_args) : 1024)>();
   __shared__ float sm[RL_LDS];
   const vae_recon_loss_args& r = a;
   const int plane = blockIdx.x, HW = a.h * a.w, L = a.levels, R = a.window_size;
@@ -252,6 +253,7 @@ __global__ void __launch_bounds__(RL_T) mssim_finalize_kernel(const vae_recon_lo
 
 // centre-weighted MSE: per plane sum of mask * d^2 and the seed 2 * mask * d / N
 __global__ void __launch_bounds__(RL_T) center_plane_kernel(const vae_recon_loss_args a) {
+  kernarg_prefetch<(sizeof(vae_recon_loss_args) < 1024 ? sizeof(vae_recon_loss_args) : 1024)>();
   __shared__ float red[RL_T / 64];
   const int plane = blockIdx.x, HW = a.h * a.w;
   const float* x = a.recon + (long)plane * HW;

@@ -79,6 +79,7 @@ constexpr int RF_LDG = RG_KK + 4;                     // result row pitch (fp32)
 static_assert(RF_ROWS * RF_LDG * 4 <= RF_LDS_A, "result tile fits the operand tile");
 
 __global__ void __launch_bounds__(RF_T) rgb_out_fwd_kernel(const RgbFwd q) {
+  kernarg_prefetch<(sizeof(RgbFwd) < 1024 ? sizeof(RgbFwd) : 1024)>();
   __shared__ __attribute__((aligned(16))) char lds_a[RF_LDS_A];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[RG_KK * RG_LDA];
   __shared__ float red[RF_T / 64];
@@ -226,6 +227,7 @@ struct RgbBwd {
 
 constexpr int RB_DYR = 2 * RG_TI + 2;                 // dy rows a tile reads (one halo row each side)
 __global__ void __launch_bounds__(RB_T) rgb_out_bwd_kernel(const RgbBwd q) {
+  kernarg_prefetch<(sizeof(RgbBwd) < 1024 ? sizeof(RgbBwd) : 1024)>();
   __shared__ __attribute__((aligned(16))) __bf16 Xs[RB_PIX * RG_LDA];   // lrelu(x), then the dx tile
   __shared__ __attribute__((aligned(16))) __bf16 Gs[RB_PIX * RG_LDK];   // gathered dy rows per pixel
   __shared__ __attribute__((aligned(16))) __bf16 Ws[RG_C * RG_LDK];     // W[c][tap*4+k]
@@ -359,6 +361,7 @@ struct RgbIn {
 
 constexpr int RI_XR = 2 * RG_TI + 2;                  // image rows a tile reads
 __global__ void __launch_bounds__(RB_T) rgb_in_wgrad_kernel(const RgbIn q) {
+  kernarg_prefetch<(sizeof(RgbIn) < 1024 ? sizeof(RgbIn) : 1024)>();
   __shared__ __attribute__((aligned(16))) __bf16 Us[RB_PIX * RG_LDA];
   __shared__ __attribute__((aligned(16))) __bf16 Gs[RB_PIX * RG_LDK];
   __shared__ __attribute__((aligned(16))) __bf16 Xi[RI_XR * 2 * RG_H * 4];

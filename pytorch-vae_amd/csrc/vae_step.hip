@@ -41,6 +41,7 @@ __device__ __forceinline__ void image_pixel(const vae_step_begin_args& a, long p
 
 template <class T>
 __global__ void __launch_bounds__(256) step_begin_ex_kernel(const StepBegin s) {
+  kernarg_prefetch<(sizeof(StepBegin) < 1024 ? sizeof(StepBegin) : 1024)>();
   const int b = blockIdx.x, tid = threadIdx.x;
   if (b < s.nz) {
     f32x4* z = static_cast<f32x4*>(s.a.zero);

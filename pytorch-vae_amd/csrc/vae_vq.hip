@@ -41,6 +41,7 @@ typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 // RB: 16-row blocks per wave (workgroup = 4 waves x RB x 16 rows)
 template <class T, int D, int RB>
 __global__ void __launch_bounds__(256) vq_fwd_kernel(vae_vq_args a) {
+  kernarg_prefetch<(sizeof(vae_vq_args) < 1024 ? sizeof(vae_vq_args) : 1024)>();
   constexpr int VQF_ROWS = 64 * RB;
   constexpr int S = D / 4;                         // k-steps (dims per lane)
   constexpr int LDC = D + 4;                       // padded codebook row (floats)
@@ -188,6 +189,7 @@ __global__ void __launch_bounds__(256) vq_fwd_kernel(vae_vq_args a) {
 
 template <class T>
 __global__ void __launch_bounds__(256) vq_bwd_kernel(vae_vq_args a) {
+  kernarg_prefetch<(sizeof(vae_vq_args) < 1024 ? sizeof(vae_vq_args) : 1024)>();
   const int D = a.dim;
   const int e = threadIdx.x % D;
   const int lanes_rows = 256 / D;                            // row groups per workgroup
@@ -237,6 +239,7 @@ __global__ void __launch_bounds__(256) vq_bwd_kernel(vae_vq_args a) {
 // workgroup (h*w % 256 == 0, checked on the host).
 template <class T, int C>
 __global__ void __launch_bounds__(256) recon_kernel(vae_recon_args a, int bwd) {
+  kernarg_prefetch<(sizeof(vae_recon_args) < 1024 ? sizeof(vae_recon_args) : 1024)>();
   __shared__ float red[4];
   const long hw = (long)a.h * a.w;
   const long pix = (long)blockIdx.x * 256 + threadIdx.x;     // over n*h*w

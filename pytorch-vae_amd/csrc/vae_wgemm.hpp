@@ -344,6 +344,7 @@ __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid0, ch
 template <int BM, int BJ, int XU, int XV>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BM >= 128 ? 2 : 1)))
 wgemm_kernel(const WgParams p) {
+  kernarg_prefetch<(sizeof(WgParams) < 1024 ? sizeof(WgParams) : 1024)>();
   __shared__ __attribute__((aligned(16))) char lds[wgemm_lds_bytes<BM, BJ>()];
   wgemm_body<BM, BJ, XU, XV>(p, (int)blockIdx.x, lds);
 }
@@ -591,6 +592,7 @@ __device__ __forceinline__ void wgemm_taps_body(const WgParams& p, const int bid
 template <int BM, int BJ, int XU, int XV, int RR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR >= 4 ? 2 : 1)))
 wgemm_taps_kernel(const WgParams p) {
+  kernarg_prefetch<(sizeof(WgParams) < 1024 ? sizeof(WgParams) : 1024)>();
   __shared__ __attribute__((aligned(16))) char lds[wgemm_taps_lds_bytes<BM, BJ, RR>()];
   wgemm_taps_body<BM, BJ, XU, XV, RR>(p, (int)blockIdx.x, lds);
 }

@@ -86,6 +86,7 @@ __device__ __forceinline__ uint4 wg_xform(const uint32_t (&w)[4], const uint32_t
 }
 
 __global__ void __launch_bounds__(256) wgrad_bf16_kernel(const WgradParams p) {
+  kernarg_prefetch<(sizeof(WgradParams) < 1024 ? sizeof(WgradParams) : 1024)>();
   __shared__ __attribute__((aligned(16))) char Us[2][WG_BK * 256];
   __shared__ __attribute__((aligned(16))) char Vs[2][WG_BK * 256];
   __shared__ float tabs[6 * WG_BM];

@@ -75,6 +75,7 @@ constexpr int wg3_lds() {
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wg3_kernel(const Wg3Group g) {
+  kernarg_prefetch<(sizeof(Wg3Group) < 1024 ? sizeof(Wg3Group) : 1024)>();
   __shared__ __attribute__((aligned(16))) char lds[wg3_lds()];
   // read in place from the kernel-argument segment (scalar loads at a uniform dynamic offset):
   // indexing the by-value parameter with a runtime layer index copies all of it to scratch
