@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 21
+#define VAE_ABI_VERSION 22
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -170,6 +170,11 @@ typedef struct vae_conv_args {
    * of an operand zero-padded on that axis (the 8-channel RGB image), indices >= dw_inner are
    * dropped (bf16 weight-gradient GEMM path only; elsewhere VAE_E_UNSUPPORTED). */
   int32_t dw_inner;
+  /* 1: every cross-workgroup reduction of this call runs in a fixed order (partials to the
+   * workspace, summed by an ordered pass) instead of float atomics, so repeated calls give
+   * bit-identical results (the parity mode of experiment.py:308-311's gradients).  Needs the
+   * workspace *_workspace_size reports for it; dtype VAE_F32 only (VAE_E_UNSUPPORTED otherwise). */
+  int32_t deterministic;
 } vae_conv_args;
 
 /* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,
@@ -201,6 +206,7 @@ typedef struct vae_linear_args {
    * bn_counter: reserved (a zeroed uint32 slot; may be NULL). */
   const struct vae_bn_args* bn_finalize;
   uint32_t* bn_counter;
+  int32_t deterministic;    /* as vae_conv_args.deterministic */
 } vae_linear_args;
 
 /* Final layer of the decoder: Conv2d(C->3, k3, s1, p1) + Tanh (vanilla_vae.py:73-75,
@@ -227,6 +233,13 @@ typedef struct vae_head_args {
   int64_t workspace_bytes;
   const struct vae_bn_args* bn_finalize;   /* as vae_conv_args.bn_finalize (bwd: final BatchNorm) */
   uint32_t* bn_counter;
+  /* bwd, optional (bf16 MFMA path, kind VAE_LOSS_VANILLA or VAE_LOSS_BETA_H, samples 1): the loss
+   * this backward seeds from.  Its seed coefficient is the constant 2/(n*3*h*w) (coef is not read)
+   * and the call also evaluates the loss — vae_elbo_fwd's outputs: out, per_img, head_coef, kl_coef
+   * — in one extra workgroup of its filter-partial reduction, so the step needs no vae_elbo_fwd
+   * launch.  NULL: coef as above. */
+  const struct vae_elbo_args* elbo;
+  int32_t deterministic;    /* as vae_conv_args.deterministic (VALU kernels, fp32) */
 } vae_head_args;
 
 

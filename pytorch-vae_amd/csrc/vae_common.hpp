@@ -23,6 +23,26 @@ int bn_finalize_launch(const vae_bn_args* a, hipStream_t stream);
 // returned by a fast-path launcher whose preconditions do not hold (the caller falls back)
 constexpr int kHeadFallback = 0x7fff0001;
 
+// ---------------------------------------------------------------- deterministic reductions
+// A call made with `deterministic` set writes every cross-workgroup partial sum it would have
+// added with a float atomic to its own row of a workspace slab instead, and one ordered pass
+// (ordered_sum_launch, vae_misc.hip) adds the rows in a fixed order:
+//   output (g, c), g < groups, c < cols, sums slab rows [g*rpg, (g+1)*rpg) in ascending order,
+//   each row at column (c / cw) * hstride + c % cw + f * fstride for f = 0 .. folds-1, and adds the
+//   total into dst[c / cw][g * gstride + c % cw] (one thread owns each output: no atomics).
+// The result no longer depends on workgroup timing, so repeated calls are bit-identical.
+struct OrdSum {
+  const float* slab;
+  long rstride;
+  int groups, rpg, cols, cw;
+  long hstride;
+  int folds;
+  long fstride;
+  float* dst[2];
+  long gstride;
+};
+int ordered_sum_launch(const OrdSum& o, hipStream_t st);
+
 // ---------------------------------------------------------------- workspace queries (host)
 // vae_*_workspace_size runs an entry point's whole planning with an unbounded workspace and the
 // query flag set: every site that would use workspace records its bytes (ws_fits) and VAE_LAUNCH

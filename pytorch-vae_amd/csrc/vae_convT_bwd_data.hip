@@ -9,6 +9,7 @@ extern "C" int vae_convT2d_bwd_data(const vae_conv_args* a, void* stream) {
   if (!geom_ok(a, "convT2d_bwd_data") || !a->dy || !a->wt || !a->dx) return fail(VAE_E_BADARG, "convT2d_bwd_data: null tensor");
   if (!xf_ok(a->dy_xf, "convT2d_bwd_data.dy") || !epi_ok(a->dx_epi, "convT2d_bwd_data.epi")) return VAE_E_BADARG;
   GemmParams p = base_params();
+  p.det = a->deterministic;
   p.M = a->n * a->h * a->w; p.N = a->c; p.K = a->r * a->r * a->k;
   p.a_ptr = a->dy; p.a_xf = sanitize(a->dy_xf);
   p.b_ptr = a->wt; p.b_ld = p.K;

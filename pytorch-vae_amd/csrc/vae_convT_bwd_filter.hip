@@ -36,6 +36,7 @@ extern "C" int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream) {
     return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
   }
   GemmParams p = base_params();
+  p.det = a->deterministic;
   const int Nw = a->r * a->r * a->k;
   p.M = a->c; p.N = Nw; p.K = a->n * a->h * a->w;
   p.dbc = closed ? a->db : nullptr; p.dbc_from_b = 1;
@@ -44,7 +45,7 @@ extern "C" int vae_convT2d_bwd_filter(const vae_conv_args* a, void* stream) {
   p.gn = a->n; p.gh = a->p; p.gw = a->q; p.gc = a->k; p.gp = a->h; p.gq = a->w;
   p.gr = a->r; p.gs = a->stride; p.gpad = a->pad;
   p.out = a->dw; p.out_ld = Nw;
-  int rc = launch<A_KM, B_GATHER, E_ACC, false, true>(a->dtype, false, false, p, a->split_k, nullptr, 0, (hipStream_t)stream);
+  int rc = launch<A_KM, B_GATHER, E_ACC, false, true>(a->dtype, false, false, p, a->split_k, p.det ? a->workspace : nullptr, p.det ? a->workspace_bytes : 0, (hipStream_t)stream);
   if (rc) return rc;
   if (a->db && !closed) return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
   return VAE_OK;

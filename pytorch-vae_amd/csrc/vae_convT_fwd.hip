@@ -15,6 +15,7 @@ extern "C" int vae_convT2d_fwd(const vae_conv_args* a, void* stream) {
   const int S = a->stride;
   if (a->p % S || a->q % S) return fail(VAE_E_BADSHAPE, "convT2d_fwd: output not a multiple of stride");
   GemmParams p = base_params();
+  p.det = a->deterministic;
   if (!make_taps(p, S, a->r, a->pad)) return fail(VAE_E_UNSUPPORTED, "convT2d_fwd: stride/kernel");
   p.nphase = S * S;
   p.M = a->n * (a->p / S) * (a->q / S); p.N = a->k; p.K = 0;

@@ -44,6 +44,7 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
     // bf16 conv-GEMM: phase gather of dy (any stride; stride 1 is one phase of R*R taps) against
     // the swapped-axes weights WT[c][r][s][k] (caller's wt_t, or built at the workspace's end)
     GemmParams q = base_params();
+    q.det = a->deterministic;
     if (make_taps(q, S, a->r, a->pad)) {
       q.nphase = S * S;
       q.M = a->n * (a->h / S) * (a->w / S); q.N = a->c; q.K = 0;
@@ -90,6 +91,7 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
     int rc = flip_weights_launch(static_cast<const __bf16*>(a->wt), wf, a->k, a->r, a->c, (hipStream_t)stream);
     if (rc) return rc;
     GemmParams p = base_params();
+    p.det = a->deterministic;
     p.M = a->n * a->h * a->w; p.N = a->c; p.K = a->r * a->r * a->k;
     p.a_ptr = a->dy; p.a_xf = sanitize(a->dy_xf);
     p.b_ptr = wf; p.b_ld = p.K;
@@ -105,6 +107,7 @@ extern "C" int vae_conv2d_bwd_data(const vae_conv_args* a, void* stream) {
     });
   }
   GemmParams p = base_params();
+  p.det = a->deterministic;
   if (!make_taps(p, S, a->r, a->pad)) return fail(VAE_E_UNSUPPORTED, "conv2d_bwd_data: stride/kernel");
   p.nphase = S * S;
   p.M = a->n * (a->h / S) * (a->w / S); p.N = a->c; p.K = 0;

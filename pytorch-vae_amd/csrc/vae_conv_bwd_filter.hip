@@ -66,6 +66,7 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
     return column_sum_launch(a->dtype, a->dy, (long)a->n * a->p * a->q, a->k, a->db, (hipStream_t)stream);
   }
   GemmParams p = base_params();
+  p.det = a->deterministic;
   const int Nw = a->r * a->r * a->c;
   const bool ones = a->db && !closed;                           // Σdy as an extra GEMM column
   p.M = a->k; p.N = Nw + (ones ? 1 : 0); p.K = a->n * a->p * a->q;
@@ -76,6 +77,7 @@ extern "C" int vae_conv2d_bwd_filter(const vae_conv_args* a, void* stream) {
   p.gn = a->n; p.gh = a->h; p.gw = a->w; p.gc = a->c; p.gp = a->p; p.gq = a->q;
   p.gr = a->r; p.gs = a->stride; p.gpad = a->pad;
   p.out = a->dw; p.out_ld = Nw;
-  return launch<A_KM, B_GATHER, E_ACC, true, false, false, true>(a->dtype, false, a->x_nchw_f32 != 0, p, a->split_k, nullptr, 0,
+  return launch<A_KM, B_GATHER, E_ACC, true, false, false, true>(a->dtype, false, a->x_nchw_f32 != 0, p, a->split_k,
+                                                    p.det ? a->workspace : nullptr, p.det ? a->workspace_bytes : 0,
                                                     (hipStream_t)stream);
 }

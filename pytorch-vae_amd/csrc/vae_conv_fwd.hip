@@ -36,6 +36,7 @@ extern "C" int vae_conv2d_fwd(const vae_conv_args* a, void* stream) {
     return c3_launch(c, (hipStream_t)stream);
   }
   GemmParams p = base_params();
+  p.det = a->deterministic;
   p.M = a->n * a->p * a->q; p.N = a->k; p.K = a->r * a->r * a->c;
   p.a_ptr = a->x; p.a_xf = sanitize(a->x_xf); p.g_nchw = a->x_nchw_f32;
   p.b_ptr = a->wt; p.b_ld = p.K;

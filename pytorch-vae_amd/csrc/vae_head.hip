@@ -28,6 +28,7 @@
 #include <stdlib.h>
 
 #include "vae_common.hpp"
+#include "vae_elbo.hpp"
 
 namespace vae {
 namespace {
@@ -68,6 +69,7 @@ struct HeadQ {
   const float* wt; const float* bias;  // [3][3][3][C] fp32 native, [3]
   const float* target; float* recon; float* sse;
   const float* coef; const float* grad_recon;
+  float hc;                            // coef == NULL: the constant dL/d(sse_i) of a fused ELBO
   __bf16* dx; float* dgamma; float* dbeta; int sum_reps, sum_rstride;
   float* slab;                         // [grid][27 C + 3] filter partials, or NULL: atomics into dw/db
   float* dw; float* db;
@@ -436,7 +438,7 @@ __device__ __forceinline__ void seed_load(const HeadQ& q, int tile_i, SeedLd& ld
 __device__ __forceinline__ float gseed(const HeadQ& q, int n, const SeedLd& ld, int j, int co) {
   const float y = ld.y[j][co];
   if (q.grad_recon) return ld.t[j][co] * (1.f - y * y);
-  return q.coef[n] * (y - ld.t[j][co]) * (1.f - y * y);   // 0 outside the image (y = t = 0)
+  return (q.coef ? q.coef[n] : q.hc) * (y - ld.t[j][co]) * (1.f - y * y);   // 0 outside the image (y = t = 0)
 }
 
 // One workgroup = one tile x HC of the CT input channels (CT / HC channel slices: the C = 128
@@ -727,10 +729,18 @@ head_bwd_mfma(HeadQ q) {
 // (columns < NW) and db (the NCO columns after): 16 columns x 16 row-parts per workgroup, each
 // part's loads issued together, parts combined in a fixed order (deterministic).
 constexpr int RR_COLS = 16, RR_PARTS = 16, RR_UNROLL = 8;
+// (elbo.kind >= 0: one extra workgroup, the last, evaluates the step's ELBO — vae_head_args.elbo)
 template <int HC, int CT>
-__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, float* dw, float* db, int cb0) {
+__global__ void __launch_bounds__(256) reduce_rows_kernel(const float* src, int rows, float* dw, float* db, int cb0,
+                                                          const vae_elbo_args elbo) {
   using T = HT<HC, 4>;
   __shared__ float red[RR_PARTS][RR_COLS];
+  if (elbo.kind >= 0 && blockIdx.x == gridDim.x - 1) {
+    __shared__ float kld_row[1024];
+    __shared__ float ered[4][4];
+    elbo_block(elbo, kld_row, ered);
+    return;
+  }
   const int cl = threadIdx.x % RR_COLS, part = threadIdx.x / RR_COLS;
   const int c = blockIdx.x * RR_COLS + cl;
   float s = 0.f;
@@ -797,12 +807,27 @@ int head_bwd_go(const vae_head_args* a, HeadQ q, int gsl_max, hipStream_t st) {
   if (q.filter && ws && !ws_fits(need, a->workspace_bytes, "head_bwd filter partials")) return VAE_E_BADARG;
   const bool slab = q.filter && ws;
   q.slab = slab ? ws : nullptr;
+  vae_elbo_args el;
+  memset(&el, 0, sizeof(el));
+  el.kind = -1;
+  if (a->elbo) {
+    el = *a->elbo;
+    if ((el.kind != VAE_LOSS_VANILLA && el.kind != VAE_LOSS_BETA_H) || (el.samples > 1) || !slab || !q.filter)
+      return fail(VAE_E_UNSUPPORTED, "head_bwd: fused ELBO needs the vanilla / BetaVAE-H loss, samples 1 and a workspace");
+    q.coef = nullptr;
+    q.hc = 2.f / ((float)el.batch * (float)el.img_elems);
+  }
   VAE_LAUNCH((head_bwd_mfma<HC, ROWS, CT>), dim3(grid), dim3(256), 0, st, q);
   int rc = check_launch("head_bwd_mfma");
   if (rc || !q.filter || !slab) return rc;
+  vae_elbo_args none;
+  memset(&none, 0, sizeof(none));
+  none.kind = -1;
   for (int sl = 0; sl < NSL && !rc; ++sl) {      // a slice's slab rows are contiguous positions
-    VAE_LAUNCH((reduce_rows_kernel<HC, CT>), dim3((T::SLAB_COLS + RR_COLS - 1) / RR_COLS), dim3(256), 0, st,
-               (const float*)ws + (long)sl * gsl * T::SLAB_COLS, gsl, a->dw, sl == 0 ? a->db : nullptr, sl * HC);
+    const bool e = sl == 0 && el.kind >= 0;
+    VAE_LAUNCH((reduce_rows_kernel<HC, CT>), dim3((T::SLAB_COLS + RR_COLS - 1) / RR_COLS + (e ? 1 : 0)), dim3(256), 0,
+               st, (const float*)ws + (long)sl * gsl * T::SLAB_COLS, gsl, a->dw, sl == 0 ? a->db : nullptr, sl * HC,
+               e ? el : none);
     rc = check_launch("reduce_rows");
   }
   return rc;

@@ -99,6 +99,12 @@ struct GemmParams {
   unsigned long long* probe; // VAE_PROBE builds: per-block phase timestamps (diagnostics only)
   int m_fast;                // cgemm tile order: m fastest (an XCD's range spans few n columns:
                              // weight-heavy layers) instead of n fastest (host: vae_launch.hpp)
+  // deterministic calls (vaehip.h vae_conv_args.deterministic): E_ACC runs on the slab path, and
+  // the per-channel sums / reparameterization terms go to det_slab rows (one per contributing
+  // block or row) that ordered_sum_launch adds in a fixed order
+  int det;
+  float* det_slab;
+  int det_rows;              // rows of per-channel sums in det_slab
 };
 
 // Phase timestamps of one block (VAE_PROBE builds): record = {block id, wall0, wall3, clk0..clk3,
@@ -775,8 +781,14 @@ __device__ __forceinline__ ReparamIn reparam_load(const GemmParams& p, int row, 
 __device__ __forceinline__ void reparam_apply(const GemmParams& p, int row, int col, float v, const ReparamIn& r) {
   const int b = row / p.samples;
   const float sd = expf(0.5f * r.lv);
-  atomicAdd(p.dmulv + (long)b * 2 * p.latent + col, v + r.c * r.mu);
-  atomicAdd(p.dmulv + (long)b * 2 * p.latent + p.latent + col, v * r.ep * 0.5f * sd + r.c * 0.5f * (expf(r.lv) - 1.f));
+  const float t1 = v + r.c * r.mu, t2 = v * r.ep * 0.5f * sd + r.c * 0.5f * (expf(r.lv) - 1.f);
+  if (p.det_slab) {                       // row's own terms; the ordered pass sums a mu row's samples
+    p.det_slab[(long)row * 2 * p.latent + col] = t1;
+    p.det_slab[(long)row * 2 * p.latent + p.latent + col] = t2;
+    return;
+  }
+  atomicAdd(p.dmulv + (long)b * 2 * p.latent + col, t1);
+  atomicAdd(p.dmulv + (long)b * 2 * p.latent + p.latent + col, t2);
 }
 
 template <int EM>
@@ -791,6 +803,11 @@ __device__ __forceinline__ void epi_flush_sums(const GemmParams& p, int rep, int
   const long roff = p.sum_reps > 1 ? (long)(rep % p.sum_reps) * p.sum_rstride : 0;
   float* g1 = ((EM == E_STORE) ? p.sum : p.dbeta) + roff;
   float* g2 = ((EM == E_STORE) ? p.sumsq : p.dgamma) + roff;
+  if (p.det_slab) {                       // contributor rep's own row [2][N]; ordered pass folds columns
+    p.det_slab[(long)rep * 2 * p.N + col] = s1;
+    p.det_slab[(long)rep * 2 * p.N + p.N + col] = s2;
+    return;
+  }
   const int ch = (EM == E_STORE) ? col : (int)(col - p.fd_ech.div(col) * p.epi_xf.channels);
   atomicAdd(g1 + ch, s1);
   atomicAdd(g2 + ch, s2);
@@ -862,7 +879,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
 
   __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
   __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
-  __shared__ float red1[BN], red2[BN];
+  __shared__ float red1[WG::WM][BN], red2[WG::WM][BN];   // per-column sums, one row per wave row
   extern __shared__ float tabs[];
 
 #ifdef VAE_PROBE
@@ -1047,7 +1064,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   tab_fill(p.a_xf, ta, false, first_block);
   tab_fill(p.b_xf, tb, false, false);
   if constexpr (EPI_TBL) tab_fill(p.epi_xf, te, true, false);
-  for (int i = tid; i < BN; i += NTHREADS) { red1[i] = 0.f; red2[i] = 0.f; }
+  for (int i = tid; i < WG::WM * BN; i += NTHREADS) { red1[i / BN][i % BN] = 0.f; red2[i / BN][i % BN] = 0.f; }
   if constexpr (EM == E_ACC) {
     const vae_xform& dyx = p.dbc_from_b ? p.b_xf : p.a_xf;
     if (first_block && dyx.kind == VAE_X_BN_DY && (p.dbc || dyx.dgamma_out || dyx.dbeta_out)) closed_form_db(dyx, p.dbc);
@@ -1084,7 +1101,7 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
   // lane holds rows 4*(lane>>4)+e, column lane&15 of each 16x16 tile
   const int rowq = m0 + wm * WTM + 4 * (lane >> 4);
   const int colq = n0 + wn * WTN + (lane & 15);
-  if constexpr (EM == E_ACC) {
+  if (EM == E_ACC && !p.slab) {
     float* out = static_cast<float*>(p.out);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1120,7 +1137,9 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
         }
       return;
     }
-    if constexpr (EM == E_REPARAM) {
+    if constexpr (EM == E_ACC) {
+      return;
+    } else if constexpr (EM == E_REPARAM) {
       ReparamIn rin[TM][TN][4];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -1184,16 +1203,21 @@ __global__ void __launch_bounds__(NTHREADS) igemm_kernel(const GemmParams p) {
           s1 += __shfl_xor(s1, 32);
           s2 += __shfl_xor(s2, 16);
           s2 += __shfl_xor(s2, 32);
-          if (lane < 16 && col_ok) {
-            atomicAdd(&red1[wn * WTN + j * 16 + lane], s1);
-            atomicAdd(&red2[wn * WTN + j * 16 + lane], s2);
+          if (lane < 16 && col_ok) {          // each (wave row, column) has one writer
+            red1[wm][wn * WTN + j * 16 + lane] = s1;
+            red2[wm][wn * WTN + j * 16 + lane] = s2;
           }
         }
       }
       if (want_sums) {
         __syncthreads();
-        for (int c = tid; c < BN; c += NTHREADS)
-          if (n0 + c < p.N) epi_flush_sums<EM>(p, blockIdx.x + blockIdx.z * gridDim.x, n0 + c, red1[c], red2[c]);
+        for (int c = tid; c < BN; c += NTHREADS) {
+          if (n0 + c >= p.N) continue;
+          float a = 0.f, b = 0.f;
+#pragma unroll
+          for (int w = 0; w < WG::WM; ++w) { a += red1[w][c]; b += red2[w][c]; }
+          epi_flush_sums<EM>(p, blockIdx.x + blockIdx.z * gridDim.x, n0 + c, a, b);
+        }
       }
     }
   }
@@ -1257,7 +1281,23 @@ __global__ void __launch_bounds__(NTHREADS) igemm_finalize(const GemmParams p) {
         for (int c = 0; c < 4; ++c) v[r][c] += t[u][r][c];
   }
   __syncthreads();   // epilogue table ready
-  if constexpr (EM == E_REPARAM) {
+  if constexpr (EM == E_ACC) {
+    // deterministic weight gradient: the slices' sum added once per element (one owner thread)
+    float* out = static_cast<float*>(p.out);
+#pragma unroll
+    for (int r = 0; r < FIN_RPT; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int col = col0 + c;
+        if (!rok[r] || col >= p.N) continue;
+        if (col == p.ones_col) {
+          if (p.bias_grad) p.bias_grad[row[r]] += v[r][c];
+        } else {
+          out[(long)row[r] * p.out_ld + col] += v[r][c];
+        }
+      }
+    return;
+  } else if constexpr (EM == E_REPARAM) {
     ReparamIn rin[FIN_RPT][4];
 #pragma unroll
     for (int r = 0; r < FIN_RPT; ++r)

@@ -220,6 +220,46 @@ inline int launch_finalize(const GemmParams& p, hipStream_t st) {
   return check_launch("igemm_finalize");
 }
 
+// ------------------------------------------------------------------ deterministic mode
+// Rows of per-channel sums a deterministic launch writes (one per contributing block): the
+// finalize's row blocks after a split-K, else the main grid's M blocks x phases.
+template <int EM>
+inline bool det_wants_sums(const GemmParams& p) {
+  return (EM == E_STORE && p.sum) || (EM == E_BNBWD && p.epi_xf.kind == VAE_X_BN_ACT);
+}
+inline long det_sum_rows(const GemmParams& p, int bm) {
+  if (p.ksplit > 1) return ((long)p.M * p.nphase + FIN_ROWS - 1) / FIN_ROWS;
+  return (long)((p.M + bm - 1) / bm) * p.nphase;
+}
+// Bytes of det_slab: the sums' rows [2][N] or the reparameterization terms [rows][2*latent].
+template <int EM>
+inline long det_slab_bytes(const GemmParams& p, int bm) {
+  if (!p.det) return 0;
+  if (det_wants_sums<EM>(p)) return det_sum_rows(p, bm) * 2 * p.N * 4;
+  if (EM == E_REPARAM) return (long)p.M * 2 * p.latent * 4;
+  return 0;
+}
+// The ordered pass over det_slab (after the main kernel and its finalize).
+template <int EM>
+inline int det_reduce(const GemmParams& p, hipStream_t st) {
+  if (!p.det_slab) return VAE_OK;
+  OrdSum o;
+  memset(&o, 0, sizeof(o));
+  o.slab = p.det_slab;
+  if (EM == E_REPARAM) {
+    o.rstride = 2L * p.latent; o.groups = p.M / p.samples; o.rpg = p.samples;
+    o.cols = 2 * p.latent; o.cw = p.latent; o.hstride = p.latent; o.folds = 1;
+    o.dst[0] = p.dmulv; o.dst[1] = p.dmulv + p.latent; o.gstride = 2L * p.latent;
+  } else {
+    const int ch = EM == E_STORE ? p.N : p.epi_xf.channels;
+    o.rstride = 2L * p.N; o.groups = 1; o.rpg = (int)(p.det_rows);
+    o.cols = 2 * ch; o.cw = ch; o.hstride = p.N; o.folds = p.N / ch; o.fstride = ch;
+    o.dst[0] = EM == E_STORE ? p.sum : p.dbeta;
+    o.dst[1] = EM == E_STORE ? p.sumsq : p.dgamma;
+  }
+  return ordered_sum_launch(o, st);
+}
+
 // A launch whose dynamic tables are large (> 64 KB: BatchNorm widths of 2048-4096 channels) is
 // checked against the LDS budget with the kernel's own static LDS; the launch is skipped and
 // check_launch's caller sees VAE_E_UNSUPPORTED through lds_error.
@@ -294,8 +334,8 @@ inline int launch_tiled(GemmParams p, Tile t, hipStream_t st) {
   }
   int rc = check_launch("igemm");
   if (rc) return rc;
-  if (EM != E_ACC && p.slab) return launch_finalize<T, EM>(p, st);
-  return VAE_OK;
+  if (p.slab && (rc = launch_finalize<T, EM>(p, st))) return rc;
+  return det_reduce<EM>(p, st);
 }
 
 // ------------------------------------------------------------------ direct-fragment GEMM path
@@ -371,7 +411,7 @@ inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req
   if (p.M <= 0 || p.N <= 0) return VAE_OK;
   finish_divs(p);
   if constexpr (BMD == B_NK && AM != A_KM && EM != E_ACC) {
-    if (!a_f32 && !b_f32 && split_req <= 0 && fgemm_ok<AM, BMD, EM>(p, 0, 0)) {
+    if (!a_f32 && !b_f32 && split_req <= 0 && !p.det && fgemm_ok<AM, BMD, EM>(p, 0, 0)) {
       if (dtype == VAE_F32) return launch_fgemm<float, float, AM, EM, DYA>(p, ws, ws_bytes, st);
       if (dtype == VAE_BF16) return launch_fgemm<__bf16, __bf16, AM, EM, DYA>(p, ws, ws_bytes, st);
     }
@@ -388,13 +428,32 @@ inline int launch(int dtype, bool a_f32, bool b_f32, GemmParams p, int split_req
   }
   const int ktiles = (kmax + bk - 1) / bk;
   const long blocks = (long)((p.M + t.bm - 1) / t.bm) * ((p.N + t.bn - 1) / t.bn) * p.nphase;
-  const bool slab = EM != E_ACC;
+  if (p.det && dtype != VAE_F32) return fail(VAE_E_UNSUPPORTED, "deterministic reductions need dtype VAE_F32");
+  // deterministic weight gradients: K slices to a slab (<= 64 MB) summed by the finalize instead
+  // of fp32 atomics into dW
+  const bool slab = EM != E_ACC || p.det;
   int split = split_req > 0 ? split_req : pick_split(blocks, ktiles);
+  if (EM == E_ACC && p.det && split_req <= 0) {
+    const long cap = (64l << 20) / ((long)p.M * p.N * p.nphase * 4);
+    if (split > cap) split = cap < 1 ? 1 : (int)cap;
+  }
   if (slab && split > 1) {
     if (int rc = split_fits(&split, split_req, p, ws, ws_bytes, "igemm split-K")) return rc;
     if (split > 1) p.slab = static_cast<float*>(ws);
   }
   p.ksplit = split < 1 ? 1 : split;
+  if (p.det) {
+    const long off = p.slab ? (((long)p.ksplit * p.M * p.N * p.nphase * 4 + 255) & ~255l) : 0;
+    const long need = det_slab_bytes<EM>(p, t.bm);
+    if (need > 0) {
+      if (!ws && !querying()) return fail(VAE_E_BADARG, "igemm: a deterministic call needs a workspace");
+      if (!ws_fits(off + need, ws_bytes, "igemm deterministic sums")) return VAE_E_BADARG;
+      p.det_slab = reinterpret_cast<float*>(static_cast<char*>(ws) + off);
+      p.det_rows = det_wants_sums<EM>(p) ? det_sum_rows(p, t.bm) : 0;
+      if (EM == E_REPARAM && p.M % p.samples) return fail(VAE_E_BADARG, "igemm: rows %d not a multiple of samples %d", p.M, p.samples);
+      if (EM == E_BNBWD && p.N % p.epi_xf.channels) return fail(VAE_E_UNSUPPORTED, "igemm: %d columns over %d channels", p.N, p.epi_xf.channels);
+    }
+  }
   if (dtype == VAE_F32) return launch_tiled<float, float, float, AM, BMD, EM, DYA, DYB>(p, t, st);
   if (dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "dtype %d", dtype);
   if constexpr (A_F32) {
@@ -665,6 +724,9 @@ inline bool geom_ok(const vae_conv_args* a, const char* what) {
   if (a->n <= 0 || a->h <= 0 || a->w <= 0 || a->c <= 0 || a->k <= 0 || a->p <= 0 || a->q <= 0 || a->r <= 0 ||
       a->stride <= 0 || a->pad < 0) {
     fail(VAE_E_BADSHAPE, "%s: bad geometry", what); return false;
+  }
+  if (a->deterministic && a->dtype != VAE_F32) {
+    fail(VAE_E_UNSUPPORTED, "%s: deterministic reductions need dtype VAE_F32", what); return false;
   }
   return true;
 }

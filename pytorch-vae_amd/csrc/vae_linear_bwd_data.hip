@@ -12,6 +12,7 @@ extern "C" int vae_linear_bwd_data(const vae_linear_args* a, void* stream) {
   if (!a || !a->dy || !a->wt || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_bwd_data: args");
   if (!a->mulv && !epi_ok(a->dx_epi, "linear_bwd_data.epi")) return VAE_E_BADARG;
   GemmParams p = base_params();
+  p.det = a->deterministic;
   p.M = a->m; p.N = a->k; p.K = a->n;
   p.a_ptr = a->dy; p.a_ld = a->n;
   p.b_ptr = a->wt; p.b_ld = a->k;

@@ -11,10 +11,12 @@ extern "C" int vae_linear_bwd_filter(const vae_linear_args* a, void* stream) {
   if (!a || !a->dy || !a->x || !a->dw || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_bwd_filter: args");
   if (!xf_ok(a->x_xf, "linear_bwd_filter.x")) return VAE_E_BADARG;
   GemmParams p = base_params();
+  p.det = a->deterministic;
   p.M = a->n; p.N = a->k + (a->db ? 1 : 0); p.K = a->m;
   p.ones_col = a->db ? a->k : -1; p.bias_grad = a->db;
   p.a_ptr = a->dy; p.a_ld = a->n;
   p.b_ptr = a->x; p.b_ld = a->k; p.b_xf = sanitize(a->x_xf);
   p.out = a->dw; p.out_ld = a->k;
-  return launch<A_KM, B_KN, E_ACC, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, nullptr, 0, (hipStream_t)stream);
+  return launch<A_KM, B_KN, E_ACC, false, false, true>(a->dtype, a->dy_f32 != 0, false, p, 0, p.det ? a->workspace : nullptr,
+                                                          p.det ? a->workspace_bytes : 0, (hipStream_t)stream);
 }

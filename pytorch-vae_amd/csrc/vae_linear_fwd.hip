@@ -10,6 +10,7 @@ extern "C" int vae_linear_fwd(const vae_linear_args* a, void* stream) {
   if (!a || !a->x || !a->wt || !a->y || a->m <= 0 || a->n <= 0 || a->k <= 0) return fail(VAE_E_BADARG, "linear_fwd: args");
   if (!xf_ok(a->x_xf, "linear_fwd.x")) return VAE_E_BADARG;
   GemmParams p = base_params();
+  p.det = a->deterministic;
   p.M = a->m; p.N = a->n; p.K = a->k;
   p.a_ptr = a->x; p.a_ld = a->k; p.a_xf = sanitize(a->x_xf);
   p.b_ptr = a->wt; p.b_ld = a->k;

@@ -9,6 +9,7 @@
 #include <math.h>
 
 #include "vae_common.hpp"
+#include "vae_elbo.hpp"
 
 namespace vae {
 
@@ -54,6 +55,7 @@ struct HeadP {
   int sum_reps, sum_rstride;
   float* dw; float* db;
   const float* grad_recon;
+  float* det_slab;           // deterministic calls: per-workgroup partial rows (OrdSum)
 };
 
 __device__ __forceinline__ float act_of(const vae_xform& xf, const float* ta, const float* tb, float v, int ch) {
@@ -174,7 +176,8 @@ __global__ void __launch_bounds__(HEAD_T) head_fwd_kernel(HeadP p) {
   if (threadIdx.x == 0) {
     float t = 0.f;
     for (int i = 0; i < HEAD_T / 64; ++i) t += red[i];
-    atomicAdd(p.sse + n, t);
+    if (p.det_slab) p.det_slab[blockIdx.x] = t;
+    else atomicAdd(p.sse + n, t);
   }
 }
 
@@ -260,8 +263,14 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_data_kernel(HeadP p) {
     __syncthreads();
     const long roff = p.sum_reps > 1 ? (long)(blockIdx.x % p.sum_reps) * p.sum_rstride : 0;
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      atomicAdd(p.dbeta + roff + c, r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c]);
-      atomicAdd(p.dgamma + roff + c, r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c]);
+      const float b = r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c], g = r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c];
+      if (p.det_slab) {
+        p.det_slab[(long)blockIdx.x * 2 * C + c] = b;
+        p.det_slab[(long)blockIdx.x * 2 * C + C + c] = g;
+      } else {
+        atomicAdd(p.dbeta + roff + c, b);
+        atomicAdd(p.dgamma + roff + c, g);
+      }
     }
   }
 }
@@ -348,8 +357,14 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_data_wide_kernel(HeadP p) {
       __syncthreads();
       if (threadIdx.x < CW) {
         const int c = threadIdx.x;
-        atomicAdd(p.dbeta + roff + c0 + c, r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c]);
-        atomicAdd(p.dgamma + roff + c0 + c, r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c]);
+        const float b = r1[0][c] + r1[1][c] + r1[2][c] + r1[3][c], g = r2[0][c] + r2[1][c] + r2[2][c] + r2[3][c];
+        if (p.det_slab) {
+          p.det_slab[(long)blockIdx.x * 2 * C + c0 + c] = b;
+          p.det_slab[(long)blockIdx.x * 2 * C + C + c0 + c] = g;
+        } else {
+          atomicAdd(p.dbeta + roff + c0 + c, b);
+          atomicAdd(p.dgamma + roff + c0 + c, g);
+        }
       }
     }
   }
@@ -409,7 +424,10 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
     const int idx = threadIdx.x + i * HEAD_T;
     if (idx >= nidx) break;
 #pragma unroll
-    for (int co = 0; co < CO; ++co) atomicAdd(p.dw + co * nidx + idx, acc[i][co]);
+    for (int co = 0; co < CO; ++co) {
+      if (p.det_slab) p.det_slab[(long)blockIdx.x * (CO * nidx + CO) + co * nidx + idx] = acc[i][co];
+      else atomicAdd(p.dw + co * nidx + idx, acc[i][co]);
+    }
   }
   if (p.db) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -423,7 +441,8 @@ __global__ void __launch_bounds__(HEAD_T) head_bwd_filter_kernel(HeadP p) {
     if (threadIdx.x < CO) {
       float t = 0.f;
       for (int i = 0; i < HEAD_T / 64; ++i) t += red[threadIdx.x][i];
-      atomicAdd(p.db + threadIdx.x, t);
+      if (p.det_slab) p.det_slab[(long)blockIdx.x * (CO * nidx + CO) + CO * nidx + threadIdx.x] = t;
+      else atomicAdd(p.db + threadIdx.x, t);
     }
   }
 }
@@ -435,6 +454,8 @@ int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
   if (a->w <= 0 || a->w > 256 || HEAD_T % a->w || a->h % (HEAD_T / a->w))
     return fail(VAE_E_UNSUPPORTED, "%s: spatial %dx%d (need w | 256 and (256/w) | h)", what, a->h, a->w);
   if (a->dtype != VAE_F32 && a->dtype != VAE_BF16) return fail(VAE_E_BADDTYPE, "%s: dtype", what);
+  if (a->deterministic && a->dtype != VAE_F32)
+    return fail(VAE_E_UNSUPPORTED, "%s: deterministic reductions need dtype VAE_F32", what);
   memset(&p, 0, sizeof(p));
   p.n = a->n; p.h = a->h; p.w = a->w; p.c = a->c; p.rows = HEAD_T / a->w;
   p.samples = a->samples > 0 ? a->samples : 1;
@@ -446,6 +467,16 @@ int head_setup(const vae_head_args* a, HeadP& p, const char* what) {
   p.dw = a->dw; p.db = a->db; p.grad_recon = a->grad_recon;
   if (p.xf.channels <= 0) p.xf.channels = a->c;
   if (p.epi.channels <= 0) p.epi.channels = a->c;
+  return VAE_OK;
+}
+
+// A deterministic head call keeps its per-workgroup partials (`floats` of them) at the start of
+// the workspace; the entry point adds them with ordered_sum_launch after its kernel.
+int head_det(const vae_head_args* a, HeadP& p, long floats, const char* what) {
+  if (!a->deterministic || floats <= 0) return VAE_OK;
+  if (!a->workspace && !querying()) return fail(VAE_E_BADARG, "%s: a deterministic call needs a workspace", what);
+  if (!ws_fits(floats * 4, a->workspace_bytes, what)) return VAE_E_BADARG;
+  p.det_slab = static_cast<float*>(a->workspace);
   return VAE_OK;
 }
 
@@ -485,97 +516,7 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
   kernarg_prefetch<(sizeof(vae_elbo_args) < 1024 ? sizeof(vae_elbo_args) : 1024)>();
   __shared__ float kld_row[1024];
   __shared__ float red[4][4];
-  const int B = a.batch, S = a.samples > 0 ? a.samples : 1, D = a.latent;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // kld_b = -0.5 Σ_d (1 + lv - mu^2 - exp(lv)): 4 threads per row, each a quarter of the latent
-  // dims with all its loads in flight at once (64 rows per pass)
-  if (a.kind != VAE_LOSS_VQ) {
-    const int part = threadIdx.x & 3, per = (D + 3) / 4;
-    for (int b0 = 0; b0 < B; b0 += 64) {
-      const int b = b0 + (threadIdx.x >> 2);
-      float s = 0.f;
-      if (b < B) {
-        const float* mu = a.mulv + (long)b * 2 * D;
-        const float* lv = mu + D;
-        const int d0 = part * per, d1 = min(D, d0 + per);
-#pragma unroll 32
-        for (int d = d0; d < d1; ++d) s += 1.f + lv[d] - mu[d] * mu[d] - expf(lv[d]);
-      }
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      if (part == 0 && b < B) kld_row[b] = -0.5f * s;
-    }
-  }
-  __syncthreads();
-  const float inv_img = 1.f / (float)a.img_elems;
-  // totals: Σ sse, Σ kld_b
-  float ts = 0.f, tk = 0.f;
-  for (int i = threadIdx.x; i < B * S; i += 256) ts += a.sse[i];
-  for (int b = threadIdx.x; b < B && a.kind != VAE_LOSS_VQ; b += 256) tk += kld_row[b];
-  for (int off = 32; off > 0; off >>= 1) { ts += __shfl_xor(ts, off); tk += __shfl_xor(tk, off); }
-  if (lane == 0) { red[0][wv] = ts; red[1][wv] = tk; }
-  __syncthreads();
-  const float sse_tot = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-  const float kld_mean = (red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)B;
-  for (int i = threadIdx.x; i < B * S; i += 256) a.per_img[i] = a.sse[i] * inv_img;
-
-  if (a.kind == VAE_LOSS_VQ) {                  // vq_vae.py:203-211
-    const float recon = sse_tot / ((float)B * (float)a.img_elems);
-    const float vq = (1.f + a.vq_beta) * (*a.vq_sse) / a.vq_elems;
-    if (threadIdx.x == 0) { a.out[0] = recon + vq; a.out[1] = recon; a.out[2] = vq; a.out[3] = 0.f; }
-    return;
-  }
-  if (a.kind != VAE_LOSS_IWAE) {
-    const float recon = sse_tot / ((float)B * (float)a.img_elems);
-    float loss, klc, kld_report;
-    if (a.kind == VAE_LOSS_VANILLA) {
-      loss = recon + a.kld_weight * kld_mean; klc = a.kld_weight; kld_report = -kld_mean;
-    } else if (a.kind == VAE_LOSS_BETA_H) {
-      loss = recon + a.beta * a.kld_weight * kld_mean; klc = a.beta * a.kld_weight; kld_report = kld_mean;
-    } else {
-      const float it = a.iter ? *a.iter : 1.f;
-      const float C = fminf(fmaxf(a.c_max / a.c_stop_iter * it, 0.f), a.c_max);
-      const float dlt = kld_mean - C;
-      loss = recon + a.gamma * a.kld_weight * fabsf(dlt);
-      klc = a.gamma * a.kld_weight * (dlt > 0.f ? 1.f : (dlt < 0.f ? -1.f : 0.f));
-      kld_report = kld_mean;
-    }
-    const float hc = 2.f / ((float)B * (float)a.img_elems);
-    for (int i = threadIdx.x; i < B; i += 256) { a.head_coef[i] = hc; a.kl_coef[i] = klc / (float)B; }
-    if (threadIdx.x == 0) { a.out[0] = loss; a.out[1] = recon; a.out[2] = kld_report; a.out[3] = kld_mean; }
-    return;
-  }
-  // IWAE: lw[b,s] = sse/img + M_N*kld_b ; w = softmax_s(lw) ; loss = mean_b Σ_s w lw
-  float lsum = 0.f;
-  for (int b = threadIdx.x; b < B; b += 256) {
-    float mx = -INFINITY;
-    for (int s = 0; s < S; ++s) mx = fmaxf(mx, a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b]);
-    float den = 0.f;
-    for (int s = 0; s < S; ++s) den += expf(a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b] - mx);
-    float wl = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const float lw = a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b];
-      wl += expf(lw - mx) / den * lw;
-    }
-    for (int s = 0; s < S; ++s) {
-      const float lw = a.sse[b * S + s] * inv_img + a.kld_weight * kld_row[b];
-      const float w = expf(lw - mx) / den;
-      const float g = w * (1.f + lw - wl) / (float)B;          // dL/dlw
-      a.head_coef[b * S + s] = g * 2.f * inv_img;
-      a.kl_coef[b * S + s] = g * a.kld_weight;
-    }
-    lsum += wl;
-  }
-  for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
-  __syncthreads();
-  if (lane == 0) red[2][wv] = lsum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    a.out[0] = (red[2][0] + red[2][1] + red[2][2] + red[2][3]) / (float)B;
-    a.out[1] = sse_tot * inv_img / (float)(B * S);
-    a.out[2] = -kld_mean;
-    a.out[3] = kld_mean;
-  }
+  elbo_block(a, kld_row, red);
 }
 
 // ---------------------------------------------------------------------------- Adam
@@ -622,7 +563,59 @@ int grid_for(long n, int per_block = 256, int max_blocks = 2048) {
   return (int)(b > max_blocks ? max_blocks : b);
 }
 
+// The ordered pass of a deterministic call (OrdSum, vae_common.hpp): 32 outputs per workgroup,
+// 8 row lanes each taking the rows r = lane (mod 8) in ascending order, the 8 lane totals added
+// in lane order — a fixed summation tree whatever the timing.
+__global__ void __launch_bounds__(256) ordered_sum_kernel(const OrdSum o) {
+  __shared__ float part[8][33];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const long e = (long)blockIdx.x * 32 + cl;
+  const bool ok = e < (long)o.groups * o.cols;
+  const int g = ok ? (int)(e / o.cols) : 0;
+  const int c = ok ? (int)(e - (long)g * o.cols) : 0;
+  const int half = c / o.cw, cc = c - half * o.cw;
+  const float* base = o.slab + (long)g * o.rpg * o.rstride + (long)half * o.hstride + cc;
+  float s = 0.f;
+  if (ok) {
+    int r = rl;
+    for (; r + 24 < o.rpg; r += 32) {                      // 4 rows' loads in flight
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float t = 0.f;
+        for (int f = 0; f < o.folds; ++f) t += base[(long)(r + 8 * u) * o.rstride + (long)f * o.fstride];
+        v[u] = t;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; r < o.rpg; r += 8) {
+      float t = 0.f;
+      for (int f = 0; f < o.folds; ++f) t += base[(long)r * o.rstride + (long)f * o.fstride];
+      s += t;
+    }
+  }
+  part[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && ok) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) t += part[l][cl];
+    float* d = o.dst[half] + (long)g * o.gstride + cc;
+    *d += t;
+  }
+}
+
 }  // namespace
+
+int ordered_sum_launch(const OrdSum& o, hipStream_t st) {
+  const long outs = (long)o.groups * o.cols;
+  if (outs <= 0 || o.rpg <= 0) return VAE_OK;
+  if (!o.slab || !o.dst[0] || (o.cols > o.cw && !o.dst[1]))
+    return fail(VAE_E_BADARG, "ordered_sum: null slab or destination");
+  VAE_LAUNCH(ordered_sum_kernel, dim3((unsigned)((outs + 31) / 32)), dim3(256), 0, st, o);
+  return check_launch("ordered_sum");
+}
 }  // namespace vae
 
 using namespace vae;
@@ -675,9 +668,15 @@ extern "C" int vae_head_fwd(const vae_head_args* a, void* stream) {
   if (rc != kHeadFallback) return rc;
   const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (head_cw(p.c) + 4) * sizeof(float);
   if (lds > 64 * 1024) return fail(VAE_E_UNSUPPORTED, "head_fwd: tile too large");
+  if ((rc = head_det(a, p, p.tiles, "head_fwd"))) return rc;
   if (a->dtype == VAE_F32) VAE_LAUNCH(head_fwd_kernel<float>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   else VAE_LAUNCH(head_fwd_kernel<__bf16>, dim3(p.tiles), dim3(HEAD_T), lds, (hipStream_t)stream, p);
-  return check_launch("head_fwd");
+  if ((rc = check_launch("head_fwd")) || !p.det_slab) return rc;
+  OrdSum o;                                          // sse[n] += the image's tiles, in tile order
+  memset(&o, 0, sizeof(o));
+  o.slab = p.det_slab; o.rstride = 1; o.groups = p.n; o.rpg = p.h / p.rows; o.cols = 1; o.cw = 1; o.folds = 1;
+  o.dst[0] = p.sse; o.gstride = 1;
+  return ordered_sum_launch(o, (hipStream_t)stream);
 }
 
 extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
@@ -691,6 +690,8 @@ extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
   rc = head_bwd_mfma_launch(a, true, false, st);
   if (rc != kHeadFallback) return rc;
   const bool f = a->dtype == VAE_F32;
+  const bool sums = p.epi.kind == VAE_X_BN_ACT;
+  if (sums && (rc = head_det(a, p, (long)p.tiles * 2 * p.c, "head_bwd_data"))) return rc;
   switch (a->c) {
     case 32:
       if (f) VAE_LAUNCH((head_bwd_data_kernel<float, 32>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
@@ -706,7 +707,12 @@ extern "C" int vae_head_bwd_data(const vae_head_args* a, void* stream) {
       else VAE_LAUNCH((head_bwd_data_wide_kernel<__bf16>), dim3(p.tiles), dim3(HEAD_T), 0, st, p);
       break;
   }
-  return check_launch("head_bwd_data");
+  if ((rc = check_launch("head_bwd_data")) || !p.det_slab) return rc;
+  OrdSum o;                                          // Σg, Σg·x̂ over the tiles, in tile order
+  memset(&o, 0, sizeof(o));
+  o.slab = p.det_slab; o.rstride = 2L * p.c; o.groups = 1; o.rpg = p.tiles; o.cols = 2 * p.c; o.cw = p.c;
+  o.hstride = p.c; o.folds = 1; o.dst[0] = p.dbeta; o.dst[1] = p.dgamma;
+  return ordered_sum_launch(o, st);
 }
 
 extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
@@ -719,9 +725,16 @@ extern "C" int vae_head_bwd_filter(const vae_head_args* a, void* stream) {
   if (rc != kHeadFallback) return rc;
   const size_t lds = (size_t)(p.rows + 2) * (p.w + 2) * (head_cw(p.c) + 4) * sizeof(float);
   const int grid = p.tiles < 256 ? p.tiles : 256;
+  const int nw = CO * 9 * p.c;                       // dW elements; db follows in a partial row
+  if ((rc = head_det(a, p, (long)grid * (nw + CO), "head_bwd_filter"))) return rc;
   if (a->dtype == VAE_F32) VAE_LAUNCH(head_bwd_filter_kernel<float>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
   else VAE_LAUNCH(head_bwd_filter_kernel<__bf16>, dim3(grid), dim3(HEAD_T), lds, (hipStream_t)stream, p);
-  return check_launch("head_bwd_filter");
+  if ((rc = check_launch("head_bwd_filter")) || !p.det_slab) return rc;
+  OrdSum o;                                          // dW, db over the workgroups, in order
+  memset(&o, 0, sizeof(o));
+  o.slab = p.det_slab; o.rstride = nw + CO; o.groups = 1; o.rpg = grid; o.cols = p.db ? nw + CO : nw; o.cw = nw;
+  o.hstride = nw; o.folds = 1; o.dst[0] = p.dw; o.dst[1] = p.db;
+  return ordered_sum_launch(o, (hipStream_t)stream);
 }
 
 extern "C" int vae_bn_finalize(const vae_bn_args* a, void* stream) { return vae::bn_finalize_launch(a, (hipStream_t)stream); }
@@ -747,9 +760,10 @@ extern "C" int vae_head_bwd(const vae_head_args* a, void* stream) {
   HeadP p;
   int rc = head_setup(a, p, "head_bwd");
   if (rc) return rc;
-  if ((!a->coef && !a->grad_recon) || !a->dx || !a->dw) return fail(VAE_E_BADARG, "head_bwd: coef/grad_recon/dx/dw");
+  if ((!a->coef && !a->grad_recon && !a->elbo) || !a->dx || !a->dw) return fail(VAE_E_BADARG, "head_bwd: coef/grad_recon/dx/dw");
   if (p.epi.kind == VAE_X_BN_ACT && (!p.dgamma || !p.dbeta || !p.epi.aux)) return fail(VAE_E_BADARG, "head_bwd: BN epilogue");
   rc = head_bwd_mfma_launch(a, true, true, (hipStream_t)stream);
+  if (rc == kHeadFallback && a->elbo) return fail(VAE_E_UNSUPPORTED, "head_bwd: a fused ELBO needs the bf16 MFMA path");
   if (rc == kHeadFallback) {
     if ((rc = vae_head_bwd_data(a, stream))) return rc;
     rc = vae_head_bwd_filter(a, stream);

@@ -60,7 +60,9 @@ __device__ __forceinline__ wgm_bf16x4 wgm_tr_read(const char* generic_lds_addr) 
 // MFMA; two workgroups still fit a CU's LDS), 32 below
 template <int BM> constexpr int wg_kp() { return BM >= 128 ? 64 : 32; }
 // operand tiles of one workgroup (bytes of LDS): 2 buffers x (U + V) rows of KP pixels
-template <int BM, int BJ> constexpr int wgemm_lds_bytes() { return 2 * wg_kp<BM>() * (wg_rs<BM>() + wg_rs<BJ>()); }
+template <int BM, int BJ, int KPX = 0> constexpr int wgemm_lds_bytes() {
+  return 2 * (KPX > 0 ? KPX : wg_kp<BM>()) * (wg_rs<BM>() + wg_rs<BJ>());
+}
 
 // Accumulator tile -> dW (or this K slice's partial slab): lane element (i, j, e) is row
 // mrow + 16i + e, column jcol + 16j, at offset row * rowstride + coff + column.  A single K slice
@@ -126,10 +128,11 @@ __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, cons
 #endif
 // nunits > 1 (the grouped launch, vae_wgrad_batch.hip): the workgroup runs work units bid0 ..
 // bid0 + nunits - 1 of its layer one after another, building the BatchNorm tables once.
-template <int BM, int BJ, int XU, int XV>
+// KPX: pixels per K-step (0: wg_kp<BM>; the grouped launch runs its 64-wide tiles at 64)
+template <int BM, int BJ, int XU, int XV, int KPX = 0>
 __device__ __forceinline__ void wgemm_body(const WgParams& p, const int bid0, char* lds,
                                            unsigned long long* clk = nullptr, const int nunits = 1) {
-  constexpr int KP = wg_kp<BM>();
+  constexpr int KP = KPX > 0 ? KPX : wg_kp<BM>();
   constexpr int RSU = wg_rs<BM>(), RSV = wg_rs<BJ>();
   constexpr int CU = BM / 8, CV = BJ / 8;              // 16-byte chunks per pixel row
   constexpr int RPU = 256 / CU, RPV = 256 / CV;        // pixel rows per pass

@@ -69,9 +69,13 @@ struct Wg3Group {
 };
 static_assert(sizeof(Wg3Group) <= 7680, "kernel argument block");
 
+// pixels per K-step of the 64-wide per-tap bodies (the standalone kernel's 32 halve the MFMA work
+// per barrier)
+constexpr int kWg3KP = 64;
 constexpr int wg3_max(int a, int b) { return a > b ? a : b; }
 constexpr int wg3_lds() {
-  return wg3_max(wgemm_taps_lds_bytes<32, 32, 3>(), wg3_max(wgemm_lds_bytes<64, 64>(), wgemm_lds_bytes<64, 128>()));
+  return wg3_max(wgemm_taps_lds_bytes<32, 32, 3>(),
+                 wg3_max(wgemm_lds_bytes<64, 64, kWg3KP>(), wgemm_lds_bytes<64, 128, kWg3KP>()));
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) wg3_kernel(const Wg3Group g) {
@@ -95,14 +99,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) w
     case 1: wgemm_taps_body<32, 32, VAE_X_BN_DY, VAE_X_BN_ACT, 3>(p, bid, lds, clkp); break;
     case 2: wgemm_taps_body<32, 32, VAE_X_NONE, VAE_X_BN_DY, 3>(p, bid, lds, clkp); break;
     case 3: wgemm_taps_body<32, 32, VAE_X_BN_ACT, VAE_X_BN_DY, 3>(p, bid, lds, clkp); break;
-    case 4: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds, clkp, nu); break;
-    case 5: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds, clkp, nu); break;
-    case 6: wgemm_body<64, 64, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
-    case 7: wgemm_body<64, 64, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
-    case 8: wgemm_body<64, 128, VAE_X_BN_DY, VAE_X_NONE>(p, bid, lds, clkp, nu); break;
-    case 9: wgemm_body<64, 128, VAE_X_BN_DY, VAE_X_BN_ACT>(p, bid, lds, clkp, nu); break;
-    case 10: wgemm_body<64, 128, VAE_X_NONE, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
-    default: wgemm_body<64, 128, VAE_X_BN_ACT, VAE_X_BN_DY>(p, bid, lds, clkp, nu); break;
+    case 4: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_NONE, kWg3KP>(p, bid, lds, clkp, nu); break;
+    case 5: wgemm_body<64, 64, VAE_X_BN_DY, VAE_X_BN_ACT, kWg3KP>(p, bid, lds, clkp, nu); break;
+    case 6: wgemm_body<64, 64, VAE_X_NONE, VAE_X_BN_DY, kWg3KP>(p, bid, lds, clkp, nu); break;
+    case 7: wgemm_body<64, 64, VAE_X_BN_ACT, VAE_X_BN_DY, kWg3KP>(p, bid, lds, clkp, nu); break;
+    case 8: wgemm_body<64, 128, VAE_X_BN_DY, VAE_X_NONE, kWg3KP>(p, bid, lds, clkp, nu); break;
+    case 9: wgemm_body<64, 128, VAE_X_BN_DY, VAE_X_BN_ACT, kWg3KP>(p, bid, lds, clkp, nu); break;
+    case 10: wgemm_body<64, 128, VAE_X_NONE, VAE_X_BN_DY, kWg3KP>(p, bid, lds, clkp, nu); break;
+    default: wgemm_body<64, 128, VAE_X_BN_ACT, VAE_X_BN_DY, kWg3KP>(p, bid, lds, clkp, nu); break;
   }
   WG_PROBE_END(i, bid, x);
 }
@@ -204,14 +208,14 @@ inline bool wg3_layer(const WgParams& w0, int idx, Wg3Layer* L) {
     L->step_us = 1.2 + bytes / 51200.0;
   } else if (p.J >= 128) {                             // 64 x 128 tiles, one tap per workgroup
     L->var = 8 + var;
-    L->KP = wg_kp<64>();
+    L->KP = kWg3KP;
     L->tiles = (long)((p.M + 63) / 64) * ((p.J + 127) / 128) * p.R * p.R;
-    L->step_us = 0.95;
+    L->step_us = 0.95 * kWg3KP / 32 * 0.75;
   } else {                                             // 64 x 64 tiles, one tap per workgroup
     L->var = 4 + var;
-    L->KP = wg_kp<64>();
+    L->KP = kWg3KP;
     L->tiles = (long)((p.M + 63) / 64) * ((p.J + 63) / 64) * p.R * p.R;
-    L->step_us = 0.65;
+    L->step_us = 0.65 * kWg3KP / 32 * 0.75;
   }
   L->steps = (npix + L->KP - 1) / L->KP;
   L->p = p;

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # any other value V loads libvaehip_V.so (a build-flag variant for A/B timing)
 if os.environ.get("VAE_HIP_LIB"):
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_%s.so" % os.environ["VAE_HIP_LIB"])
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -55,7 +55,7 @@ class ConvArgs(ctypes.Structure):
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
                 ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
                 ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("wt_t", c_void_p),
-                ("dw_inner", c_int32)]
+                ("dw_inner", c_int32), ("deterministic", c_int32)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -67,7 +67,7 @@ class LinearArgs(ctypes.Structure):
                 ("dw", c_void_p), ("db", c_void_p),
                 ("mulv", c_void_p), ("eps", c_void_p), ("kl_coef", c_void_p), ("dmulv", c_void_p),
                 ("samples", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
-                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p)]
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("deterministic", c_int32)]
 
 
 class HeadArgs(ctypes.Structure):
@@ -78,7 +78,8 @@ class HeadArgs(ctypes.Structure):
                 ("dx_dbeta", c_void_p), ("sum_reps", c_int32), ("sum_rstride", c_int32),
                 ("dw", c_void_p), ("db", c_void_p), ("grad_recon", c_void_p),
                 ("workspace", c_void_p), ("workspace_bytes", c_int64),
-                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p)]
+                ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("elbo", c_void_p),
+                ("deterministic", c_int32)]
 
 
 class ElboArgs(ctypes.Structure):

@@ -135,10 +135,14 @@ class TrainStep:
             if p.loss_kind == L.LOSS_BETA_B:
                 p.num_iter.add_(1.0)
             p._run(p.fwd_calls[skip:], st)
-            if self.comm is not None:
+            if self.comm is not None and not getattr(p, "elbo_in_head", False):
                 p.metrics.copy_(p.out)
         lo = 0 if k == 0 else self.buckets[k - 1][0]
         p._run(p.bwd_calls[lo:self.buckets[k][0]], st)
+        if k == 0 and self.comm is not None and getattr(p, "elbo_in_head", False):
+            # the loss terms come from the head backward (vae_head_args.elbo), the first call of
+            # segment 0's backward: copied behind it, reduced with the last bucket as before
+            p.metrics.copy_(p.out)
 
     def _opt(self):
         self.opt.apply(self.plan.grads, L.stream_ptr())

@@ -134,8 +134,13 @@ class StepPlan:
                  samples: int = 1, beta: float = 4.0, gamma: float = 1000.0, max_capacity: float = 25.0,
                  capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
                  concurrent: bool = False, fuse_bn: bool = False, bn_in_consumer: bool = True,
-                 wg_overlap: bool = False, recon_loss: Optional[dict] = None):
+                 wg_overlap: bool = False, recon_loss: Optional[dict] = None,
+                 deterministic: Optional[bool] = None):
         self.net = net
+        # deterministic: every cross-workgroup reduction of the step in a fixed order (vaehip.h
+        # vae_conv_args.deterministic), so two runs of the same step give bit-identical gradients;
+        # the default for fp32 (parity) plans, unsupported by the bf16 kernels.
+        self.deterministic = (net.dtype == torch.float32) if deterministic is None else bool(deterministic)
         # recon_loss (the Autoencoder's other reconstruction losses, vaehip.h vae_recon_loss):
         # {"kind": "center", "mask": [H][W] device tensor} or {"kind": "mssim", "window": 1-D window}.
         # The loss runs inside the step in place of the ELBO and seeds the backward with its
@@ -305,6 +310,11 @@ class StepPlan:
             first_lin = next((i for i, (fn, _) in enumerate(raw) if fn == "vae_linear_bwd_data"), None)
             if first_lin is not None:
                 splits = [first_lin]
+        if self.deterministic:
+            for fn, ref in list(self.fwd_calls) + list(self.bwd_calls_raw):
+                obj = getattr(ref, "_obj", ref)
+                if hasattr(obj, "deterministic"):
+                    obj.deterministic = 1
         self.bwd_calls, new_ends = batch_filter_calls(self.bwd_calls_raw, ends, splits)
         size_workspaces(self, [self.fwd_calls, self.bwd_calls])
         return new_ends
@@ -596,9 +606,16 @@ class StepPlan:
         e.kl_coef = self.kl_coef.data_ptr()
         self.n_decode1 = len(F)
         self.elbo_args = e
+        # elbo_in_head: the loss evaluated by the head backward (vaehip.h vae_head_args.elbo: one
+        # extra workgroup of its filter-partial reduction, the seed coefficient a constant) instead
+        # of a vae_elbo_fwd launch between the forward and the backward — the bf16 head kernels,
+        # the vanilla / BetaVAE-H losses (their seeds do not depend on the batch), one sample
+        self.elbo_in_head = (self.fused_loss and self.training and self.recon_loss is None and not self.wide_head
+                             and self.S == 1 and T == L.BF16
+                             and self.loss_kind in (L.LOSS_VANILLA, L.LOSS_BETA_H))
         if self.recon_loss is not None:
             self._add_recon_loss(F)
-        elif self.fused_loss:
+        elif self.fused_loss and not self.elbo_in_head:
             self._add(F, "vae_elbo_fwd", e)
 
         # ================================================================ backward
@@ -622,6 +639,8 @@ class StepPlan:
         self.bwd_sums(hb, "final_layer.1")
         hb.dw = self.g("final_layer.3.weight")
         hb.db = self.g("final_layer.3.bias")
+        if self.elbo_in_head:
+            hb.elbo = ctypes.addressof(e)
         if self.wide_head:
             self._wide_head_bwd(Bw, cnt)
             self._head_bwd = None

@@ -149,6 +149,23 @@ def test_step_bf16_close(case):
     assert abs(out[2] - meta["loss"]["KLD"]) <= 2e-2 * abs(meta["loss"]["KLD"])
 
 
+@pytest.mark.parametrize("case", CASES)
+def test_step_is_bit_reproducible(case):
+    """Two runs of the teacher-forced fp32 step of test_step_matches_reference give bit-identical
+    loss terms, reconstructions, mu/log_var, per-image MSE, every gradient and the BatchNorm running
+    statistics: fp32 plans reduce in a fixed order (StepPlan(deterministic=True), vaehip.h
+    vae_conv_args.deterministic) instead of with float atomics."""
+    meta, _ = load_case(case)
+    runs = []
+    for _ in range(2):
+        net, plan, _opt = _run_step(meta)
+        assert plan.deterministic
+        runs.append([t.detach().cpu().clone() for t in (plan.out, plan.recon, plan.mulv, plan.per_img, plan.grads,
+                                                         net.running)])
+    for name, a, b in zip(("out", "recon", "mulv", "per_img", "grads", "running"), *runs):
+        assert torch.equal(a, b), (case, name, float((a - b).abs().max()))
+
+
 def test_step_with_fused_bn_finalize_matches_separate():
     """StepPlan(fuse_bn=True): every BatchNorm finalisation folded into the last workgroup of the
     GEMM that produced its statistics (vaehip.h bn_finalize/bn_counter) gives the same step."""
