@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 22
+#define VAE_ABI_VERSION 23
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -474,6 +474,11 @@ typedef struct vae_step_begin_args {
   void* y;
   int32_t npad;
   vae_pad_desc pad[VAE_PAD_MAX];
+  /* up to VAE_SWAP_MAX swapped-axes weight copies (what vae_swap_axes does with these descriptors),
+   * refreshed from the fp32 weights as the step starts — after the previous step's optimizer,
+   * before the first GEMM that reads them — instead of a launch of their own behind the optimizer */
+  int32_t nswap;
+  vae_swap_desc swap[VAE_SWAP_MAX];
 } vae_step_begin_args;
 int vae_step_begin_ex(const vae_step_begin_args* a, void* stream);
 

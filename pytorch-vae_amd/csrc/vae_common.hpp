@@ -503,4 +503,29 @@ __device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, b
   tab_build(x, t, epi, update_running, scr);
 }
 
+// One 32x32 (a, b) tile of one tap of a swapped-axes weight copy (vae_swap_axes): dst[b][tap][a] =
+// bf16(src[a][tap][b]) through a padded LDS tile, so reads and writes are both 64-byte row segments
+// (an element-wise gather reads with a stride of rs*b elements).  blk < swap_tiles(d).
+__host__ __device__ inline int swap_tiles(const vae_swap_desc& d) { return ((d.a + 31) / 32) * ((d.b + 31) / 32) * d.rs; }
+__device__ __forceinline__ void swap_tile(const vae_swap_desc& d, int blk, float (*t)[33]) {
+  const int nb = (d.b + 31) / 32, na = (d.a + 31) / 32;
+  const int bt = blk % nb; blk /= nb;
+  const int at = blk % na;
+  const int tap = blk / na;
+  const int a0 = at * 32, b0 = bt * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* src = static_cast<const float*>(d.src);
+  __bf16* dst = static_cast<__bf16*>(d.dst);
+  for (int j = ty; j < 32; j += 8) {
+    const int a = a0 + j, b = b0 + tx;
+    t[j][tx] = (a < d.a && b < d.b) ? src[((long)a * d.rs + tap) * d.b + b] : 0.f;
+  }
+  __syncthreads();
+  for (int j = ty; j < 32; j += 8) {
+    const int b = b0 + j, a = a0 + tx;
+    if (a < d.a && b < d.b) dst[((long)b * d.rs + tap) * d.a + a] = (__bf16)t[tx][j];
+  }
+}
+
 }  // namespace vae
+

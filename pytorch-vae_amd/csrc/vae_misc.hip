@@ -520,26 +520,59 @@ __global__ void __launch_bounds__(256) elbo_kernel(vae_elbo_args a) {
 }
 
 // ---------------------------------------------------------------------------- Adam
-template <bool LOWP>
-__global__ void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, const int* step, const float* lr, double b1, double b2, float eps,
-                            float wd, __bf16* __restrict__ lowp) {
+struct AdamK {
+  float omb1, omb2, b2f, step_size, bc2s, eps, wd;
+};
+__device__ __forceinline__ float adam_elem(const AdamK& k, float& pi, float gi, float& mi, float& vi) {
+  if (k.wd != 0.f) gi = fmaf(k.wd, pi, gi);
+  mi = mi + k.omb1 * (gi - mi);                                      // lerp (torch Adam)
+  vi = vi * k.b2f + k.omb2 * gi * gi;                                // mul_(beta2).addcmul_(g, g, 1-beta2)
+  const float den = sqrtf(vi) / k.bc2s + k.eps;
+  pi = pi - k.step_size * (mi / den);
+  return pi;
+}
+// V = 4: 16-byte accesses (the four fp32 arrays 16-byte aligned, the bf16 copy 8-byte aligned),
+// the n % 4 tail by block 0; V = 1: one element per access
+template <bool LOWP, int V>
+__global__ void __launch_bounds__(256) adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, const int* step,
+                                                   const float* lr, double b1, double b2, float eps, float wd,
+                                                   __bf16* __restrict__ lowp) {
   // torch.optim.Adam (single-tensor path): the scalars it derives from the Python-float
   // hyper-parameters (1 - beta, bias corrections, step size) are formed in double and rounded
   // once, as torch does — 1 - 0.999f in fp32 would be 1.3e-5 off 1 - 0.999
   const double t = (double)(*step);
-  const float omb1 = (float)(1.0 - b1), omb2 = (float)(1.0 - b2), b2f = (float)b2;
   const double bc1 = 1.0 - pow(b1, t), bc2 = 1.0 - pow(b2, t);
-  const float step_size = (float)((double)*lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    float gi = g[i];
-    float pi = p[i];
-    if (wd != 0.f) gi = fmaf(wd, pi, gi);
-    const float mi = m[i] + omb1 * (gi - m[i]);                       // lerp (torch Adam)
-    const float vi = v[i] * b2f + omb2 * gi * gi;                     // mul_(beta2).addcmul_(g, g, 1-beta2)
-    const float den = sqrtf(vi) / bc2s + eps;
-    pi = pi - step_size * (mi / den);
+  const AdamK k{(float)(1.0 - b1), (float)(1.0 - b2), (float)b2, (float)((double)*lr / bc1), (float)sqrt(bc2), eps, wd};
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long nv = n / V;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    if constexpr (V == 4) {
+      f32x4 p4 = reinterpret_cast<const f32x4*>(p)[i];
+      const f32x4 g4 = reinterpret_cast<const f32x4*>(g)[i];
+      f32x4 m4 = reinterpret_cast<const f32x4*>(m)[i];
+      f32x4 v4 = reinterpret_cast<const f32x4*>(v)[i];
+      float pe[4], me[4], ve[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pe[e] = p4[e]; me[e] = m4[e]; ve[e] = v4[e];
+        adam_elem(k, pe[e], g4[e], me[e], ve[e]);
+      }
+      reinterpret_cast<f32x4*>(p)[i] = f32x4{pe[0], pe[1], pe[2], pe[3]};
+      reinterpret_cast<f32x4*>(m)[i] = f32x4{me[0], me[1], me[2], me[3]};
+      reinterpret_cast<f32x4*>(v)[i] = f32x4{ve[0], ve[1], ve[2], ve[3]};
+      if (LOWP) reinterpret_cast<bf16x4*>(lowp)[i] = bf16x4{(__bf16)pe[0], (__bf16)pe[1], (__bf16)pe[2], (__bf16)pe[3]};
+    } else {
+      float pi = p[i], mi = m[i], vi = v[i];
+      adam_elem(k, pi, g[i], mi, vi);
+      m[i] = mi; v[i] = vi; p[i] = pi;
+      if (LOWP) lowp[i] = (__bf16)pi;
+    }
+  }
+  if (V > 1 && blockIdx.x == 0 && threadIdx.x < n - nv * V) {
+    const long i = nv * V + threadIdx.x;
+    float pi = p[i], mi = m[i], vi = v[i];
+    adam_elem(k, pi, g[i], mi, vi);
     m[i] = mi; v[i] = vi; p[i] = pi;
     if (LOWP) lowp[i] = (__bf16)pi;
   }
@@ -802,11 +835,19 @@ extern "C" int vae_adam_step(int64_t n, float* p, const float* g, float* m, floa
                              void* stream) {
   if (n <= 0) return VAE_OK;
   if (!p || !g || !m || !v || !step || !lr) return fail(VAE_E_BADARG, "adam_step: null");
-  const int grid = grid_for(n);
-  if (p_lowp)
-    VAE_LAUNCH(adam_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)p_lowp);
-  else
-    VAE_LAUNCH(adam_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, (__bf16*)nullptr);
+  auto al = [](const void* q, uintptr_t a) { return ((uintptr_t)q % a) == 0; };
+  const bool vec = al(p, 16) && al(g, 16) && al(m, 16) && al(v, 16) && (!p_lowp || al(p_lowp, 8));
+  const hipStream_t st = (hipStream_t)stream;
+  __bf16* lp = (__bf16*)p_lowp;
+  if (vec) {
+    const int grid = grid_for((n + 3) / 4);
+    if (p_lowp) VAE_LAUNCH((adam_kernel<true, 4>), dim3(grid), dim3(256), 0, st, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, lp);
+    else VAE_LAUNCH((adam_kernel<false, 4>), dim3(grid), dim3(256), 0, st, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, lp);
+  } else {
+    const int grid = grid_for(n);
+    if (p_lowp) VAE_LAUNCH((adam_kernel<true, 1>), dim3(grid), dim3(256), 0, st, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, lp);
+    else VAE_LAUNCH((adam_kernel<false, 1>), dim3(grid), dim3(256), 0, st, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, lp);
+  }
   return check_launch("adam_step");
 }
 
@@ -913,25 +954,7 @@ __global__ void __launch_bounds__(256) swap_axes_kernel(const SwapBatch sb) {
   __shared__ float t[32][33];
   int i = 0;
   while (i + 1 < sb.count && (int)blockIdx.x >= sb.tiles0[i + 1]) ++i;
-  const vae_swap_desc d = sb.d[i];
-  int blk = blockIdx.x - sb.tiles0[i];
-  const int nb = (d.b + 31) / 32, na = (d.a + 31) / 32;
-  const int bt = blk % nb; blk /= nb;
-  const int at = blk % na;
-  const int tap = blk / na;
-  const int a0 = at * 32, b0 = bt * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const float* src = static_cast<const float*>(d.src);
-  __bf16* dst = static_cast<__bf16*>(d.dst);
-  for (int j = ty; j < 32; j += 8) {
-    const int a = a0 + j, b = b0 + tx;
-    t[j][tx] = (a < d.a && b < d.b) ? src[((long)a * d.rs + tap) * d.b + b] : 0.f;
-  }
-  __syncthreads();
-  for (int j = ty; j < 32; j += 8) {
-    const int b = b0 + j, a = a0 + tx;
-    if (a < d.a && b < d.b) dst[((long)b * d.rs + tap) * d.a + a] = (__bf16)t[tx][j];
-  }
+  swap_tile(sb.d[i], blockIdx.x - sb.tiles0[i], t);
 }
 }  // namespace
 
@@ -946,7 +969,7 @@ extern "C" int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* st
     if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0) return fail(VAE_E_BADARG, "swap_axes: descriptor %d", i);
     sb.d[i] = d;
     sb.tiles0[i] = tiles;
-    tiles += ((d.a + 31) / 32) * ((d.b + 31) / 32) * d.rs;
+    tiles += swap_tiles(d);
   }
   sb.tiles0[count] = tiles;
   sb.count = count;

@@ -5,6 +5,9 @@
 //   [nz, nz + nx)      the fp32 NCHW image -> NHWC with cp channels (zeros above c), one pixel per
 //                      thread, one 16-byte store per pixel for bf16 / cp = 8 — vae_nchw_to_nhwc_pad
 //   [nz + nx, ...)     up to VAE_PAD_MAX padded weight copies — vae_pad_channels
+//   [..., end)         up to VAE_SWAP_MAX swapped-axes weight copies — vae_swap_axes (they read the fp32
+//                      weights the previous step's optimizer wrote; measured as a launch of their own
+//                      behind the optimizer: 8.5 us per VanillaVAE step, profiles/r5p)
 // The reference's step (experiment.py:45-49) feeds the image straight into the first Conv2d
 // (models/vanilla_vae.py:84); the padding exists only so that the first layer runs on the packed
 // 16-byte GEMM operand path.  profiles/r3a: the three separate launches took 6.5 + 5.2 + 4.8 us.
@@ -19,6 +22,8 @@ struct StepBegin {
   int ntail;             // bytes after them
   int nz, nx;            // blocks of the zeroing and of the image ranges
   int pad0[VAE_PAD_MAX + 1];   // first block of each pad descriptor (relative to nz + nx)
+  int np;                      // blocks of the pad range
+  int swap0[VAE_SWAP_MAX + 1]; // first block of each swap descriptor (relative to nz + nx + np)
 };
 
 template <class T>
@@ -56,6 +61,14 @@ __global__ void __launch_bounds__(256) step_begin_ex_kernel(const StepBegin s) {
     return;
   }
   const int pb = b - s.nz - s.nx;
+  if (pb >= s.np) {
+    __shared__ float t[32][33];
+    const int sb = pb - s.np;
+    int k = 0;
+    while (k + 1 < s.a.nswap && sb >= s.swap0[k + 1]) ++k;
+    swap_tile(s.a.swap[k], sb - s.swap0[k], t);
+    return;
+  }
   int k = 0;
   while (k + 1 < s.a.npad && pb >= s.pad0[k + 1]) ++k;
   const vae_pad_desc& d = s.a.pad[k];
@@ -98,7 +111,17 @@ extern "C" int vae_step_begin_ex(const vae_step_begin_args* a, void* stream) {
     nb += (int)((d.rows * d.cp + 255) / 256);
   }
   s.pad0[a->npad] = nb;
-  const dim3 grid((unsigned)(s.nz + s.nx + nb));
+  s.np = nb;
+  if (a->nswap < 0 || a->nswap > VAE_SWAP_MAX) return fail(VAE_E_BADARG, "step_begin_ex: %d swaps", a->nswap);
+  int ns = 0;
+  for (int k = 0; k < a->nswap; ++k) {
+    const vae_swap_desc& d = a->swap[k];
+    if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0) return fail(VAE_E_BADARG, "step_begin_ex: swap %d", k);
+    s.swap0[k] = ns;
+    ns += swap_tiles(d);
+  }
+  s.swap0[a->nswap] = ns;
+  const dim3 grid((unsigned)(s.nz + s.nx + nb + ns));
   if (a->dtype == VAE_BF16) VAE_LAUNCH(step_begin_ex_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, s);
   else VAE_LAUNCH(step_begin_ex_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, s);
   return check_launch("step_begin_ex");

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # any other value V loads libvaehip_V.so (a build-flag variant for A/B timing)
 if os.environ.get("VAE_HIP_LIB"):
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_%s.so" % os.environ["VAE_HIP_LIB"])
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -144,7 +144,8 @@ class PadDesc(ctypes.Structure):
 class StepBeginArgs(ctypes.Structure):
     _fields_ = [("zero", c_void_p), ("bytes", c_int64), ("step", c_void_p), ("dtype", c_int32),
                 ("n", c_int32), ("c", c_int32), ("h", c_int32), ("w", c_int32), ("cp", c_int32),
-                ("x", c_void_p), ("y", c_void_p), ("npad", c_int32), ("pad", PadDesc * PAD_MAX)]
+                ("x", c_void_p), ("y", c_void_p), ("npad", c_int32), ("pad", PadDesc * PAD_MAX),
+                ("nswap", c_int32), ("swap", SwapDesc * SWAP_MAX)]
 
 
 class LatentArgs(ctypes.Structure):

@@ -9,6 +9,7 @@ buffer with RCCL between the backward graph and the optimizer graph.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Optional
 
@@ -38,14 +39,20 @@ class FusedAdam:
     def set_lr(self, lr: float):
         self.lr.fill_(float(lr))
 
-    def apply(self, grads: torch.Tensor, stream=None):
+    def apply(self, grads: torch.Tensor, stream=None, refresh_swaps: bool = True):
+        """One Adam step over the flat parameters (writes the bf16 copy).  refresh_swaps=False leaves
+        the swapped-axes weight copies stale (net.swaps_stale) for a caller that refreshes them at the
+        start of its next step (TrainStep: inside vae_step_begin_ex)."""
         net = self.net
         L.call("vae_adam_step", net.params.numel(), net.params.data_ptr(), grads.data_ptr(), self.m.data_ptr(),
                self.v.data_ptr(), self.step.data_ptr(), self.lr.data_ptr(), self.betas[0], self.betas[1], self.eps,
                self.weight_decay, net.lowp.data_ptr() if net.lowp is not None else None,
                stream if stream is not None else L.stream_ptr())
         if getattr(net, "swap_descs", None) is not None:
-            net.refresh_swaps(stream)
+            if refresh_swaps:
+                net.refresh_swaps(stream)
+            else:
+                net.swaps_stale = True
 
 
 PAD_FNS = ("vae_nchw_to_nhwc_pad", "vae_pad_channels")
@@ -69,6 +76,13 @@ def begin_args(plan, step: torch.Tensor):
             break
         k += 1
     a.npad = npad
+    # the swapped-axes weight copies the bf16 GEMMs read (net.swap_descs), refreshed in the same
+    # launch from the weights the previous step's optimizer wrote
+    sw = getattr(plan.net, "swap_descs", None)
+    if isinstance(sw, ctypes.Array) and 0 < len(sw) <= L.SWAP_MAX:      # (VQNet: several arrays)
+        a.nswap = len(sw)
+        for i in range(len(sw)):
+            a.swap[i] = sw[i]
     return a, k
 
 
@@ -119,6 +133,7 @@ class TrainStep:
         # the step's head (zeroing, step count, image and weight padding) as one launch;
         # VAE_NO_BEGIN_EX=1 keeps vae_step_begin + the padding calls (A/B timing)
         self._begin = None if os.environ.get("VAE_NO_BEGIN_EX") else begin_args(plan, opt.step)
+        self._begin_swaps = self._begin is not None and self._begin[0].nswap > 0
 
     # -------------------------------------------------------------- eager pieces
     def _segment(self, k: int):
@@ -130,6 +145,8 @@ class TrainStep:
             if self._begin is not None:
                 args, skip = self._begin
                 L.call("vae_step_begin_ex", args, st)
+                if self._begin_swaps:
+                    self.net.swaps_stale = False        # (refreshed by that launch)
             else:
                 L.call("vae_step_begin", p.zero.data_ptr(), p.zero.numel() * 4, self.opt.step.data_ptr(), st)
             if p.loss_kind == L.LOSS_BETA_B:
@@ -145,7 +162,8 @@ class TrainStep:
             p.metrics.copy_(p.out)
 
     def _opt(self):
-        self.opt.apply(self.plan.grads, L.stream_ptr())
+        # with the swapped copies refreshed by the next step's head, the optimizer skips its own pass
+        self.opt.apply(self.plan.grads, L.stream_ptr(), refresh_swaps=not self._begin_swaps)
 
     def _capture(self):
         # warm up on a side stream (allocations, lazy init), then capture
@@ -215,6 +233,8 @@ class TrainStep:
             self._opt()
         if bcast is not None:
             bcast.wait()                 # before the next step's forward updates them
+        if self._begin_swaps:
+            self.net.swaps_stale = True  # the swapped copies follow at the next step's head
         self.net.num_batches_tracked += 1
 
     def loss_terms(self):

@@ -78,6 +78,7 @@ class VAENet:
         self.swap_descs, self.lowp_t = make_swaps(self.layout, self.params, names, self.device, self.wt_t)
 
     def refresh_swaps(self, stream=None):
+        self.swaps_stale = False
         if self.swap_descs is not None:
             L.call("vae_swap_axes", len(self.swap_descs), ctypes.byref(self.swap_descs),
                    stream if stream is not None else L.stream_ptr())
@@ -1040,6 +1041,11 @@ def run_calls(plan, calls, stream):
     on `stream` before it and runs on the side stream; the side stream is joined back into
     `stream` at the end of the list.  Recorded inside a HIP graph capture this becomes the
     graph's fork/join edges, so the replayed graph runs the two chains concurrently."""
+    net = getattr(plan, "net", None)
+    if getattr(net, "swaps_stale", False):
+        # the swapped-axes weight copies trail the last optimizer step (a TrainStep refreshes them
+        # inside its next step's head launch): bring them up to date before anything reads them
+        net.refresh_swaps(stream)
     side = getattr(plan, "side", None)
     main = torch.cuda.current_stream() if side is not None else None
     if main is not None and main.cuda_stream != stream:
