@@ -585,15 +585,18 @@ inline int cg_minwg() { return kCgMinWg; }
 inline int cg_splitwg() { return kCgSplitWg; }
 
 // Largest tile that still gives every CU ~2 workgroups; split-K (slabs + igemm_finalize) when
-// even the smallest leaves the chip half empty and K is deep.
-inline CgTile cg_pick(long M, long N, int nphase, long table_bytes = 0) {
+// even the smallest leaves the chip half empty and K is deep.  xform: the gathered operand is
+// transformed on load (BatchNorm tables, a second raw tensor for BN_DY): those instantiations hold
+// two 64 x 32 workgroups per CU, so a 64 x 32 grid of 4 per CU ran as two rounds (tools/kprobe.py:
+// the encoder.1 data gradient's second round started 11.9 us in, 21.9 us in all) — 128 x 32 from 4
+// per CU makes it one round; transform-free layers keep it for the long thin maps only.
+inline CgTile cg_pick(long M, long N, int nphase, long table_bytes = 0, bool xform = false) {
   const CgTile c[] = {{128, 128}, {128, 32}, {64, 64}, {64, 32}, {32, 64}, {32, 32}};
   for (const CgTile& t : c) {
     if (table_bytes + cg_static_bytes(t.bm, t.bn) > kLdsBytes) continue;   // (wide BatchNorm tables)
     if (t.bm > 32 && M < t.bm) continue;
     if (t.bn > 32 && N < t.bn) continue;
-    // 128 x 32 only for the long thin maps (>= 8 workgroups per CU at 64 x 32)
-    if (t.bm == 128 && t.bn == 32 && tile_blocks(M, N, nphase, Tile{64, 32}) < 8 * kCUs) continue;
+    if (t.bm == 128 && t.bn == 32 && tile_blocks(M, N, nphase, Tile{64, 32}) < (xform ? 4 : 8) * kCUs) continue;
     if (tile_blocks(M, N, nphase, Tile{t.bm, t.bn}) >= (long)cg_minwg() * kCUs) return t;
   }
   return CgTile{32, 32};
@@ -641,7 +644,8 @@ inline int cg_launch(GemmParams p, int split_req, void* ws, long ws_bytes, hipSt
     const int rc = bgemm_launch(p, AM, EM, ws, ws_bytes, st);
     if (rc != kHeadFallback) return rc;
   }
-  const CgTile t = cg_pick(p.M, p.N, p.nphase, cg_table_bytes(p, EM));
+  const CgTile t = cg_pick(p.M, p.N, p.nphase, cg_table_bytes(p, EM),
+                           p.a_xf.kind == VAE_X_BN_ACT || p.a_xf.kind == VAE_X_BN_DY);
   const int bk = t.bm >= 128 ? 64 : 128;
   // tile order (vae_cgemm.hpp): m fastest when the weights outweigh the gathered input tensor
   p.m_fast = (long)p.b_bytes > (long)p.a_bytes ? 1 : 0;
