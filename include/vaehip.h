@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 23
+#define VAE_ABI_VERSION 24
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -404,6 +404,8 @@ typedef struct vae_swap_desc {
   const void* src;
   void* dst;
   int32_t a, rs, b;
+  int32_t src_dtype;                 /* VAE_F32 (the master weights) or VAE_BF16 (their bf16 copy:
+                                        half the bytes, the same rounded values) */
 } vae_swap_desc;
 int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* stream);
 /* --- workspace queries ----------------------------------------------------

@@ -504,7 +504,7 @@ __device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, b
 }
 
 // One 32x32 (a, b) tile of one tap of a swapped-axes weight copy (vae_swap_axes): dst[b][tap][a] =
-// bf16(src[a][tap][b]) through a padded LDS tile, so reads and writes are both 64-byte row segments
+// bf16(src[a][tap][b]) (src fp32, or already bf16) through a padded LDS tile, so reads and writes are both 64-byte row segments
 // (an element-wise gather reads with a stride of rs*b elements).  blk < swap_tiles(d).
 __host__ __device__ inline int swap_tiles(const vae_swap_desc& d) { return ((d.a + 31) / 32) * ((d.b + 31) / 32) * d.rs; }
 __device__ __forceinline__ void swap_tile(const vae_swap_desc& d, int blk, float (*t)[33]) {
@@ -514,11 +514,13 @@ __device__ __forceinline__ void swap_tile(const vae_swap_desc& d, int blk, float
   const int tap = blk / na;
   const int a0 = at * 32, b0 = bt * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const float* src = static_cast<const float*>(d.src);
   __bf16* dst = static_cast<__bf16*>(d.dst);
   for (int j = ty; j < 32; j += 8) {
     const int a = a0 + j, b = b0 + tx;
-    t[j][tx] = (a < d.a && b < d.b) ? src[((long)a * d.rs + tap) * d.b + b] : 0.f;
+    const long i = ((long)a * d.rs + tap) * d.b + b;
+    t[j][tx] = !(a < d.a && b < d.b) ? 0.f
+               : d.src_dtype == VAE_BF16 ? (float)static_cast<const __bf16*>(d.src)[i]
+                                         : static_cast<const float*>(d.src)[i];
   }
   __syncthreads();
   for (int j = ty; j < 32; j += 8) {

@@ -966,7 +966,8 @@ extern "C" int vae_swap_axes(int32_t count, const vae_swap_desc* descs, void* st
   int tiles = 0;
   for (int i = 0; i < count; ++i) {
     const vae_swap_desc& d = descs[i];
-    if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0) return fail(VAE_E_BADARG, "swap_axes: descriptor %d", i);
+    if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0 || (d.src_dtype != VAE_F32 && d.src_dtype != VAE_BF16))
+      return fail(VAE_E_BADARG, "swap_axes: descriptor %d", i);
     sb.d[i] = d;
     sb.tiles0[i] = tiles;
     tiles += swap_tiles(d);

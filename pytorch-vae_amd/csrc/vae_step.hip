@@ -116,7 +116,8 @@ extern "C" int vae_step_begin_ex(const vae_step_begin_args* a, void* stream) {
   int ns = 0;
   for (int k = 0; k < a->nswap; ++k) {
     const vae_swap_desc& d = a->swap[k];
-    if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0) return fail(VAE_E_BADARG, "step_begin_ex: swap %d", k);
+    if (!d.src || !d.dst || d.a <= 0 || d.b <= 0 || d.rs <= 0 || (d.src_dtype != VAE_F32 && d.src_dtype != VAE_BF16))
+      return fail(VAE_E_BADARG, "step_begin_ex: swap %d", k);
     s.swap0[k] = ns;
     ns += swap_tiles(d);
   }

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # any other value V loads libvaehip_V.so (a build-flag variant for A/B timing)
 if os.environ.get("VAE_HIP_LIB"):
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_%s.so" % os.environ["VAE_HIP_LIB"])
-ABI_VERSION = 23
+ABI_VERSION = 24
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -130,7 +130,8 @@ class RecordArgs(ctypes.Structure):
 
 
 class SwapDesc(ctypes.Structure):
-    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("a", c_int32), ("rs", c_int32), ("b", c_int32)]
+    _fields_ = [("src", c_void_p), ("dst", c_void_p), ("a", c_int32), ("rs", c_int32), ("b", c_int32),
+                ("src_dtype", c_int32)]
 
 
 SWAP_MAX = 16

@@ -75,7 +75,7 @@ class VAENet:
             return
         names = ([f"encoder.{i}.0.weight" for i in range(1, len(self.hidden_dims))] +
                  [f"decoder.{i}.0.weight" for i in range(len(self.hidden_dims) - 1)] + ["final_layer.0.weight"])
-        self.swap_descs, self.lowp_t = make_swaps(self.layout, self.params, names, self.device, self.wt_t)
+        self.swap_descs, self.lowp_t = make_swaps(self.layout, self.params, names, self.device, self.wt_t, self.lowp)
 
     def refresh_swaps(self, stream=None):
         self.swaps_stale = False
@@ -1074,10 +1074,11 @@ def call_one(fn, arg, stream):
         L.call(fn, arg, stream)
 
 
-def make_swaps(layout: Layout, params: torch.Tensor, names, device, out: Dict[str, int]):
+def make_swaps(layout: Layout, params: torch.Tensor, names, device, out: Dict[str, int], lowp=None):
     """Descriptor array for vae_swap_axes over the named conv / convT weights (native
     [a][r][s][b] -> bf16 [b][r][s][a]) and the bf16 buffer holding the copies; `out` maps
-    each name to its copy's device pointer."""
+    each name to its copy's device pointer.  lowp: the bf16 copy of `params` to read instead of
+    the fp32 master (the same rounded values, half the bytes); it must be refreshed first."""
     specs = [layout.by_name[n] for n in names if n in layout.by_name]
     if len(specs) > L.SWAP_MAX:
         raise ValueError(f"{len(specs)} swapped weights > {L.SWAP_MAX} per vae_swap_axes launch")
@@ -1088,7 +1089,10 @@ def make_swaps(layout: Layout, params: torch.Tensor, names, device, out: Dict[st
     for i, (spec, n) in enumerate(zip(specs, sizes)):
         a, r, r2, b = spec.native_shape
         d = descs[i]
-        d.src = params.data_ptr() + 4 * spec.offset
+        if lowp is not None:
+            d.src, d.src_dtype = lowp.data_ptr() + 2 * spec.offset, L.BF16
+        else:
+            d.src, d.src_dtype = params.data_ptr() + 4 * spec.offset, L.F32
         d.dst = buf.data_ptr() + 2 * o
         d.a, d.rs, d.b = a, r * r2, b
         out[spec.name] = d.dst
