@@ -96,6 +96,14 @@ constexpr int cg_ring(int loads) {
   return kRingLoads / loads < 2 ? 2 : (kRingLoads / loads > kRingMax ? kRingMax : kRingLoads / loads);
 }
 template <int LOADS> constexpr int cg_stages() { return cg_ring(LOADS); }
+// OR == 3: a one-round kernel with twice the ring, for forward grids of at most two workgroups per
+// CU (the deep layers: 256-512 tiles of 5-10 K-steps), whose occupancy the extra registers do not
+// lower — their whole K slice is requested in the prologue instead of one ring refill per step
+// (VanillaVAE forward convs 1-2 us each faster)
+constexpr int kRingLoadsDeep = 40, kRingMaxDeep = 16;
+constexpr int cg_ring_deep(int loads) {
+  return kRingLoadsDeep / loads < 2 ? 2 : (kRingLoadsDeep / loads > kRingMaxDeep ? kRingMaxDeep : kRingLoadsDeep / loads);
+}
 // the weight-gradient kernels keep ~20 loads in flight (their K slices are sized for it)
 template <int LOADS> constexpr int wg_stages() {
   return 20 / LOADS < 2 ? 2 : (20 / LOADS > 8 ? 8 : 20 / LOADS);
@@ -129,7 +137,7 @@ __device__ __forceinline__ void cgemm_body(const GemmParams& p, const int bid, c
   constexpr int RPP = 256 / KC;                      // rows covered per pass of the block
   constexpr int APT = (BM + RPP - 1) / RPP, BPT = (BN + RPP - 1) / RPP;
   constexpr bool DY = XA == VAE_X_BN_DY;
-  constexpr int NSF = cg_stages<APT * (DY ? 2 : 1) + BPT>();
+  constexpr int NSF = OR == 3 ? cg_ring_deep(APT * (DY ? 2 : 1) + BPT) : cg_stages<APT * (DY ? 2 : 1) + BPT>();
   constexpr int NS = OR == 2 ? (NSF < 2 ? NSF : 2) : NSF;
   // OR == 2 keeps one LDS buffer (a barrier between its two steps): with half the LDS, 4-6
   // workgroups fit a CU instead of 2-3 — these big-M launches have thousands of short workgroups
