@@ -263,11 +263,26 @@ def _profiles(pattern, arch):
     return sorted(paths, key=key, reverse=True)
 
 
-def _matching_profile(pattern, arch, kernels, digest):
+def _profile_workload(d):
+    """(arch, batch) a profile summary was measured on, from the bench arguments it records
+    (tools/pmc_summary.py / prof_summary.py --config; none given = the default VanillaVAE B=64)."""
+    toks = str(d.get("config") or "").split()
+    arch, batch = "vanilla", None
+    for i, t in enumerate(toks[:-1]):
+        if t == "--arch":
+            arch = toks[i + 1]
+        elif t == "--batch":
+            batch = int(toks[i + 1])
+    return arch, batch if batch is not None else 64
+
+
+def _matching_profile(pattern, arch, kernels, digest, batch=None):
     """Newest profiles/ summary measured on THIS build (its `digest` equals the loaded library's
-    vae_build_digest, i.e. the same csrc sources) that holds EVERY kernel of the call; else None
+    vae_build_digest, i.e. the same csrc sources) and on this workload (arch and batch: the same
+    kernels of another batch size move other bytes) that holds EVERY kernel of the call; else None
     with the reason."""
     why = "no profiles/%s summary" % pattern
+    want = (arch, batch if batch is not None else 64)
     for path in _profiles(pattern, arch):
         try:
             d = json.load(open(path))
@@ -275,6 +290,9 @@ def _matching_profile(pattern, arch, kernels, digest):
             continue
         if d.get("digest") != digest:
             why = f"no {pattern} summary of this build (digest {digest})"
+            continue
+        if _profile_workload(d) != want:
+            why = f"no {pattern} summary of this build for {want[0]} batch {want[1]}"
             continue
         rows = {k: _row_of(k_, d.get("kernels", {})) for k_ in kernels for k in [k_[1]]}
         if any(v is None for v in rows.values()):
@@ -284,11 +302,11 @@ def _matching_profile(pattern, arch, kernels, digest):
     return None, None, why
 
 
-def pmc_traffic(kernels, digest, arch="vanilla"):
+def pmc_traffic(kernels, digest, arch="vanilla", batch=None):
     """HBM bytes per launch of a call = the sum over ITS kernels (tools/pmc_summary.py: 2 x
     FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md §HBM) from a PMC summary of this very build that
     holds all of them; otherwise None (with the reason)."""
-    path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest)
+    path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest, batch)
     if path is None:
         return None, rows
     per = {k: d["kernels"][r].get("hbm_bytes_per_launch") for k, r in rows.items()}
@@ -302,12 +320,12 @@ def pmc_traffic(kernels, digest, arch="vanilla"):
             "file": os.path.relpath(path, REPO), "digest": d.get("digest"), "head": d.get("head")}, None
 
 
-def step_traffic(calls, digest, arch="vanilla"):
+def step_traffic(calls, digest, arch="vanilla", batch=None):
     """HBM bytes of one whole step from the PMC summary of this build: per call, the per-launch
     bytes of its kernels (a kernel shared by several calls contributes its average once per call,
     so the sum over the step's calls is the step total).  (None, reason) when any kernel is missing."""
     kernels = [k for ks in calls for k in ks]
-    path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest)
+    path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest, batch)
     if path is None:
         return None, rows
     total = 0.0
@@ -320,10 +338,10 @@ def step_traffic(calls, digest, arch="vanilla"):
     return {"bytes": int(total), "file": os.path.relpath(path, REPO)}, None
 
 
-def rocprof_times(kernels, digest, arch="vanilla"):
+def rocprof_times(kernels, digest, arch="vanilla", batch=None):
     """Average duration (us) of a call's kernels in a rocprofv3 --kernel-trace --stats summary of
     this build (tools/prof_summary.py), or None (with the reason)."""
-    path, d, rows = _matching_profile("*kstats*.json", arch, kernels, digest)
+    path, d, rows = _matching_profile("*kstats*.json", arch, kernels, digest, batch)
     if path is None:
         return None, rows
     per = {k: d["kernels"][r]["avg_us"] for k, r in rows.items()}
@@ -596,13 +614,13 @@ def main():
     from vae_amd import _lib as L
     digest = L.load().vae_build_digest().decode()
     kernels = call_kernels(fn, rows_ref[idx])
-    tr, why_tr = pmc_traffic(kernels, digest, args.arch)
+    tr, why_tr = pmc_traffic(kernels, digest, args.arch, args.batch)
     roof["traffic"] = tr["bytes"] if tr else None
     roof["traffic_ratio"] = round(tr["bytes"] / by, 3) if tr and by else None
     roof["traffic_source"] = tr if tr else {"missing": why_tr}
     roof["kernel"] = f"{fn} (call #{idx} of the step; its kernels: {', '.join(k[1] for k in kernels) or 'n/a'})"
     roof["us_per_launch"] = round(us, 2)
-    rp, why_rp = rocprof_times(kernels, digest, args.arch)
+    rp, why_rp = rocprof_times(kernels, digest, args.arch, args.batch)
     roof["rocprof"] = rp if rp else {"missing": why_rp}
     roof["build_digest"] = digest
     roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}
@@ -626,7 +644,7 @@ def main():
                  "step_gflop": round(step_flops / 1e9, 3)}
     # the whole step's counter traffic against its algorithmic bytes
     step_bytes = sum(r[3] for r in rows)
-    st_tr, why_st = step_traffic([call_kernels(f_, r_) for (_, f_, _, _), r_ in zip(rows, rows_ref)], digest, args.arch)
+    st_tr, why_st = step_traffic([call_kernels(f_, r_) for (_, f_, _, _), r_ in zip(rows, rows_ref)], digest, args.arch, args.batch)
     step_roof["algorithmic_bytes"] = int(step_bytes)
     step_roof["traffic"] = st_tr["bytes"] if st_tr else None
     step_roof["traffic_ratio"] = round(st_tr["bytes"] / step_bytes, 3) if st_tr and step_bytes else None
