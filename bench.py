@@ -258,7 +258,7 @@ def _profiles(pattern, arch):
     tag = arch if arch == "vq" or arch in AE_WIDTHS else None
     paths = [p for p in glob.glob(os.path.join(REPO, "profiles", pattern))
              if (re.search(tag + r"(_|\.|$)", os.path.basename(p)) if tag else
-                 not re.search(r"vq|ae_", os.path.basename(p)))]
+                 not re.search(r"(^|_)(vq|ae)_", os.path.basename(p)))]     # (not "iwae_")
     key = lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))]
     return sorted(paths, key=key, reverse=True)
 
