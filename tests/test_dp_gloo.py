@@ -80,7 +80,9 @@ def _worker(rank, world, port, q):
         assert h is not None
         before = float(t[0])
         assert before in (float(rank + 1), float(sum(range(1, world + 1))))   # not yet scaled
+        assert not h.is_completed()          #  the sum may have landed, the mean has not
         h.wait()
+        assert h.is_completed()
         assert torch.equal(t, torch.full_like(t, sum(range(1, world + 1)) / world))
         broadcast_buffers(run)
         err = float((mine - want).abs().max() / want.abs().max())

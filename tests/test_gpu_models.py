@@ -373,3 +373,31 @@ def test_graph_engine_mixed_batch_sizes_share_one_adam_state():
     torch.testing.assert_close(st['exp_avg_sq'], rs['exp_avg_sq'], rtol=1e-5, atol=1e-12)
     torch.testing.assert_close(model.flat.detach(), ref.detach(), rtol=1e-5, atol=1e-6)
     gs.flush()
+
+
+@pytest.mark.parametrize("normalize,size", [(True, 64), (False, 64), (True, 40)])
+def test_mssim_dropin_matches_torch_restatement(normalize, size):
+    """Autoencoder(use_mssim_loss=True).loss_function on CUDA tensors: 64x64 planes on the HIP MS-SSIM
+    kernel (vae_recon_loss) with the module's own `normalize` (the drop-in always used
+    normalize=True), other plane sizes (40x40: the pyramid does not halve exactly, the reference's
+    avg_pool2d floors it) on the torch restatement instead of an error — loss within 1e-4 and
+    dL/drecon within 1e-3 relative of the torch MSSIM (mssim_vae.py:182-282) on the CPU."""
+    from vae_amd.models import MSSIM, vae_models
+    model = vae_models["Autoencoder"](in_channels=3, latent_dim=128, use_mssim_loss=True, dtype=torch.float32,
+                                      device="cuda")
+    model.mssim.normalize = normalize
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand(2, 3, size, size, generator=g)
+    r = (x + 0.05 * torch.randn(x.shape, generator=g)).clamp(0, 1)
+    rc = r.cuda().requires_grad_(True)
+    loss = model.loss_function(rc, x.cuda())["loss"]
+    loss.backward()
+    ref_mod = MSSIM(3, normalize=normalize)
+    rr = r.clone().requires_grad_(True)
+    want = ref_mod(rr, x)
+    want.backward()
+    assert torch.isfinite(want)
+    assert abs(float(loss) - float(want)) <= 1e-4 * abs(float(want)) + 1e-7, (float(loss), float(want))
+    gd = rc.grad.cpu().double()
+    gw = rr.grad.double()
+    assert float((gd - gw).norm() / gw.norm()) < 1e-3
