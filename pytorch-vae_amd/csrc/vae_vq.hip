@@ -187,14 +187,21 @@ __global__ void __launch_bounds__(256) vq_fwd_kernel(vae_vq_args a) {
   if (tid == 0) atomicAdd(a.sse, (red[0] + red[1]) + (red[2] + red[3]));
 }
 
-template <class T>
+// LM: the workgroup merges its rows' codebook-gradient runs in LDS first (a slot per distinct code
+// of its rows), then issues one global atomic per (distinct code, dimension): the runs of the 32-row
+// thread segments were one atomic each, and rows that share a code across threads and row groups
+// (a codebook in use by few codes) all hit the same addresses.  dim <= 64 dividing 256, codes <= 1024.
+constexpr int kVqLdsCodes = 1024;
+constexpr int kVqLdsRows = 512;                            // rows per workgroup at dim 16
+template <class T, bool LM>
 __global__ void __launch_bounds__(256) vq_bwd_kernel(vae_vq_args a) {
   kernarg_prefetch<(sizeof(vae_vq_args) < 1024 ? sizeof(vae_vq_args) : 1024)>();
   const int D = a.dim;
   const int e = threadIdx.x % D;
   const int lanes_rows = 256 / D;                            // row groups per workgroup
   const long r0 = ((long)blockIdx.x * lanes_rows + threadIdx.x / D) * VQB_RUN;
-  if (threadIdx.x >= lanes_rows * D) return;
+  const bool active = threadIdx.x < lanes_rows * D;
+  if (!LM && !active) return;
   const float n = (float)a.rows * (float)D;
   const float s = a.loss_grad ? *a.loss_grad : 1.f;
   const float cz = s * a.beta * 2.f / n, ce = s * 2.f / n;
@@ -208,31 +215,69 @@ __global__ void __launch_bounds__(256) vq_bwd_kernel(vae_vq_args a) {
 #pragma unroll
   for (int i = 0; i < VQB_RUN; ++i) {
     const long r = min(r0 + i, (long)a.rows - 1);
-    kk[i] = a.indices[r];
-    pre[i] = ld_f(lat + r * D + e);
-    dqv[i] = ld_f(dq + r * D + e);
+    kk[i] = active ? a.indices[r] : 0;
+    pre[i] = active ? ld_f(lat + r * D + e) : 0.f;
+    dqv[i] = active ? ld_f(dq + r * D + e) : 0.f;
+  }
+  __shared__ int slot_of[LM ? kVqLdsCodes : 1];
+  __shared__ int code_of[LM ? kVqLdsRows : 1];
+  __shared__ float lacc[LM ? 8192 : 1];
+  __shared__ int nslot;
+  if constexpr (LM) {
+    for (int c = threadIdx.x; c < a.codes; c += 256) slot_of[c] = -1;
+    if (threadIdx.x == 0) nslot = 0;
+    __syncthreads();
+    if (active && e == 0)                                    // mark the codes of this thread's rows
+      for (int i = 0; i < VQB_RUN; ++i)
+        if (r0 + i < a.rows && (unsigned long)kk[i] < (unsigned long)a.codes) slot_of[kk[i]] = -2;
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.codes; c += 256)
+      if (slot_of[c] == -2) {
+        const int sl = atomicAdd(&nslot, 1);
+        slot_of[c] = sl;
+        code_of[sl] = c;
+      }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nslot * D; i += 256) lacc[i] = 0.f;
+    __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < VQB_RUN; ++i) qv[i] = a.codebook[kk[i] * D + e];
+  for (int i = 0; i < VQB_RUN; ++i) qv[i] = active ? a.codebook[kk[i] * D + e] : 0.f;
   long cur = -1;
   float acc = 0.f;
-#pragma unroll
-  for (int i = 0; i < VQB_RUN; ++i) {
-    const long r = r0 + i;
-    if (r >= a.rows) break;
-    const long k = kk[i];
-    const float z = a.lat_xf.kind == VAE_X_ACT ? lrelu(pre[i], a.lat_xf.slope) : pre[i];
-    float g = dqv[i] + cz * (z - qv[i]);
-    if (a.lat_xf.kind == VAE_X_ACT) g = pre[i] > 0.f ? g : g * a.lat_xf.slope;
-    dlat[r * D + e] = cvt<T>(g);
-    if (k != cur) {
-      if (cur >= 0) atomicAdd(a.dcodebook + cur * D + e, acc);
-      cur = k;
-      acc = 0.f;
+  auto flush = [&](long code, float v) {
+    if constexpr (LM) {
+      if ((unsigned long)code < (unsigned long)a.codes) atomicAdd(&lacc[slot_of[code] * D + e], v);
+    } else {
+      atomicAdd(a.dcodebook + code * D + e, v);
     }
-    acc += ce * (qv[i] - z);
+  };
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < VQB_RUN; ++i) {
+      const long r = r0 + i;
+      if (r >= a.rows) break;
+      const long k = kk[i];
+      const float z = a.lat_xf.kind == VAE_X_ACT ? lrelu(pre[i], a.lat_xf.slope) : pre[i];
+      float g = dqv[i] + cz * (z - qv[i]);
+      if (a.lat_xf.kind == VAE_X_ACT) g = pre[i] > 0.f ? g : g * a.lat_xf.slope;
+      dlat[r * D + e] = cvt<T>(g);
+      if (k != cur) {
+        if (cur >= 0) flush(cur, acc);
+        cur = k;
+        acc = 0.f;
+      }
+      acc += ce * (qv[i] - z);
+    }
+    if (cur >= 0) flush(cur, acc);
   }
-  if (cur >= 0) atomicAdd(a.dcodebook + cur * D + e, acc);
+  if constexpr (LM) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < nslot * D; i += 256) {
+      const int sl = i / D, d = i - sl * D;
+      atomicAdd(a.dcodebook + (long)code_of[sl] * D + d, lacc[i]);
+    }
+  }
 }
 
 // Tanh + reconstruction SSE (+ backward seed).  One thread per pixel, 256 pixels of one image per
@@ -419,8 +464,15 @@ extern "C" int vae_vq_bwd(const vae_vq_args* a, void* stream) {
   const int groups = 256 / a->dim;
   const long runs = ((long)a->rows + VQB_RUN - 1) / VQB_RUN;
   const dim3 grid((unsigned)((runs + groups - 1) / groups));
-  if (a->dtype == VAE_F32) VAE_LAUNCH(vq_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, *a);
-  else VAE_LAUNCH(vq_bwd_kernel<__bf16>, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  const bool lm = a->dim <= 64 && 256 % a->dim == 0 && a->dim >= 16 && a->codes <= kVqLdsCodes;
+  const hipStream_t st = (hipStream_t)stream;
+  if (a->dtype == VAE_F32) {
+    if (lm) VAE_LAUNCH((vq_bwd_kernel<float, true>), grid, dim3(256), 0, st, *a);
+    else VAE_LAUNCH((vq_bwd_kernel<float, false>), grid, dim3(256), 0, st, *a);
+  } else {
+    if (lm) VAE_LAUNCH((vq_bwd_kernel<__bf16, true>), grid, dim3(256), 0, st, *a);
+    else VAE_LAUNCH((vq_bwd_kernel<__bf16, false>), grid, dim3(256), 0, st, *a);
+  }
   return check_launch("vq_bwd");
 }
 
