@@ -272,3 +272,38 @@ def test_bf16_mode_tracks_bf16_autocast_oracle():
     print(report)
     for name, e_hip, e_ac in rows:
         assert e_hip <= 2 * e_ac + 2e-3, (name, e_hip, e_ac)
+
+
+@pytest.mark.parametrize("loss", ["vanilla", "betaH"])
+def test_fused_head_elbo_equals_elbo_launch(loss):
+    """The bf16 step evaluates the ELBO inside the head backward's reduction launch
+    (vaehip.h vae_head_args.elbo) instead of a vae_elbo_fwd launch: the same arguments through
+    vae_elbo_fwd on the step's own SSE and mu/log_var give bit-identical loss terms, per-image MSE
+    and KL coefficients, and the head's constant seed coefficient equals what vae_elbo_fwd writes."""
+    import ctypes
+    from vae_amd import _lib as L
+    from vae_amd.net import StepPlan, VAENet
+    net = VAENet(latent_dim=128, dtype=torch.bfloat16, device="cuda", generator=torch.Generator().manual_seed(2))
+    plan = StepPlan(net, 32, loss=loss, kld_weight=2.5e-4)
+    assert plan.elbo_in_head
+    g = torch.Generator(device="cuda").manual_seed(4)
+    plan.x.copy_(torch.rand(plan.x.shape, generator=g, device="cuda"))
+    plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
+    st = L.stream_ptr()
+    plan.begin(st)
+    plan.forward(st)
+    plan.backward(st)
+    torch.cuda.synchronize()
+    e = L.ElboArgs.from_buffer_copy(plan.elbo_args)
+    out = torch.zeros_like(plan.out)
+    per_img = torch.zeros_like(plan.per_img)
+    head_coef = torch.zeros_like(plan.head_coef)
+    kl_coef = torch.zeros_like(plan.kl_coef)
+    e.out, e.per_img, e.head_coef, e.kl_coef = out.data_ptr(), per_img.data_ptr(), head_coef.data_ptr(), kl_coef.data_ptr()
+    L.call("vae_elbo_fwd", ctypes.byref(e), st)
+    torch.cuda.synchronize()
+    assert torch.equal(out, plan.out), (out, plan.out)
+    assert torch.equal(per_img, plan.per_img)
+    assert torch.equal(kl_coef, plan.kl_coef)
+    n_img = plan.x.numel() // plan.x.shape[0]
+    assert torch.allclose(head_coef, torch.full_like(head_coef, 2.0 / (plan.B * n_img)), rtol=1e-6, atol=0)
