@@ -65,6 +65,9 @@ def parse():
                          "ae_vvbig: the Autoencoder of configs/big_ae.yaml / patient_vbig_ae.yaml / "
                          "patient_vvbig_ae.yaml (MSE, no KL)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-comm", action="store_true",
+                    help="N > 1: capture the bucket all-reduces (RCCL) into the step's one graph "
+                         "(engine.TrainStep(graph_comm=True)) instead of issuing them from the host")
     ap.add_argument("--concurrent", choices=["auto", "on", "off"], default="auto",
                     help="weight gradients on a side stream beside the data-gradient chain; auto = off: the "
                          "VanillaVAE family measured 0.88 vs 0.77 ms (r1: the graph's per-call fork/join edges cost "
@@ -575,7 +578,8 @@ def main():
     # eps: drawn inside the step every step on the device (the reference's randn_like,
     # vanilla_vae.py:116) where the fused bottleneck does it; otherwise a resident N(0,1) draw
     ae = args.arch in AE_WIDTHS
-    step = TrainStep(net, plan, opt, graph=not args.no_graph, device_eps=None if ae or args.arch == "vq" else 1265 + rank)
+    step = TrainStep(net, plan, opt, graph=not args.no_graph, device_eps=None if ae or args.arch == "vq" else 1265 + rank,
+                     graph_comm=args.graph_comm)
     if hasattr(plan, "eps") and not ae and not step.device_eps:
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
 
@@ -676,7 +680,8 @@ def main():
                                 f"{'VanillaVAE' if args.arch == 'vanilla' else args.arch} latent_dim=128 "
                                 f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}"),
                    "per_gpu_batch": args.batch, "global_batch": world * args.batch,
-                   "parallelism": f"dp{world}", "graph": not args.no_graph, "comm": comm,
+                   "parallelism": f"dp{world}", "graph": not args.no_graph,
+                   "comm": comm + (" (in-graph)" if getattr(step, "graph_comm", False) else ""),
                    "devices_used": min(world, ndev)},
         "elbo": ({"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1], "finite": finite}
                  if args.arch in AE_WIDTHS else      # (the Autoencoder's loss is the MSE alone)

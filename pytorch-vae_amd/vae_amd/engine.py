@@ -98,7 +98,8 @@ class TrainStep:
     queued, so it runs on the communication stream while the rest of the backward computes."""
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
-                 nbuckets: int = 4, device_eps: Optional[int] = None, force_buckets: bool = False):
+                 nbuckets: int = 4, device_eps: Optional[int] = None, force_buckets: bool = False,
+                 graph_comm: bool = False):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -127,6 +128,15 @@ class TrainStep:
         else:
             self.buckets = [(len(plan.bwd_calls), 0, plan.grads.numel())]
             self.comm = None
+        # graph_comm: the bucket all-reduces (RCCL) and the buffer broadcast captured into ONE graph
+        # with the backward segments and the optimizer — each all-reduce on a communication stream
+        # forked after its segment and joined before Adam — so a step is one replay, with no host
+        # round trip per bucket.  Needs the "nccl" (RCCL) backend; checked bit for bit against the
+        # host-issued path at world size 1 (tests/test_gpu_zz_rccl.py).  Opt-in: multi-rank capture
+        # has not run on a multi-GPU node yet.
+        self.graph_comm = (graph_comm and graph and self.comm is not None
+                           and dist.get_backend(process_group) == "nccl")
+        self.comm_stream = torch.cuda.Stream(device=net.device) if self.graph_comm else None
         self.graphs = []
         self.g_opt: Optional[torch.cuda.CUDAGraph] = None
         self.stream = torch.cuda.Stream(device=net.device)
@@ -182,6 +192,24 @@ class TrainStep:
         self.opt.v.copy_(state[3]); self.opt.step.copy_(state[4]); self.plan.num_iter.copy_(state[5])
         self.net.sync_lowp()
         self.graphs = []
+        if self.graph_comm:
+            g = torch.cuda.CUDAGraph()
+            cs = self.comm_stream
+            with torch.cuda.graph(g, stream=s):
+                for k in range(len(self.buckets)):
+                    self._segment(k)
+                    _, b0, b1 = self.buckets[k]
+                    cs.wait_stream(s)                   # this segment's gradients are complete
+                    with torch.cuda.stream(cs):
+                        dist.all_reduce(self.plan.zero[b0:b1], op=dist.ReduceOp.AVG, group=self.pg)
+                with torch.cuda.stream(cs):
+                    broadcast_buffers(self.net.running, self.pg)
+                s.wait_stream(cs)
+                self._opt()
+            self.graphs.append(g)
+            self.g_opt = None
+            torch.cuda.synchronize()
+            return
         if self.comm is None:
             # one rank: the whole step (forward, backward and the optimizer) is one graph, one
             # launch from the host — two graphs per step left an ~8.7 us gap between them
@@ -213,6 +241,12 @@ class TrainStep:
             self.plan.eps.copy_(eps.reshape(self.plan.eps.shape))
         if self.use_graph and not self.graphs:
             self._capture()
+        if self.graph_comm:
+            self.graphs[0].replay()                     # segments, all-reduces, broadcast, Adam
+            if self._begin_swaps:
+                self.net.swaps_stale = True
+            self.net.num_batches_tracked += 1
+            return
         for k in range(len(self.buckets)):
             if self.use_graph:
                 self.graphs[k].replay()

@@ -12,7 +12,9 @@ The fp32 plans run every cross-workgroup reduction in a fixed order (StepPlan(de
 vaehip.h vae_conv_args.deterministic: partial rows in the workspace, summed by an ordered pass), so
 the bucketed plan's different batching of the weight gradients and segment graphs cannot move a bit;
 an all-reduce of one rank (AVG over one contribution) is exact.  A broken exchange (a bucket missed,
-summed twice or raced by the next segment) changes the result."""
+summed twice or raced by the next segment) changes the result.  A third run captures the same
+bucketed step with its all-reduces and buffer broadcast as ONE graph (TrainStep(graph_comm=True):
+RCCL collectives on a forked communication stream inside the capture) and must match bit for bit."""
 import os
 import socket
 
@@ -34,14 +36,16 @@ def _port():
     return p
 
 
-def _run(force, x, eps):
+def _run(force, x, eps, graph_comm=False):
     from oracle import vae_oracle as O
     from vae_amd.engine import FusedAdam, TrainStep
     from vae_amd.net import StepPlan, VAENet
     net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda:0")
     net.load_reference_state_dict(O.make_params(O.vanilla_param_spec(), SEED))
     plan = StepPlan(net, B, kld_weight=M_N)
-    step = TrainStep(net, plan, FusedAdam(net, lr=LR), graph=True, nbuckets=4, force_buckets=force)
+    step = TrainStep(net, plan, FusedAdam(net, lr=LR), graph=True, nbuckets=4, force_buckets=force,
+                     graph_comm=graph_comm)
+    assert step.graph_comm == graph_comm
     if force:
         assert step.comm is not None and len(step.buckets) >= 2, step.buckets
     else:
@@ -73,12 +77,13 @@ def _worker(port, q):
         x, eps = x.cuda(), eps.cuda()
         ga, sa, ta, nb = _run(True, x, eps)
         gb, sb, tb, _ = _run(False, x, eps)
+        gc, sc, tc, _ = _run(True, x, eps, graph_comm=True)
         dist.barrier()
         dist.destroy_process_group()
-        q.put((ga, sa, ta, gb, sb, tb, nb))
+        q.put((ga, sa, ta, gb, sb, tb, nb, gc, sc, tc))
     except Exception:
         import traceback
-        q.put((traceback.format_exc(),) + (None,) * 6)
+        q.put((traceback.format_exc(),) + (None,) * 9)
 
 
 def test_rccl_bucketed_step_matches_one_graph_step():
@@ -86,7 +91,7 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_port(), q))
     p.start()
-    ga, sa, ta, gb, sb, tb, nb = q.get(timeout=240)
+    ga, sa, ta, gb, sb, tb, nb, gc, sc, tc = q.get(timeout=240)
     p.join(timeout=60)
     assert not isinstance(ga, str), ga
     assert nb >= 2
@@ -96,3 +101,9 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     for k in sb:                          # parameters after each step, BatchNorm buffers
         assert np.array_equal(sa[k], sb[k]), (k, float(np.abs(sa[k].astype(np.float64) - sb[k]).max()))
     assert np.array_equal(np.array(ta), np.array(tb)), (ta, tb)     # both steps' loss terms
+    # the same bucketed step as ONE graph with the RCCL all-reduces captured (TrainStep(graph_comm=True))
+    for k in gb:
+        assert np.array_equal(gc[k], gb[k]), ("graph_comm", k)
+    for k in sb:
+        assert np.array_equal(sc[k], sb[k]), ("graph_comm", k)
+    assert np.array_equal(np.array(tc), np.array(tb)), (tc, tb)
