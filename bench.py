@@ -65,6 +65,8 @@ def parse():
                          "ae_vvbig: the Autoencoder of configs/big_ae.yaml / patient_vbig_ae.yaml / "
                          "patient_vvbig_ae.yaml (MSE, no KL)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--force-buckets", action="store_true",
+                    help="run the bucketed all-reduce path even at one rank (under torch.distributed.run)")
     ap.add_argument("--graph-comm", action="store_true",
                     help="N > 1: capture the bucket all-reduces (RCCL) into the step's one graph "
                          "(engine.TrainStep(graph_comm=True)) instead of issuing them from the host")
@@ -521,7 +523,8 @@ def main():
     args = parse()
     if "RANK" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))          # parent: never touches the GPU
-    distributed = "RANK" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+    # (--force-buckets under torch.distributed.run with one rank: the RCCL path at world size 1)
+    distributed = "RANK" in os.environ and (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.force_buckets)
     if args.selftest:
         return selftest(args, distributed)
     ndev = max(1, torch.cuda.device_count())
@@ -579,7 +582,7 @@ def main():
     # vanilla_vae.py:116) where the fused bottleneck does it; otherwise a resident N(0,1) draw
     ae = args.arch in AE_WIDTHS
     step = TrainStep(net, plan, opt, graph=not args.no_graph, device_eps=None if ae or args.arch == "vq" else 1265 + rank,
-                     graph_comm=args.graph_comm)
+                     graph_comm=args.graph_comm, force_buckets=args.force_buckets)
     if hasattr(plan, "eps") and not ae and not step.device_eps:
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
 
