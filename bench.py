@@ -65,11 +65,12 @@ def parse():
                          "ae_vvbig: the Autoencoder of configs/big_ae.yaml / patient_vbig_ae.yaml / "
                          "patient_vvbig_ae.yaml (MSE, no KL)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--buckets", type=int, default=1, help="N > 1: gradient buckets (all-reduces) per step")
     ap.add_argument("--force-buckets", action="store_true",
                     help="run the bucketed all-reduce path even at one rank (under torch.distributed.run)")
-    ap.add_argument("--graph-comm", action="store_true",
-                    help="N > 1: capture the bucket all-reduces (RCCL) into the step's one graph "
-                         "(engine.TrainStep(graph_comm=True)) instead of issuing them from the host")
+    ap.add_argument("--host-comm", action="store_true",
+                    help="N > 1: issue the bucket all-reduces from the host between segment graphs instead "
+                         "of capturing them (RCCL) into the step's one graph (engine.TrainStep(graph_comm))")
     ap.add_argument("--concurrent", choices=["auto", "on", "off"], default="auto",
                     help="weight gradients on a side stream beside the data-gradient chain; auto = off: the "
                          "VanillaVAE family measured 0.88 vs 0.77 ms (r1: the graph's per-call fork/join edges cost "
@@ -582,7 +583,7 @@ def main():
     # vanilla_vae.py:116) where the fused bottleneck does it; otherwise a resident N(0,1) draw
     ae = args.arch in AE_WIDTHS
     step = TrainStep(net, plan, opt, graph=not args.no_graph, device_eps=None if ae or args.arch == "vq" else 1265 + rank,
-                     graph_comm=args.graph_comm, force_buckets=args.force_buckets)
+                     graph_comm=not args.host_comm, force_buckets=args.force_buckets, nbuckets=args.buckets)
     if hasattr(plan, "eps") and not ae and not step.device_eps:
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
 

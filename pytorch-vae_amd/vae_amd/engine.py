@@ -98,8 +98,8 @@ class TrainStep:
     queued, so it runs on the communication stream while the rest of the backward computes."""
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
-                 nbuckets: int = 4, device_eps: Optional[int] = None, force_buckets: bool = False,
-                 graph_comm: bool = False):
+                 nbuckets: int = 1, device_eps: Optional[int] = None, force_buckets: bool = False,
+                 graph_comm: bool = True):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -131,9 +131,13 @@ class TrainStep:
         # graph_comm: the bucket all-reduces (RCCL) and the buffer broadcast captured into ONE graph
         # with the backward segments and the optimizer — each all-reduce on a communication stream
         # forked after its segment and joined before Adam — so a step is one replay, with no host
-        # round trip per bucket.  Needs the "nccl" (RCCL) backend; checked bit for bit against the
-        # host-issued path at world size 1 (tests/test_gpu_zz_rccl.py).  Opt-in: multi-rank capture
-        # has not run on a multi-GPU node yet.
+        # round trip per bucket.  Needs the "nccl" (RCCL) backend (gloo: host-issued); checked bit for
+        # bit against the host-issued path at world size 1 (tests/test_gpu_zz_rccl.py).
+        # nbuckets = 1 by default: at one rank (bench.py --force-buckets) the step took 0.483 ms with
+        # one in-graph bucket, 0.542 with two, 0.585 with four (0.553 / 0.584 / 0.644 host-issued;
+        # 0.461 without the exchange) — each extra bucket splits the backward into another segment
+        # and another grouped weight-gradient launch, which costs more than the ~100 us of a
+        # 15.75 MB all-reduce it could hide (profiles/r5_notes.md).
         self.graph_comm = (graph_comm and graph and self.comm is not None
                            and dist.get_backend(process_group) == "nccl")
         self.comm_stream = torch.cuda.Stream(device=net.device) if self.graph_comm else None
@@ -193,8 +197,11 @@ class TrainStep:
         self.net.sync_lowp()
         self.graphs = []
         if self.graph_comm:
-            g = torch.cuda.CUDAGraph()
             cs = self.comm_stream
+            with torch.cuda.stream(cs):         # communicators up before the capture records them
+                dist.all_reduce(torch.zeros(1, device=self.net.device), group=self.pg)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 for k in range(len(self.buckets)):
                     self._segment(k)

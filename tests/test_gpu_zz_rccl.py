@@ -36,18 +36,18 @@ def _port():
     return p
 
 
-def _run(force, x, eps, graph_comm=False):
+def _run(force, x, eps, graph_comm=False, nbuckets=4):
     from oracle import vae_oracle as O
     from vae_amd.engine import FusedAdam, TrainStep
     from vae_amd.net import StepPlan, VAENet
     net = VAENet(latent_dim=128, dtype=torch.float32, device="cuda:0")
     net.load_reference_state_dict(O.make_params(O.vanilla_param_spec(), SEED))
     plan = StepPlan(net, B, kld_weight=M_N)
-    step = TrainStep(net, plan, FusedAdam(net, lr=LR), graph=True, nbuckets=4, force_buckets=force,
+    step = TrainStep(net, plan, FusedAdam(net, lr=LR), graph=True, nbuckets=nbuckets, force_buckets=force,
                      graph_comm=graph_comm)
     assert step.graph_comm == graph_comm
     if force:
-        assert step.comm is not None and len(step.buckets) >= 2, step.buckets
+        assert step.comm is not None and len(step.buckets) >= min(2, nbuckets), step.buckets
     else:
         assert step.comm is None
     step(x, eps)
@@ -78,12 +78,13 @@ def _worker(port, q):
         ga, sa, ta, nb = _run(True, x, eps)
         gb, sb, tb, _ = _run(False, x, eps)
         gc, sc, tc, _ = _run(True, x, eps, graph_comm=True)
+        gd, sd, td, _ = _run(True, x, eps, graph_comm=True, nbuckets=1)   # the N > 1 default
         dist.barrier()
         dist.destroy_process_group()
-        q.put((ga, sa, ta, gb, sb, tb, nb, gc, sc, tc))
+        q.put((ga, sa, ta, gb, sb, tb, nb, gc, sc, tc, gd, sd, td))
     except Exception:
         import traceback
-        q.put((traceback.format_exc(),) + (None,) * 9)
+        q.put((traceback.format_exc(),) + (None,) * 12)
 
 
 def test_rccl_bucketed_step_matches_one_graph_step():
@@ -91,7 +92,7 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_port(), q))
     p.start()
-    ga, sa, ta, gb, sb, tb, nb, gc, sc, tc = q.get(timeout=240)
+    ga, sa, ta, gb, sb, tb, nb, gc, sc, tc, gd, sd, td = q.get(timeout=240)
     p.join(timeout=60)
     assert not isinstance(ga, str), ga
     assert nb >= 2
@@ -107,3 +108,9 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     for k in sb:
         assert np.array_equal(sc[k], sb[k]), ("graph_comm", k)
     assert np.array_equal(np.array(tc), np.array(tb)), (tc, tb)
+    # and with one bucket (TrainStep's default at N > 1): one segment, one all-reduce, in-graph
+    for k in gb:
+        assert np.array_equal(gd[k], gb[k]), ("1 bucket", k)
+    for k in sb:
+        assert np.array_equal(sd[k], sb[k]), ("1 bucket", k)
+    assert np.array_equal(np.array(td), np.array(tb)), (td, tb)
