@@ -288,6 +288,7 @@ def _matching_profile(pattern, arch, kernels, digest, batch=None):
     kernels of another batch size move other bytes) that holds EVERY kernel of the call; else None
     with the reason."""
     why = "no profiles/%s summary" % pattern
+    why_wl = None                                   # (a summary of this build, another workload)
     want = (arch, batch if batch is not None else 64)
     for path in _profiles(pattern, arch):
         try:
@@ -298,14 +299,14 @@ def _matching_profile(pattern, arch, kernels, digest, batch=None):
             why = f"no {pattern} summary of this build (digest {digest})"
             continue
         if _profile_workload(d) != want:
-            why = f"no {pattern} summary of this build for {want[0]} batch {want[1]}"
+            why_wl = f"no {pattern} summary of this build for {want[0]} batch {want[1]}"
             continue
         rows = {k: _row_of(k_, d.get("kernels", {})) for k_ in kernels for k in [k_[1]]}
         if any(v is None for v in rows.values()):
             why = f"{os.path.relpath(path, REPO)} lacks " + ", ".join(k for k, v in rows.items() if v is None)
             continue
         return path, d, rows
-    return None, None, why
+    return None, None, why_wl or why
 
 
 def pmc_traffic(kernels, digest, arch="vanilla", batch=None):
