@@ -46,6 +46,9 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "train images/sec (node) VanillaVAE 64×64 bs=64 at 1/2/4/8 GPU; ELBO match"
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # dense, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
+# a profile summary pairs with a call only when its kernels' rocprof time (average per launch x
+# launches in the call) is within this fraction of the call's event-timed duration
+PAIR_TOL = 0.15
 # the fork's Autoencoder configs (models/autoencoder.py; hidden_dims of configs/*ae*.yaml)
 AE_WIDTHS = {"ae_big": [128, 256, 512, 1024, 2048], "ae_vbig": [256, 512, 1024, 2048, 4096],
              "ae_vvbig": [512, 1024, 2048, 4096, 4096]}
@@ -226,9 +229,11 @@ def time_kernels(plan, reps=20):
 
 
 def call_kernels(fn, ref):
-    """The device kernels one call of the step launches, as (mangled, demangled) names: the call
+    """The device kernels one call of the step launches, as (mangled, demangled, launches): the call
     is run once more with the library's launch log on (vaehip.h vae_launch_log) — what rocprofv3
-    and the PMC summaries key their rows by.  (Runs after the timed region, like time_kernels.)"""
+    and the PMC summaries key their rows by; `launches` is how many times the call launches that
+    kernel (a grouped call may run one kernel several times).  (Runs after the timed region, like
+    time_kernels.)"""
     import ctypes
     from vae_amd import _lib as L
     from vae_amd.net import call_one
@@ -243,14 +248,15 @@ def call_kernels(fn, ref):
     lib.vae_launch_log_names(buf, need)
     out = []
     for line in buf.value.decode(errors="replace").splitlines():
-        m, _, d = line.partition("\t")
-        out.append((m, d or m))
+        f = line.split("\t")
+        m, d = f[0], (f[1] if len(f) > 1 and f[1] else f[0])
+        out.append((m, d, int(f[2]) if len(f) > 2 else 1))     # (mangled, demangled, launches)
     return out
 
 
 def _row_of(kernel, names):
     """The row of `names` (profile keys) that is this kernel (mangled or demangled form), or None."""
-    m, d = kernel
+    m, d = kernel[0], kernel[1]
     for k in names:
         if k in (m, d):
             return k
@@ -316,21 +322,24 @@ def pmc_traffic(kernels, digest, arch="vanilla", batch=None):
     path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest, batch)
     if path is None:
         return None, rows
+    n_of = {k[1]: (k[2] if len(k) > 2 else 1) for k in kernels}
     per = {k: d["kernels"][r].get("hbm_bytes_per_launch") for k, r in rows.items()}
     if any(v is None for v in per.values()):
         return None, f"{os.path.relpath(path, REPO)}: no FETCH_SIZE/WRITE_SIZE for every kernel"
+    # bytes of the CALL: each kernel's per-launch bytes times its launches in the call
+    per = {k: v * n_of.get(k, 1) for k, v in per.items()}
     # the same summary's SQ / TCC counters of each kernel (tools/pmc_summary.py): MFMA busy
     # (SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x CUs), wave-cycle fraction parked in waits
     # (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and the L2 hit rate (TCC_HIT / (TCC_HIT + TCC_MISS))
     counters = {k: {c: d["kernels"][r].get(c) for c in ("mfma_busy", "wait_frac", "l2_hit")} for k, r in rows.items()}
-    return {"bytes": sum(per.values()), "bytes_per_kernel": per, "counters": counters,
+    return {"bytes": sum(per.values()), "bytes_per_kernel": per, "launches": n_of, "counters": counters,
             "file": os.path.relpath(path, REPO), "digest": d.get("digest"), "head": d.get("head")}, None
 
 
 def step_traffic(calls, digest, arch="vanilla", batch=None):
     """HBM bytes of one whole step from the PMC summary of this build: per call, the per-launch
-    bytes of its kernels (a kernel shared by several calls contributes its average once per call,
-    so the sum over the step's calls is the step total).  (None, reason) when any kernel is missing."""
+    bytes of its kernels times their launches in the call (a kernel shared by several calls
+    contributes its average once per launch, so the sum over the step's calls is the step total).  (None, reason) when any kernel is missing."""
     kernels = [k for ks in calls for k in ks]
     path, d, rows = _matching_profile("*pmc*.json", arch, kernels, digest, batch)
     if path is None:
@@ -341,7 +350,7 @@ def step_traffic(calls, digest, arch="vanilla", batch=None):
             v = d["kernels"][_row_of(k, d["kernels"])].get("hbm_bytes_per_launch")
             if v is None:
                 return None, f"{os.path.relpath(path, REPO)}: no FETCH_SIZE/WRITE_SIZE for {k[1]}"
-            total += v
+            total += v * (k[2] if len(k) > 2 else 1)
     return {"bytes": int(total), "file": os.path.relpath(path, REPO)}, None
 
 
@@ -351,20 +360,51 @@ def rocprof_times(kernels, digest, arch="vanilla", batch=None):
     path, d, rows = _matching_profile("*kstats*.json", arch, kernels, digest, batch)
     if path is None:
         return None, rows
+    n_of = {k[1]: (k[2] if len(k) > 2 else 1) for k in kernels}
     per = {k: d["kernels"][r]["avg_us"] for k, r in rows.items()}
-    return {"avg_us": per, "sum_avg_us": round(sum(per.values()), 2), "file": os.path.relpath(path, REPO),
-            "head": d.get("head")}, None
+    # time of the CALL: each kernel's average launch times its launches in the call
+    return {"avg_us": per, "launches": n_of, "sum_avg_us": round(sum(v * n_of.get(k, 1) for k, v in per.items()), 2),
+            "file": os.path.relpath(path, REPO), "head": d.get("head")}, None
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+def host_cpus():
+    """CPUs this process may actually use: os.cpu_count() (the whole machine), the affinity mask,
+    and the cgroup CPU quota (cgroup v2 cpu.max, v1 cfs_quota/period) — on the GPU box the job's
+    share is a quota far below the machine's count."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        info["cgroup_quota_cpus"] = round(quota, 2)
+    usable = min(v for v in (info.get("affinity"), quota, os.cpu_count()) if v)
+    info["usable"] = max(1, int(usable))
+    return info
+
+
 def cpu_baseline(batch, seconds, arch="vanilla", threads=None):
     """The oracle's fp32 step (fwd + loss + bwd + Adam) on the host cores, bounded sample.
-    threads: torch intra-op threads (default: torch's own, i.e. OMP_NUM_THREADS — the box's CPU
-    share for one GPU, 16; os.cpu_count() reports the whole machine there)."""
+    threads: torch intra-op threads; default: every CPU this process may use (host_cpus: the
+    smallest of os.cpu_count(), the affinity mask and the cgroup quota — the GPU box shows the
+    whole machine's 256 CPUs to os.cpu_count() but holds a job to its share)."""
     from oracle import vae_oracle as O
     prev = torch.get_num_threads()
-    if threads:
-        torch.set_num_threads(threads)
+    cpus = host_cpus()
+    torch.set_num_threads(threads or cpus["usable"])
     threads = torch.get_num_threads()
     vq = arch == "vq"
     ae = AE_WIDTHS.get(arch)
@@ -410,9 +450,11 @@ def cpu_baseline(batch, seconds, arch="vanilla", threads=None):
             break
     name = "VQVAE" if vq else (f"Autoencoder {ae}" if ae else "VanillaVAE")
     torch.set_num_threads(prev)
+    lim = ", ".join(f"{k} {v}" for k, v in cpus.items() if k != "usable")
     return {"value": round(n * batch / el, 2), "unit": "images/s", "cores": threads, "kind": "port",
+            "host_cpus": cpus,
             "sample": f"oracle {name} fp32 train step (fwd+loss+bwd+Adam), B={batch}, {n} steps / {el:.1f}s "
-                      f"on {threads} threads ({os.cpu_count()} visible CPUs)"}
+                      f"on {threads} threads (usable CPUs {cpus['usable']}: {lim})"}
 
 
 # ----------------------------------------------------------------------------- main
@@ -630,6 +672,14 @@ def main():
     roof["kernel"] = f"{fn} (call #{idx} of the step; its kernels: {', '.join(k[1] for k in kernels) or 'n/a'})"
     roof["us_per_launch"] = round(us, 2)
     rp, why_rp = rocprof_times(kernels, digest, args.arch, args.batch)
+    if rp and abs(rp["sum_avg_us"] - us) > PAIR_TOL * us:
+        # the profile's kernels do not account for this call's measured time: not the same work
+        # (another plan or launch count), so neither its times nor its counters are evidence here
+        why = (f"{rp['file']}: rocprof sum {rp['sum_avg_us']} us vs {us:.2f} us event time "
+               f"(> {PAIR_TOL:.0%} apart)")
+        rp, why_rp = None, why
+        roof["traffic"] = roof["traffic_ratio"] = None
+        roof["traffic_source"] = {"missing": why}
     roof["rocprof"] = rp if rp else {"missing": why_rp}
     roof["build_digest"] = digest
     roof["algorithmic"] = {"flops": fl, "bytes": by, "ai_flop_per_byte": round(ai, 1)}

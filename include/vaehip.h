@@ -320,8 +320,9 @@ const char* vae_last_error(void);
  *   written into profiles so a counter summary is only ever matched with the code it measured.
  * vae_launch_log(1) starts recording (per host thread) the device kernels every later entry point
  *   launches, vae_launch_log(0) stops; vae_launch_log_names writes the recorded kernels as lines
- *   "<mangled>\t<demangled>\n" into buf (NUL-terminated, truncated to cap) and returns the bytes
- *   the full text needs. */
+ *   "<mangled>\t<demangled>\t<launches>\n" (first-launch order; <launches>: how many times the
+ *   kernel was launched while recording) into buf (NUL-terminated, truncated to cap) and returns the
+ *   bytes the full text needs. */
 const char* vae_build_digest(void);
 int vae_launch_log(int32_t on);
 int64_t vae_launch_log_names(char* buf, int64_t cap);

@@ -88,17 +88,18 @@ struct LaunchLog {
   int on;
   int n;
   const void* k[64];
+  int count[64];       // launches of each kernel while on (a call may launch one kernel several times)
 };
 inline LaunchLog& launch_log() {
-  static thread_local LaunchLog l = {0, 0, {}};
+  static thread_local LaunchLog l = {0, 0, {}, {}};
   return l;
 }
 inline void log_launch(const void* k) {
   LaunchLog& l = launch_log();
   if (!l.on) return;
   for (int i = 0; i < l.n; ++i)
-    if (l.k[i] == k) return;
-  if (l.n < 64) l.k[l.n++] = k;
+    if (l.k[i] == k) { ++l.count[i]; return; }
+  if (l.n < 64) { l.count[l.n] = 1; l.k[l.n++] = k; }
 }
 }  // namespace vae
 #define VAE_LAUNCH(K, ...)                                      \

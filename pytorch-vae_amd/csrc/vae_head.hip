@@ -814,6 +814,15 @@ int head_bwd_go(const vae_head_args* a, HeadQ q, int gsl_max, hipStream_t st) {
     el = *a->elbo;
     if ((el.kind != VAE_LOSS_VANILLA && el.kind != VAE_LOSS_BETA_H) || (el.samples > 1) || !slab || !q.filter)
       return fail(VAE_E_UNSUPPORTED, "head_bwd: fused ELBO needs the vanilla / BetaVAE-H loss, samples 1 and a workspace");
+    // vae_elbo_fwd's checks (elbo_block keeps per-row KL terms in a 1024-entry LDS array), and the
+    // loss must describe the batch this call's seed scales
+    if (!el.sse || !el.out || !el.per_img || !el.mulv)
+      return fail(VAE_E_BADARG, "head_bwd: fused ELBO args");
+    if (el.batch <= 0 || el.batch > 1024 || el.latent <= 0 || el.img_elems <= 0)
+      return fail(VAE_E_BADSHAPE, "head_bwd: fused ELBO sizes (batch %d, latent %d)", el.batch, el.latent);
+    if (el.batch != q.n || el.img_elems != 3 * q.h * a->w)
+      return fail(VAE_E_BADSHAPE, "head_bwd: fused ELBO batch %d / image %d vs the head's %d x %d", el.batch,
+                  el.img_elems, q.n, 3 * q.h * a->w);
     q.coef = nullptr;
     q.hc = 2.f / ((float)el.batch * (float)el.img_elems);
   }

@@ -671,7 +671,7 @@ extern "C" int64_t vae_launch_log_names(char* buf, int64_t cap) {
     int st = 0;
     char* d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
     const int w = snprintf(buf && need < cap ? buf + need : nullptr, buf && need < cap ? (size_t)(cap - need) : 0,
-                           "%s\t%s\n", m, (st == 0 && d) ? d : m);
+                           "%s\t%s\t%d\n", m, (st == 0 && d) ? d : m, l.count[i]);
     free(d);
     need += w > 0 ? w : 0;
   }

@@ -119,8 +119,11 @@ class _MeanWork:
         return True
 
     def is_completed(self):
-        """True only once wait() has applied the 1/world scale: before that the tensor holds the
-        rank SUM, not the mean (a poller must call wait() before reading it)."""
+        """torch Work semantics: True once the all-reduce has finished (a poller never needs wait()).
+        The 1/world scale is applied here on the first True, so whenever this returns True the
+        tensor holds the rank mean, as with RCCL's AVG handle."""
+        if not self.scaled and self.work.is_completed():
+            self.wait()
         return self.scaled
 
 

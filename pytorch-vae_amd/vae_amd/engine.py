@@ -10,7 +10,6 @@ buffer with RCCL between the backward graph and the optimizer graph.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 import torch
@@ -99,7 +98,7 @@ class TrainStep:
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
                  nbuckets: int = 1, device_eps: Optional[int] = None, force_buckets: bool = False,
-                 graph_comm: bool = True):
+                 graph_comm: bool = True, begin_ex: bool = True):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -145,8 +144,8 @@ class TrainStep:
         self.g_opt: Optional[torch.cuda.CUDAGraph] = None
         self.stream = torch.cuda.Stream(device=net.device)
         # the step's head (zeroing, step count, image and weight padding) as one launch;
-        # VAE_NO_BEGIN_EX=1 keeps vae_step_begin + the padding calls (A/B timing)
-        self._begin = None if os.environ.get("VAE_NO_BEGIN_EX") else begin_args(plan, opt.step)
+        # begin_ex=False keeps vae_step_begin + the padding calls (tests/test_gpu_routes.py)
+        self._begin = begin_args(plan, opt.step) if begin_ex else None
         self._begin_swaps = self._begin is not None and self._begin[0].nswap > 0
 
     # -------------------------------------------------------------- eager pieces

@@ -227,14 +227,17 @@ class _HipVAE(BaseVAE):
         return dict(loss="iwae" if self.samples > 1 else "vanilla", samples=self.samples)
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
-                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None,
+                         plan_options: Optional[dict] = None):
         """The whole training step of this model — forward, loss_function (vae_elbo_fwd), backward,
         [gradient all-reduce], Adam — as one engine.TrainStep on the model's own parameters,
         replayed from HIP graphs: the graph path of VAEXperiment.training_step + backward +
         optimizer.step (experiment.fit(..., engine="graph")).  `opt`: an engine.FusedAdam to share
-        (one Adam state for the steps of every batch size, as the reference's single optimizer)."""
+        (one Adam state for the steps of every batch size, as the reference's single optimizer).
+        `plan_options`: StepPlan route options (latent_kernels, head_kernels, pad_rgb, materialise,
+        mat_min_flops, batch_wgrads, wg_overlap)."""
         from .engine import FusedAdam, TrainStep
-        plan = StepPlan(self.net, batch, kld_weight=kld_weight, **self._loss_config())
+        plan = StepPlan(self.net, batch, kld_weight=kld_weight, **self._loss_config(), **(plan_options or {}))
         if opt is None:
             opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
         return TrainStep(self.net, plan, opt, graph=graph, process_group=process_group)
@@ -604,11 +607,13 @@ class Autoencoder(_HipVAE):
         return dict(loss="vanilla", samples=1, recon_loss=self._recon_loss_cfg(self.net.device))
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
-                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None,
+                         plan_options: Optional[dict] = None):
         """The whole Autoencoder step in one graph, whichever reconstruction loss the model has: the
         plain MSE on the ELBO kernel (M_N = 0), or the centre-weighted MSE / MS-SSIM on vae_recon_loss
         (loss terms, per-image MSE and the dL/drecon seed of the fused backward)."""
-        step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group, opt)
+        step = super().fused_train_step(batch, 0.0, lr, weight_decay, betas, graph, process_group, opt,
+                                        plan_options=plan_options)
         step.plan.eps.zero_()
         step.zero_eps = True
         return step
@@ -764,11 +769,12 @@ class VQVAE(BaseVAE):
         return [recon, input, vq_loss]
 
     def fused_train_step(self, batch: int, kld_weight: float, lr: float, weight_decay: float = 0.0,
-                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None):
+                         betas=(0.9, 0.999), graph: bool = True, process_group=None, opt=None,
+                         plan_options: Optional[dict] = None):
         """See _HipVAE.fused_train_step (the VQ-VAE loss ignores kld_weight, vq_vae.py:194-211)."""
         from .engine import FusedAdam, TrainStep
         from .vq import VQStepPlan
-        plan = VQStepPlan(self.net, batch, beta=self.beta)
+        plan = VQStepPlan(self.net, batch, beta=self.beta, **(plan_options or {}))
         if opt is None:
             opt = FusedAdam(self.net, lr=lr, betas=betas, weight_decay=weight_decay)
         return TrainStep(self.net, plan, opt, graph=graph, process_group=process_group)

@@ -16,7 +16,6 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -25,9 +24,9 @@ from . import _lib as L
 from .layout import Layout, default_init, reference_key_order, vanilla_layout
 
 SLOPE = 0.01         # nn.LeakyReLU default
-# layers at least this large take materialised operands (StepPlan.big_layer); VAE_MAT_MIN
-# overrides it (A/B sweeps only)
-MAT_MIN_FLOPS = float(os.environ.get("VAE_MAT_MIN", "4e9"))
+# layers at least this large take materialised operands by default (StepPlan.big_layer,
+# StepPlan(mat_min_flops=...))
+MAT_MIN_FLOPS = 4e9
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 
@@ -136,8 +135,17 @@ class StepPlan:
                  capacity_max_iter: float = 1e5, fused_loss: bool = True, training: bool = True,
                  concurrent: bool = False, fuse_bn: bool = False, bn_in_consumer: bool = True,
                  wg_overlap: bool = False, recon_loss: Optional[dict] = None,
-                 deterministic: Optional[bool] = None):
+                 deterministic: Optional[bool] = None, latent_kernels: bool = True, head_kernels: bool = True,
+                 pad_rgb: bool = True, materialise: bool = True, mat_min_flops: float = MAT_MIN_FLOPS,
+                 batch_wgrads: bool = True):
+        # Route options (explicit arguments; every non-default route has a GPU test,
+        # tests/test_gpu_routes.py): latent_kernels / head_kernels / pad_rgb / materialise /
+        # batch_wgrads = False keep the generic per-op calls in place of the dedicated bottleneck
+        # kernels, the 64/128-channel head kernels, the 8-channel padded RGB ends, materialised
+        # BatchNorm operands for layers >= mat_min_flops, and the batched weight gradients.
         self.net = net
+        self.materialise, self.mat_min_flops = bool(materialise), float(mat_min_flops)
+        self.batch_wgrads_on = bool(batch_wgrads)
         # deterministic: every cross-workgroup reduction of the step in a fixed order (vaehip.h
         # vae_conv_args.deterministic), so two runs of the same step give bit-identical gradients;
         # the default for fp32 (parity) plans, unsupported by the bf16 kernels.
@@ -174,11 +182,11 @@ class StepPlan:
         # latent: the bottleneck (fc_mu|fc_var, reparameterize, decoder_input and their backward) on
         # the vae_latent_* kernels — two launches each way instead of nine (vaehip.h).  bf16 training
         # plans with the fused loss (the TrainStep engine) and the shapes those kernels take;
-        # VAE_NO_LATENT=1 keeps the per-op calls (A/B timing).
+        # latent_kernels=False keeps the per-op calls.
         C5, r0 = net.hidden_dims[-1], net.hidden_dims[::-1][0]
         self.latent_fused = (T == torch.bfloat16 and training and fused_loss and net.latent_dim in (64, 128)
                              and C5 % 128 == 0 and (4 * r0) % 128 == 0 and net.img_size == 64
-                             and not os.environ.get("VAE_NO_LATENT"))
+                             and latent_kernels)
         self._keep = []            # ctypes structs referenced by the call lists
         # wide_head: a final layer wider than the head kernels take on MFMA (bf16, 64-wide images:
         # 32, 64 or 128 channels — configs/big_ae.yaml's 128 included) runs the head Conv2d(C->3)
@@ -186,9 +194,8 @@ class StepPlan:
         # reconstruction, SSE, backward seed) — the VQ-VAE output layer's route (the Autoencoder's
         # 256-512-channel final layers, and the fp32 parity mode above 32).  The reconstruction seed
         # is the mean-MSE one, so not for IWAE's per-sample weights (S > 1 keeps the head kernels).
-        # VAE_WIDE_HEAD=1 keeps the conv-GEMM route for 64/128 channels (A/B timing).
-        head_mfma = (T == torch.bfloat16 and img == 64 and h[0] in (64, 128)
-                     and not os.environ.get("VAE_WIDE_HEAD"))
+        # head_kernels=False keeps the conv-GEMM route for 64/128 channels.
+        head_mfma = T == torch.bfloat16 and img == 64 and h[0] in (64, 128) and head_kernels
         self.wide_head = h[0] > 32 and self.S == 1 and not head_mfma
 
         # -------- buffers
@@ -196,7 +203,7 @@ class StepPlan:
         self.x = torch.zeros(B, 3, img, img, **f32)                     # NCHW input (reference layout)
         # bf16: the image and the first conv's weights carried as 8 zero-padded channels (packed
         # GEMM operands; vae_nchw_to_nhwc_pad / vae_pad_channels at the start of every step)
-        self.pad_rgb = T == torch.bfloat16 and not os.environ.get("VAE_NO_PAD_RGB")
+        self.pad_rgb = T == torch.bfloat16 and pad_rgb
         if self.pad_rgb:
             self.x8 = torch.zeros(B, img, img, 8, dtype=T, device=dev)
             self.w8 = torch.zeros(h[0] * 9 * 8, dtype=T, device=dev)
@@ -275,8 +282,7 @@ class StepPlan:
         # encoder's data-gradient chain (batch_wgrads); one fork and one join per step.  Off by
         # default: measured 0.670 vs 0.648 ms/step (B=64, graph-replayed) — the graph's cross-stream
         # edges cost more than the overlap gains, as the per-call side stream of round 1 did
-        wg_overlap = wg_overlap or bool(os.environ.get("VAE_WG_OVERLAP"))        # (A/B timing)
-        self.wg_overlap = wg_overlap and training and not concurrent and not os.environ.get("VAE_NO_WG_OVERLAP")
+        self.wg_overlap = wg_overlap and training and not concurrent
         self._mat_a: Dict[str, torch.Tensor] = {}         # materialised lrelu(BN(y)) per BatchNorm
         self._mat_dz: Dict[str, torch.Tensor] = {}        # materialised BN-backward gradients
         self.side_all = self.side is not None            # concurrent: every weight-gradient call
@@ -300,7 +306,8 @@ class StepPlan:
         """Rebuild bwd_calls from bwd_calls_raw with the conv / convT weight gradients of each
         backward segment (calls [ends[k-1], ends[k]) of the raw list) moved into one
         vae_conv_bwd_filter_batch call at the segment's end, and size the workspaces.  Returns the
-        segment ends as indices into the new list.  VAE_NO_WG_BATCH=1 keeps one call per layer.
+        segment ends as indices into the new list.  batch_wgrads=False (constructor) keeps one call
+        per layer.
 
         With one segment (one rank) and wg_overlap, the decoder's weight gradients form a batch of
         their own, issued on the side stream where the decoder's data-gradient chain ends: it runs
@@ -316,7 +323,8 @@ class StepPlan:
                 obj = getattr(ref, "_obj", ref)
                 if hasattr(obj, "deterministic"):
                     obj.deterministic = 1
-        self.bwd_calls, new_ends = batch_filter_calls(self.bwd_calls_raw, ends, splits)
+        self.bwd_calls, new_ends = batch_filter_calls(self.bwd_calls_raw, ends, splits,
+                                                      enabled=self.batch_wgrads_on)
         size_workspaces(self, [self.fwd_calls, self.bwd_calls])
         return new_ends
 
@@ -409,9 +417,9 @@ class StepPlan:
         per pass and >= 128 channels on both sides (the Autoencoder's wide layers, whose GEMMs run on
         the 128 x 128 LDS-DMA tiles; the VanillaVAE's are 0.6 GFLOP, and IWAE's 32-channel final ConvT
         reaches 6 GFLOP at B*S = 320 but stays on its own kernels: materialised it measured 1.10 vs
-        1.04 ms/step).  VAE_NO_MAT=1 keeps every transform fused into its consumers (A/B timing)."""
-        return (self.net.dtype == torch.bfloat16 and self.training and flops >= MAT_MIN_FLOPS
-                and min(cin, cout) >= 128 and not os.environ.get("VAE_NO_MAT"))
+        1.04 ms/step).  materialise=False keeps every transform fused into its consumers."""
+        return (self.net.dtype == torch.bfloat16 and self.training and self.materialise
+                and flops >= self.mat_min_flops and min(cin, cout) >= 128)
 
     def mat_act(self, F, prefix: str, t: torch.Tensor, count: int):
         """lrelu(BN(t)) written once (vae_bn_apply: running statistics updated there, the forward's
@@ -612,8 +620,11 @@ class StepPlan:
         # of a vae_elbo_fwd launch between the forward and the backward — the bf16 head kernels,
         # the vanilla / BetaVAE-H losses (their seeds do not depend on the batch), one sample
         self.elbo_in_head = (self.fused_loss and self.training and self.recon_loss is None and not self.wide_head
-                             and self.S == 1 and T == L.BF16
+                             and self.S == 1 and T == L.BF16 and B <= 1024
                              and self.loss_kind in (L.LOSS_VANILLA, L.LOSS_BETA_H))
+        # (with elbo_in_head, out / per_img / head_coef / kl_coef are written by the backward: they
+        # are this step's only after backward() — loss_dict() raises in between)
+        self._loss_pending = False
         if self.recon_loss is not None:
             self._add_recon_loss(F)
         elif self.fused_loss and not self.elbo_in_head:
@@ -874,9 +885,11 @@ class StepPlan:
 
     def forward(self, stream=None):
         self._run(self.fwd_calls, stream if stream is not None else L.stream_ptr())
+        self._loss_pending = self.elbo_in_head
 
     def backward(self, stream=None):
         self._run(self.bwd_calls, stream if stream is not None else L.stream_ptr())
+        self._loss_pending = False
 
     def encode(self, stream=None):
         """encoder + fc_mu|fc_var only (mu | log_var land in self.mulv)."""
@@ -887,6 +900,9 @@ class StepPlan:
         self._run(self.fwd_calls[self.n_decode0:self.n_decode1], stream if stream is not None else L.stream_ptr())
 
     def loss_dict(self) -> Dict[str, float]:
+        if self._loss_pending:
+            raise RuntimeError("loss_dict(): this plan evaluates the ELBO in the head backward "
+                               "(elbo_in_head); run backward() first")
         o = self.out.tolist()
         third = "KLD"
         return {"loss": o[0], "Reconstruction_Loss": o[1], third: o[2]}
@@ -952,15 +968,15 @@ BATCH_FN = "vae_conv_bwd_filter_batch"
 DEFERRED_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_unpad_accumulate"))
 
 
-def batch_filter_calls(calls, ends, splits=()):
+def batch_filter_calls(calls, ends, splits=(), enabled: bool = True):
     """Weight gradients are read only by the optimizer, so within a backward segment they can
     run after the segment's data-gradient chain and together: the conv / convT bwd_filter calls
     of each segment become one vae_conv_bwd_filter_batch call (grouped launches) at its end,
     followed by the calls that must follow them (vae_unpad_accumulate reads the padded first-layer
     weight gradient).  `splits`: raw call indices inside a segment where the weight gradients so
     far are emitted as a batch of their own that runs on the plan's side stream (run_calls).
-    Returns (new call list, new segment ends)."""
-    if os.environ.get("VAE_NO_WG_BATCH"):
+    enabled=False: one call per layer, as built.  Returns (new call list, new segment ends)."""
+    if not enabled:
         return list(calls), list(ends)
     out, new_ends, lo = [], [], 0
 

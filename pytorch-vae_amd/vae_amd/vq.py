@@ -18,7 +18,6 @@ loss are their own small kernels.  All convolutions are MFMA implicit GEMMs (vae
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -136,8 +135,12 @@ class VQStepPlan:
 
     loss_kind = L.LOSS_VQ
 
-    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True, concurrent: bool = False):
+    def __init__(self, net: VQNet, batch: int, *, beta: float = 0.25, fused_loss: bool = True, concurrent: bool = False,
+                 materialise: bool = True, mat_min_flops: float = MAT_MIN_FLOPS):
+        # materialise=False: the large strided layers keep their LeakyReLU fused into the GEMM's
+        # operand load instead of one vae_bn_apply pass (tests/test_gpu_routes.py)
         self.net, self.B, self.beta, self.fused_loss = net, batch, beta, fused_loss
+        self.materialise, self.mat_min_flops = bool(materialise), float(mat_min_flops)
         dev, T = net.device, net.dtype
         h, E, img = net.hidden_dims, net.embedding_dim, net.img_size
         B = batch
@@ -311,7 +314,7 @@ class VQStepPlan:
         return out
 
     def _mat_ok(self, flops: float) -> bool:
-        return self.net.dtype == torch.bfloat16 and flops >= MAT_MIN_FLOPS and not os.environ.get("VAE_NO_MAT")
+        return self.net.dtype == torch.bfloat16 and self.materialise and flops >= self.mat_min_flops
 
     # ------------------------------------------------------------------ plan
     def _build(self):

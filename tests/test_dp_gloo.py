@@ -80,8 +80,15 @@ def _worker(rank, world, port, q):
         assert h is not None
         before = float(t[0])
         assert before in (float(rank + 1), float(sum(range(1, world + 1))))   # not yet scaled
-        assert not h.is_completed()          #  the sum may have landed, the mean has not
-        h.wait()
+        #  torch Work semantics: a poller sees completion without calling wait(), and
+        # whenever is_completed() is True the tensor already holds the mean
+        import time
+        t0 = time.time()
+        while not h.is_completed():
+            assert time.time() - t0 < 60, "is_completed() never turned True without wait()"
+            time.sleep(0.001)
+        assert torch.equal(t, torch.full_like(t, sum(range(1, world + 1)) / world))
+        h.wait()                             # idempotent: no second scale
         assert h.is_completed()
         assert torch.equal(t, torch.full_like(t, sum(range(1, world + 1)) / world))
         broadcast_buffers(run)

@@ -132,3 +132,84 @@ def test_filter_batch_workspace():
     b32 = L.FilterBatch([("vae_convT2d_bwd_filter", ctypes.byref(f32[0])), ("vae_conv2d_bwd_filter", ctypes.byref(f32[1]))])
     r = lambda v: (v + 255) // 256 * 256
     assert b32.workspace_size() == r(n1) + r(n2)
+
+
+def _vq_items():
+    """VQ-VAE B=128 residual-stack weight gradients (models/vq_vae.py:57-70): the 3x3 256 -> 256
+    conv and the 1x1 256 -> 256 conv on the 16x16 latent grid, bf16, no BatchNorm — standalone
+    items of a batch (each keeps its own plan, slab and region)."""
+    c3 = _conv(128, 16, 256, 256, stride=1, r=3, pad=1)
+    c1 = _conv(128, 16, 256, 256, stride=1, r=1, pad=0)
+    for a in (c3, c1):
+        a.dy = a.dw = FAKE
+        a.dy_xf = L.Xform(kind=L.X_NONE, channels=256)
+    return c3, c1
+
+
+def test_filter_batch_nested_queries_leave_no_state():
+    """Round-5 fault (profiles/r5_notes.md): a workspace query nested inside the batch collector
+    recorded the query's fake slab pointer.  The collector queries each standalone item's need with
+    the thread's query state saved around it (vae_wgrad_batch.hip item_need): the batch need is the
+    sum of the items' own needs, every standalone query gives the same answer before and after a
+    batch query, and a real call after the queries is planned for real (a short workspace fails in
+    planning instead of being taken for a query)."""
+    lib = L.load()
+    c3, c1 = _vq_items()
+    r = lambda v: (v + 255) // 256 * 256
+    n3, n1 = _need("vae_conv2d_bwd_filter", c3), _need("vae_conv2d_bwd_filter", c1)
+    assert n3 > 0                                 # the 3x3 weight gradient slices K into slabs
+    items = [("vae_conv2d_bwd_filter", ctypes.byref(c3)), ("vae_conv2d_bwd_filter", ctypes.byref(c1))]
+    b = L.FilterBatch(items)
+    need = b.workspace_size()
+    assert need == r(n3) + r(n1)
+    for _ in range(3):                            # repeated: no state carried from one query to the next
+        assert b.workspace_size() == need
+        assert _need("vae_conv2d_bwd_filter", c3) == n3 and _need("vae_conv2d_bwd_filter", c1) == n1
+    # a grouped VanillaVAE layer beside them: slabs after the standalone regions
+    fin = _conv(64, 32, 32, 32)
+    fin.p = fin.q = 64
+    fin.dy = fin.dw = FAKE
+    fin.x_xf, fin.dy_xf = _bn(L.X_BN_ACT, 32), _bn(L.X_BN_DY, 32)
+    mixed = L.FilterBatch(items + [("vae_convT2d_bwd_filter", ctypes.byref(fin))])
+    nm = mixed.workspace_size()
+    assert nm >= need
+    assert mixed.workspace_size() == nm
+    # the query state is off again: real calls with a short workspace are rejected in planning
+    # (a leaked query flag would return 0 here without looking at the workspace)
+    for bb, nn in ((b, need), (mixed, nm)):
+        rc = lib.vae_conv_bwd_filter_batch(len(bb.kinds), bb.kinds, bb.items, FAKE, nn - 256, None)
+        assert rc == -1 and b"workspace" in lib.vae_last_error()
+    c3.workspace, c3.workspace_bytes = FAKE, n3 - 4
+    assert lib.vae_conv2d_bwd_filter(ctypes.byref(c3), None) == -1
+    assert b"workspace" in lib.vae_last_error()
+
+
+def _head_with_elbo(n, batch, latent=128):
+    a = L.HeadArgs(dtype=L.BF16, n=n, h=64, w=64, c=32, samples=1)
+    a.x = a.wt = a.bias = a.target = a.recon = a.sse = a.dx = a.dw = a.db = FAKE
+    a.dx_dgamma = a.dx_dbeta = FAKE
+    a.x_xf = L.Xform(kind=L.X_BN_ACT, channels=32, count=1.0, slope=0.01)
+    a.dx_epi = L.Xform(kind=L.X_BN_ACT, channels=32, count=1.0, slope=0.01)
+    for f in ("sum", "sumsq", "gamma", "beta", "aux"):
+        setattr(a.x_xf, f, FAKE)
+        setattr(a.dx_epi, f, FAKE)
+    e = L.ElboArgs(kind=L.LOSS_VANILLA, batch=batch, samples=1, latent=latent, img_elems=3 * 64 * 64)
+    e.iter = e.mulv = e.sse = e.out = e.per_img = e.head_coef = e.kl_coef = FAKE
+    a.coef = FAKE                                 # (the query plans the unfused call)
+    need = _need("vae_head_bwd", a)
+    a.coef = None                                 # fused: the seed coefficient comes from the loss
+    a.workspace, a.workspace_bytes = FAKE, need
+    a.elbo = ctypes.addressof(e)
+    return a, e
+
+
+@pytest.mark.parametrize("n,batch,latent", [(2048, 2048, 128), (64, 32, 128), (64, 64, 0), (64, 0, 128)])
+def test_fused_elbo_head_rejects_bad_shapes(n, batch, latent):
+    """the ELBO fused into the head backward (vae_head_args.elbo) keeps per-row KL terms in
+    a 1024-entry LDS array; it takes vae_elbo_fwd's shape checks (batch in 1..1024, latent > 0) and
+    the loss must describe the head's own batch — rejected before anything launches."""
+    lib = L.load()
+    a, e = _head_with_elbo(n, batch, latent)
+    rc = lib.vae_head_bwd(ctypes.byref(a), None)
+    assert rc == -2, (rc, lib.vae_last_error())
+    assert b"fused ELBO" in lib.vae_last_error()
