@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VAE_ABI_VERSION 24
+#define VAE_ABI_VERSION 25
 
 enum vae_dtype { VAE_F32 = 0, VAE_BF16 = 1 };
 
@@ -175,6 +175,12 @@ typedef struct vae_conv_args {
    * bit-identical results (the parity mode of experiment.py:308-311's gradients).  Needs the
    * workspace *_workspace_size reports for it; dtype VAE_F32 only (VAE_E_UNSUPPORTED otherwise). */
   int32_t deterministic;
+  /* bwd_filter (bf16 grouped weight gradients of vae_conv_bwd_filter_batch, and the full-resolution
+   * vae_convT2d_bwd): 1 = leave this weight gradient as fp32 partial rows in the workspace instead
+   * of summing them into dw — no reduction launch; the call records a vae_grad_slab descriptor
+   * (vae_deferred_take) for the caller to reduce later (vae_adam_step_ex), and dw is then written
+   * (not accumulated) by that reduction.  The workspace must stay untouched until then. */
+  int32_t defer_reduce;
 } vae_conv_args;
 
 /* Linear y[m][n] = x[m][:]·W[n][:] + b[n] (fc_mu|fc_var fused as one N=2D layer,
@@ -240,6 +246,9 @@ typedef struct vae_head_args {
    * launch.  NULL: coef as above. */
   const struct vae_elbo_args* elbo;
   int32_t deterministic;    /* as vae_conv_args.deterministic (VALU kernels, fp32) */
+  /* bwd (bf16 MFMA path, 32-channel head): as vae_conv_args.defer_reduce for the filter partials;
+   * with elbo set the loss is deferred too (vae_deferred_take returns its arguments). */
+  int32_t defer_reduce;
 } vae_head_args;
 
 
@@ -393,6 +402,41 @@ int vae_elbo_fwd(const vae_elbo_args* a, void* stream);
 int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v,
                   const int32_t* step, const float* lr, double beta1, double beta2, float eps,
                   float weight_decay, void* p_lowp, void* stream);
+/* --- Deferred weight-gradient reductions + Adam in one launch ---------------------------
+ * A bf16 call with defer_reduce set leaves a weight gradient as fp32 partial rows and records
+ *   dst[j] = sum_{r < rows} slab[r * ld + j]   (j < count, rows summed in ascending order)
+ * in a per-host-thread list instead of launching its reduction (the fused ELBO of vae_head_args
+ * likewise).  vae_deferred_take copies the list out (up to max descriptors; returns how many there
+ * are; *has_elbo / *elbo: the deferred loss, if any) and clears it; vae_deferred_reset clears it.
+ * Workspace queries record nothing.
+ * vae_adam_step_ex: vae_adam_step over the flat buffers, with the slab descriptors reduced in the
+ * same launch (each dst inside g: the reduced gradient is written there, then that element's Adam
+ * update runs), and the deferred loss evaluated by one extra workgroup — the step's three slab
+ * reductions (head, full-resolution ConvT, grouped weight gradients) and the loss without launches
+ * of their own (models/vanilla_vae.py:124-146, experiment.py:308-311). */
+#define VAE_SLAB_MAX 32
+typedef struct vae_grad_slab {
+  float* dst;              /* inside vae_adam_args.g */
+  int64_t count;
+  const float* slab;
+  int32_t rows;
+  int64_t ld;              /* floats between rows */
+} vae_grad_slab;
+int vae_deferred_reset(void);
+int32_t vae_deferred_take(vae_grad_slab* out, int32_t max, vae_elbo_args* elbo, int32_t* has_elbo);
+typedef struct vae_adam_args {
+  int64_t n;
+  float* p; float* g; float* m; float* v;
+  const int32_t* step; const float* lr;
+  double beta1, beta2;
+  float eps, weight_decay;
+  void* p_lowp;
+  int32_t nslab;
+  vae_grad_slab slab[VAE_SLAB_MAX];
+  int32_t has_elbo;
+  vae_elbo_args elbo;
+} vae_adam_args;
+int vae_adam_step_ex(const vae_adam_args* a, void* stream);
 /* --- fp32 -> bf16 copy (weight copies when the optimizer is not vae_adam_step) -------- */
 int vae_cast_bf16(int64_t n, const float* src, void* dst, void* stream);
 /* --- swapped-axes bf16 weight copies (vae_conv_args.wt_t), several tensors per launch:

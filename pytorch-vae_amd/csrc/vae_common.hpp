@@ -58,6 +58,35 @@ inline WsQuery& ws_query() {
   return q;
 }
 inline bool querying() { return ws_query().on != 0; }
+// Deferred weight-gradient reductions (vaehip.h vae_deferred_take): a call with defer_reduce set
+// leaves its fp32 partial rows in its workspace and records them here (host thread; not while
+// querying) for vae_adam_step_ex to reduce.  Returns false (and fails) when the list is full.
+struct Deferred {
+  int n;
+  vae_grad_slab s[VAE_SLAB_MAX];
+  int has_elbo;
+  vae_elbo_args elbo;
+};
+inline Deferred& deferred() {
+  static thread_local Deferred d = {};
+  return d;
+}
+inline bool defer_slab(float* dst, long count, const float* slab, int rows, long ld) {
+  if (querying()) return true;
+  Deferred& d = deferred();
+  if (d.n >= VAE_SLAB_MAX) {
+    fail(VAE_E_UNSUPPORTED, "deferred reductions: more than %d outstanding", VAE_SLAB_MAX);
+    return false;
+  }
+  d.s[d.n++] = vae_grad_slab{dst, count, slab, rows, ld};
+  return true;
+}
+inline void defer_elbo(const vae_elbo_args& e) {
+  if (querying()) return;
+  Deferred& d = deferred();
+  d.has_elbo = 1;
+  d.elbo = e;
+}
 inline bool ws_fits(long need, long have, const char* what) {
   WsQuery& q = ws_query();
   if (q.on) {

@@ -829,6 +829,14 @@ int head_bwd_go(const vae_head_args* a, HeadQ q, int gsl_max, hipStream_t st) {
   VAE_LAUNCH((head_bwd_mfma<HC, ROWS, CT>), dim3(grid), dim3(256), 0, st, q);
   int rc = check_launch("head_bwd_mfma");
   if (rc || !q.filter || !slab) return rc;
+  if (a->defer_reduce && NSL == 1) {
+    // the filter partials (slab rows [grid][27 HC + 3], dW index = column for one channel slice) and
+    // the loss stay for vae_adam_step_ex
+    if (!defer_slab(a->dw, T::NW, ws, gsl, T::SLAB_COLS)) return VAE_E_UNSUPPORTED;
+    if (a->db && !defer_slab(a->db, NCO, ws + T::NW, gsl, T::SLAB_COLS)) return VAE_E_UNSUPPORTED;
+    if (el.kind >= 0) defer_elbo(el);
+    return VAE_OK;
+  }
   vae_elbo_args none;
   memset(&none, 0, sizeof(none));
   none.kind = -1;

@@ -541,6 +541,8 @@ int hires_convT_bwd_launch(const vae_conv_args* a, hipStream_t st) {
   q.db = a->db;
   VAE_LAUNCH(hires_convT_bwd_kernel, dim3((unsigned)grid), dim3(256), 0, st, q);
   if (int rc = check_launch("hires_convT_bwd")) return rc;
+  if (a->defer_reduce)                      // the filter partials stay for vae_adam_step_ex
+    return defer_slab(a->dw, NW, q.slab, grid, NW) ? VAE_OK : VAE_E_UNSUPPORTED;
   VAE_LAUNCH(hires_slab_reduce, dim3((NW + SR_COLS - 1) / SR_COLS), dim3(256), 0, st, (const float*)q.slab, grid, a->dw);
   return check_launch("hires_slab_reduce");
 }

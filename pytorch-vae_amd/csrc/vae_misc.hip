@@ -2,6 +2,7 @@
 // layer that would waste 13/16 of an MFMA tile, so it runs on the VALU with its input tile
 // staged once in LDS), the reparameterization, the ELBO reductions, Adam, and utilities.
 #include <cxxabi.h>
+#include <algorithm>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -849,6 +850,235 @@ extern "C" int vae_adam_step(int64_t n, float* p, const float* g, float* m, floa
     else VAE_LAUNCH((adam_kernel<false, 1>), dim3(grid), dim3(256), 0, st, (long)n, p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, lp);
   }
   return check_launch("adam_step");
+}
+
+// ---------------------------------------------------------------------------- deferred reductions
+extern "C" int vae_deferred_reset(void) {
+  deferred().n = 0;
+  deferred().has_elbo = 0;
+  return VAE_OK;
+}
+
+extern "C" int32_t vae_deferred_take(vae_grad_slab* out, int32_t max, vae_elbo_args* elbo, int32_t* has_elbo) {
+  Deferred& d = deferred();
+  const int n = d.n;
+  for (int i = 0; i < n && i < max && out; ++i) out[i] = d.s[i];
+  if (has_elbo) *has_elbo = d.has_elbo;
+  if (elbo && d.has_elbo) *elbo = d.elbo;
+  d.n = 0;
+  d.has_elbo = 0;
+  return n;
+}
+
+namespace {
+
+// vae_adam_step_ex in one grid:
+//   [0, nreg)                 vae_adam_step over the elements no descriptor covers (grid-stride,
+//                             16-byte accesses; quads inside a descriptor's range are skipped)
+//   [nreg, nreg + nslabblk)   per descriptor: "tall" slabs (rows >= kTallRows: the head's and the
+//                             full-resolution ConvT's per-workgroup partials) as 16 columns x 16 row
+//                             parts per workgroup, parts combined in LDS in ascending order; "short"
+//                             slabs (K slices of the grouped weight gradients) as 256 quads per
+//                             workgroup, each thread summing its quad's rows in ascending order —
+//                             then g = that sum is written and the element's Adam update runs
+//   [last]                    the deferred loss (elbo_block), when present
+constexpr int kTallRows = 64;
+struct AdamEx {
+  long n;
+  float* p; float* g; float* m; float* v;
+  const int* step; const float* lr;
+  double b1, b2;
+  float eps, wd;
+  __bf16* lowp;
+  int nreg, nslab;
+  int tall[VAE_SLAB_MAX];
+  int blk0[VAE_SLAB_MAX + 1];        // first workgroup of each descriptor, relative to nreg
+  long q0[VAE_SLAB_MAX], q1[VAE_SLAB_MAX];   // quads [q0, q1) of g a descriptor covers (ascending q0)
+  long off[VAE_SLAB_MAX];            // element offset of dst in g
+  vae_grad_slab s[VAE_SLAB_MAX];
+  int has_elbo;
+  vae_elbo_args e;
+};
+
+__device__ __forceinline__ AdamK adam_k(const AdamEx& a) {
+  const double t = (double)(*a.step);
+  const double bc1 = 1.0 - pow(a.b1, t), bc2 = 1.0 - pow(a.b2, t);
+  return AdamK{(float)(1.0 - a.b1), (float)(1.0 - a.b2), (float)a.b2, (float)((double)*a.lr / bc1), (float)sqrt(bc2),
+               a.eps, a.wd};
+}
+
+template <bool LOWP>
+__device__ __forceinline__ void adam_one(const AdamEx& a, const AdamK& k, long i, float gi) {
+  float pi = a.p[i], mi = a.m[i], vi = a.v[i];
+  adam_elem(k, pi, gi, mi, vi);
+  a.m[i] = mi; a.v[i] = vi; a.p[i] = pi;
+  if (LOWP) a.lowp[i] = (__bf16)pi;
+}
+
+template <bool LOWP>
+__device__ __forceinline__ void adam_quad(const AdamEx& a, const AdamK& k, long i, const f32x4 g4) {
+  f32x4 p4 = reinterpret_cast<const f32x4*>(a.p)[i];
+  f32x4 m4 = reinterpret_cast<const f32x4*>(a.m)[i];
+  f32x4 v4 = reinterpret_cast<const f32x4*>(a.v)[i];
+  float pe[4], me[4], ve[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    pe[e] = p4[e]; me[e] = m4[e]; ve[e] = v4[e];
+    adam_elem(k, pe[e], g4[e], me[e], ve[e]);
+  }
+  reinterpret_cast<f32x4*>(a.p)[i] = f32x4{pe[0], pe[1], pe[2], pe[3]};
+  reinterpret_cast<f32x4*>(a.m)[i] = f32x4{me[0], me[1], me[2], me[3]};
+  reinterpret_cast<f32x4*>(a.v)[i] = f32x4{ve[0], ve[1], ve[2], ve[3]};
+  if (LOWP) reinterpret_cast<bf16x4*>(a.lowp)[i] = bf16x4{(__bf16)pe[0], (__bf16)pe[1], (__bf16)pe[2], (__bf16)pe[3]};
+}
+
+template <bool LOWP>
+__global__ void __launch_bounds__(256) adam_ex_kernel(const AdamEx ka) {
+  kernarg_prefetch<1024>();
+  // fields read in place (a runtime descriptor index would copy the by-value block to scratch)
+  (void)ka;
+  const AdamEx& a = *(const AdamEx*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nslabblk = a.blk0[a.nslab];
+  if (a.has_elbo && b == a.nreg + nslabblk) {
+    __shared__ float kld_row[1024];
+    __shared__ float ered[4][4];
+    elbo_block(a.e, kld_row, ered);
+    return;
+  }
+  const AdamK k = adam_k(a);
+  if (b < a.nreg) {
+    const long nq = a.n / 4;
+    const long stride = (long)a.nreg * 256;
+    int j = 0;                                     // descriptors are in ascending q0
+    for (long i = (long)b * 256 + tid; i < nq; i += stride) {
+      while (j < a.nslab && a.q1[j] <= i) ++j;
+      if (j < a.nslab && i >= a.q0[j]) continue;   // a descriptor's slab workgroups own this quad
+      adam_quad<LOWP>(a, k, i, reinterpret_cast<const f32x4*>(a.g)[i]);
+    }
+    if (b == 0 && tid < a.n - nq * 4) {
+      const long i = nq * 4 + tid;
+      adam_one<LOWP>(a, k, i, a.g[i]);
+    }
+    return;
+  }
+  // the descriptor of this workgroup
+  const int sb = b - a.nreg;
+  int d = 0;
+  while (d + 1 < a.nslab && sb >= a.blk0[d + 1]) ++d;
+  d = __builtin_amdgcn_readfirstlane(d);
+  const vae_grad_slab& s = a.s[d];
+  const int lb = sb - a.blk0[d];
+  const long count = s.count, ld = s.ld;
+  const int rows = s.rows;
+  const long base = a.off[d];
+  if (a.tall[d]) {
+    __shared__ float red[16][17];
+    const int c = tid & 15, part = tid >> 4;
+    const long col = (long)lb * 16 + c;
+    float acc = 0.f;
+    if (col < count) {
+      int r = part;
+      for (; r + 16 * 7 < rows; r += 16 * 8) {
+        float t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = s.slab[(long)(r + 16 * u) * ld + col];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += t[u];
+      }
+      for (; r < rows; r += 16) acc += s.slab[(long)r * ld + col];
+    }
+    red[part][c] = acc;
+    __syncthreads();
+    if (tid < 16) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t += red[q][tid];
+      const long e = (long)lb * 16 + tid;
+      // (columns past count up to the 16-column boundary are the parameter's zero padding)
+      const float gv = e < count ? t : 0.f;
+      if (e < ((count + 15) & ~15L)) {
+        a.g[base + e] = gv;
+        adam_one<LOWP>(a, k, base + e, gv);
+      }
+    }
+    return;
+  }
+  // short: one quad per thread, rows in ascending order
+  const long q = (long)lb * 256 + tid;
+  const long e0 = q * 4;
+  if (e0 >= count) return;
+  const bool vec = (((uintptr_t)s.slab) & 15) == 0 && (ld & 3) == 0;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (vec && e0 + 4 <= count) {
+    int r = 0;
+    for (; r + 8 <= rows; r += 8) {
+      f32x4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const f32x4*>(s.slab + (long)(r + u) * ld + e0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; r < rows; ++r) acc += *reinterpret_cast<const f32x4*>(s.slab + (long)r * ld + e0);
+  } else {
+    for (int r = 0; r < rows; ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (e0 + u < count) acc[u] += s.slab[(long)r * ld + e0 + u];
+  }
+  const long gi = (base + e0) / 4;
+  reinterpret_cast<f32x4*>(a.g)[gi] = acc;
+  adam_quad<LOWP>(a, k, gi, acc);
+}
+
+}  // namespace
+
+extern "C" int vae_adam_step_ex(const vae_adam_args* a, void* stream) {
+  if (!a) return fail(VAE_E_BADARG, "adam_step_ex: args");
+  if (a->n <= 0) return VAE_OK;
+  if (!a->p || !a->g || !a->m || !a->v || !a->step || !a->lr) return fail(VAE_E_BADARG, "adam_step_ex: null");
+  auto al = [](const void* q, uintptr_t n) { return ((uintptr_t)q % n) == 0; };
+  if (!al(a->p, 16) || !al(a->g, 16) || !al(a->m, 16) || !al(a->v, 16) || (a->p_lowp && !al(a->p_lowp, 8)))
+    return fail(VAE_E_BADARG, "adam_step_ex: buffers must be 16-byte aligned (bf16 copy 8)");
+  if (a->nslab < 0 || a->nslab > VAE_SLAB_MAX) return fail(VAE_E_BADARG, "adam_step_ex: %d slabs", a->nslab);
+  if (a->has_elbo && (a->elbo.batch <= 0 || a->elbo.batch > 1024 || !a->elbo.out || !a->elbo.sse))
+    return fail(VAE_E_BADSHAPE, "adam_step_ex: deferred loss");
+  AdamEx k;
+  memset(&k, 0, sizeof(k));
+  k.n = a->n; k.p = a->p; k.g = a->g; k.m = a->m; k.v = a->v; k.step = a->step; k.lr = a->lr;
+  k.b1 = a->beta1; k.b2 = a->beta2; k.eps = a->eps; k.wd = a->weight_decay;
+  k.lowp = static_cast<__bf16*>(a->p_lowp);
+  // descriptors sorted by their position in g; each must start on a quad and not overlap the next
+  int order[VAE_SLAB_MAX];
+  for (int i = 0; i < a->nslab; ++i) order[i] = i;
+  std::sort(order, order + a->nslab, [&](int x, int y) { return a->slab[x].dst < a->slab[y].dst; });
+  int blk = 0;
+  for (int j = 0; j < a->nslab; ++j) {
+    const vae_grad_slab& s = a->slab[order[j]];
+    const long off = (long)(s.dst - a->g);
+    if (!s.dst || !s.slab || s.count <= 0 || s.rows <= 0 || s.ld < s.count || off < 0 || off + s.count > a->n || off % 4)
+      return fail(VAE_E_BADARG, "adam_step_ex: slab %d (offset %ld, count %ld)", order[j], off, (long)s.count);
+    k.s[j] = s;
+    k.off[j] = off;
+    k.tall[j] = s.rows >= kTallRows;
+    const long span = k.tall[j] ? ((s.count + 15) & ~15L) : ((s.count + 3) & ~3L);
+    if (off + span > a->n) return fail(VAE_E_BADARG, "adam_step_ex: slab %d runs past the buffer", order[j]);
+    k.q0[j] = off / 4;
+    k.q1[j] = (off + span + 3) / 4;
+    if (j > 0 && k.q0[j] < k.q1[j - 1]) return fail(VAE_E_BADARG, "adam_step_ex: slabs %d and %d overlap", order[j - 1], order[j]);
+    k.blk0[j] = blk;
+    blk += (int)(k.tall[j] ? (s.count + 15) / 16 : (s.count + 1023) / 1024);
+  }
+  k.nslab = a->nslab;
+  k.blk0[a->nslab] = blk;
+  k.nreg = grid_for((a->n + 3) / 4);
+  k.has_elbo = a->has_elbo;
+  if (a->has_elbo) k.e = a->elbo;
+  const dim3 grid((unsigned)(k.nreg + blk + (a->has_elbo ? 1 : 0)));
+  const hipStream_t st = (hipStream_t)stream;
+  if (a->p_lowp) VAE_LAUNCH(adam_ex_kernel<true>, grid, dim3(256), 0, st, k);
+  else VAE_LAUNCH(adam_ex_kernel<false>, grid, dim3(256), 0, st, k);
+  return check_launch("adam_step_ex");
 }
 
 extern "C" int vae_cast_bf16(int64_t n, const float* src, void* dst, void* stream) {

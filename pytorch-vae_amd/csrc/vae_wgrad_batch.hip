@@ -268,6 +268,8 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   // deep layers: hundreds of output tiles over few pixels) runs several units per item.  T is the
   // smallest time for which the items fit the round.
   long slab_off[kWg3Max];
+  bool defer_of[kWg3Max];
+  for (int l = 0; l < nl; ++l) defer_of[l] = items[lay[l].idx]->defer_reduce != 0;
   const long total0 = total;
   auto plan_at = [&](double T) -> long {
     total = total0;
@@ -290,9 +292,12 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       }
       L.p.slab = nullptr;
       L.p.slab_ld = L.cols;
-      L.p.own = L.slices == 1 ? 1 : 0;
+      // a deferred layer (vae_conv_args.defer_reduce) keeps even a single K slice in its slab: the
+      // caller's reduction writes dW (no read-modify-write of dW in the epilogue)
+      const bool slab = L.slices > 1 || defer_of[l];
+      L.p.own = slab ? 0 : 1;
       slab_off[l] = total;
-      if (L.slices > 1) total += (L.slices * L.cols * 4 + 255) / 256 * 256;
+      if (slab) total += (L.slices * L.cols * 4 + 255) / 256 * 256;
       const long li = (L.slices * L.tiles + L.tpi - 1) / L.tpi;
       items += li > 4096 ? (long)kWg3Items + 1 : li;
     }
@@ -335,7 +340,7 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   int ni = 0;
   for (int l = 0; l < nl; ++l) {
     Wg3Layer& L = lay[l];
-    if (L.slices > 1) L.p.slab = static_cast<float*>(region(slab_off[l]));
+    if (L.slices > 1 || defer_of[l]) L.p.slab = static_cast<float*>(region(slab_off[l]));
     g.p[l] = L.p;
     g.var[l] = L.var;
     g.tpi[l] = (int)L.tpi;
@@ -387,6 +392,10 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   Wg3Reduce r;
   memset(&r, 0, sizeof(r));
   for (int l = 0; l < nl; ++l) {
+    if (defer_of[l]) {                             // the slices stay for vae_adam_step_ex
+      if (!defer_slab(g.p[l].dw, lay[l].cols, g.p[l].slab, (int)lay[l].slices, lay[l].cols)) return VAE_E_UNSUPPORTED;
+      continue;
+    }
     if (lay[l].slices <= 1) continue;
     r.slab[r.n] = g.p[l].slab;
     r.dw[r.n] = g.p[l].dw;

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # any other value V loads libvaehip_V.so (a build-flag variant for A/B timing)
 if os.environ.get("VAE_HIP_LIB"):
     LIB_PATH = LIB_PATH.replace("libvaehip.so", "libvaehip_%s.so" % os.environ["VAE_HIP_LIB"])
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 F32, BF16 = 0, 1
 X_NONE, X_ACT, X_BN_ACT, X_BN_DY = 0, 1, 2, 3
@@ -55,7 +55,7 @@ class ConvArgs(ctypes.Structure):
                 ("dx_dgamma", c_void_p), ("dx_dbeta", c_void_p), ("dw", c_void_p), ("db", c_void_p),
                 ("split_k", c_int32), ("workspace", c_void_p), ("workspace_bytes", c_int64),
                 ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("wt_t", c_void_p),
-                ("dw_inner", c_int32), ("deterministic", c_int32)]
+                ("dw_inner", c_int32), ("deterministic", c_int32), ("defer_reduce", c_int32)]
 
 
 class LinearArgs(ctypes.Structure):
@@ -79,7 +79,7 @@ class HeadArgs(ctypes.Structure):
                 ("dw", c_void_p), ("db", c_void_p), ("grad_recon", c_void_p),
                 ("workspace", c_void_p), ("workspace_bytes", c_int64),
                 ("bn_finalize", POINTER(BnArgs)), ("bn_counter", c_void_p), ("elbo", c_void_p),
-                ("deterministic", c_int32)]
+                ("deterministic", c_int32), ("defer_reduce", c_int32)]
 
 
 class ElboArgs(ctypes.Structure):
@@ -88,6 +88,22 @@ class ElboArgs(ctypes.Structure):
                 ("c_max", c_float), ("c_stop_iter", c_float), ("iter", c_void_p), ("mulv", c_void_p),
                 ("sse", c_void_p), ("out", c_void_p), ("per_img", c_void_p), ("head_coef", c_void_p),
                 ("kl_coef", c_void_p), ("vq_sse", c_void_p), ("vq_beta", c_float), ("vq_elems", c_float)]
+
+
+SLAB_MAX = 32                      # vaehip.h VAE_SLAB_MAX
+
+
+class GradSlab(ctypes.Structure):
+    """vaehip.h vae_grad_slab: dst[j] = sum_{r < rows} slab[r * ld + j], j < count."""
+    _fields_ = [("dst", c_void_p), ("count", c_int64), ("slab", c_void_p), ("rows", c_int32), ("ld", c_int64)]
+
+
+class AdamArgs(ctypes.Structure):
+    """vaehip.h vae_adam_args (vae_adam_step_ex: Adam with the deferred slab reductions and loss)."""
+    _fields_ = [("n", c_int64), ("p", c_void_p), ("g", c_void_p), ("m", c_void_p), ("v", c_void_p),
+                ("step", c_void_p), ("lr", c_void_p), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", c_float), ("weight_decay", c_float), ("p_lowp", c_void_p), ("nslab", c_int32),
+                ("slab", GradSlab * SLAB_MAX), ("has_elbo", c_int32), ("elbo", ElboArgs)]
 
 
 class VqArgs(ctypes.Structure):
@@ -191,6 +207,9 @@ _SIGS = {
     "vae_adam_step": [c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_double,
                       ctypes.c_double, c_float, c_float, c_void_p, c_void_p],
     "vae_cast_bf16": [c_int64, c_void_p, c_void_p, c_void_p],
+    "vae_deferred_reset": [],
+    "vae_deferred_take": [POINTER(GradSlab), c_int32, POINTER(ElboArgs), POINTER(c_int32)],
+    "vae_adam_step_ex": [POINTER(AdamArgs), c_void_p],
     "vae_step_begin": [c_void_p, c_int64, c_void_p, c_void_p],
     "vae_step_record": [POINTER(RecordArgs), c_void_p],
     "vae_swap_axes": [c_int32, c_void_p, c_void_p],
@@ -265,6 +284,19 @@ WS_QUERY = {
     "vae_head_bwd_filter": ("vae_head_workspace_size", OP_BWD_FILTER),
     "vae_head_bwd": ("vae_head_workspace_size", OP_BWD),
 }
+
+
+def deferred_take():
+    """The weight-gradient reductions (and the loss) the calls since the last take / reset deferred
+    (vaehip.h vae_deferred_take): ([GradSlab], ElboArgs or None).  Clears the list."""
+    lib = load()
+    out = (GradSlab * SLAB_MAX)()
+    el = ElboArgs()
+    has = c_int32(0)
+    n = lib.vae_deferred_take(out, SLAB_MAX, ctypes.byref(el), ctypes.byref(has))
+    if n > SLAB_MAX:
+        raise VaeHipError(f"{n} deferred reductions > {SLAB_MAX}")
+    return [GradSlab.from_buffer_copy(out[i]) for i in range(n)], (el if has.value else None)
 
 
 def workspace_size(fn: str, arg) -> int:

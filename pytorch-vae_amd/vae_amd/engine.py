@@ -38,6 +38,26 @@ class FusedAdam:
     def set_lr(self, lr: float):
         self.lr.fill_(float(lr))
 
+    def apply_deferred(self, grads: torch.Tensor, slabs, elbo, stream=None):
+        """apply() with the weight-gradient reductions the backward deferred (L.deferred_take) done in
+        the same launch (vae_adam_step_ex): each reduced gradient is written into `grads` before its
+        elements' update, and a deferred loss is evaluated by one extra workgroup."""
+        net = self.net
+        if len(slabs) > L.SLAB_MAX:
+            raise ValueError(f"{len(slabs)} deferred reductions > {L.SLAB_MAX}")
+        a = self._ex = getattr(self, "_ex", None) or L.AdamArgs()
+        a.n, a.p, a.g, a.m, a.v = net.params.numel(), net.params.data_ptr(), grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr()
+        a.step, a.lr = self.step.data_ptr(), self.lr.data_ptr()
+        a.beta1, a.beta2, a.eps, a.weight_decay = self.betas[0], self.betas[1], self.eps, self.weight_decay
+        a.p_lowp = net.lowp.data_ptr() if net.lowp is not None else None
+        a.nslab = len(slabs)
+        for i, sl in enumerate(slabs):
+            a.slab[i] = sl
+        a.has_elbo = 1 if elbo is not None else 0
+        if elbo is not None:
+            a.elbo = elbo
+        L.call("vae_adam_step_ex", ctypes.byref(a), stream if stream is not None else L.stream_ptr())
+
     def apply(self, grads: torch.Tensor, stream=None, refresh_swaps: bool = True):
         """One Adam step over the flat parameters (writes the bf16 copy).  refresh_swaps=False leaves
         the swapped-axes weight copies stale (net.swaps_stale) for a caller that refreshes them at the
@@ -98,7 +118,7 @@ class TrainStep:
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
                  nbuckets: int = 1, device_eps: Optional[int] = None, force_buckets: bool = False,
-                 graph_comm: bool = True, begin_ex: bool = True):
+                 graph_comm: bool = True, begin_ex: bool = True, defer_reductions: bool = True):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -147,6 +167,12 @@ class TrainStep:
         # begin_ex=False keeps vae_step_begin + the padding calls (tests/test_gpu_routes.py)
         self._begin = begin_args(plan, opt.step) if begin_ex else None
         self._begin_swaps = self._begin is not None and self._begin[0].nswap > 0
+        # one rank: the backward's weight-gradient slab reductions (and the loss fused into the head
+        # backward) run inside the optimizer launch (StepPlan.defer_reductions, vae_adam_step_ex);
+        # with more ranks the gradients must be complete before their all-reduce
+        self.deferred = (self.comm is None and defer_reductions and hasattr(plan, "defer_reductions")
+                         and plan.defer_reductions())
+        self._slabs, self._elbo = [], None
 
     # -------------------------------------------------------------- eager pieces
     def _segment(self, k: int):
@@ -168,7 +194,12 @@ class TrainStep:
             if self.comm is not None and not getattr(p, "elbo_in_head", False):
                 p.metrics.copy_(p.out)
         lo = 0 if k == 0 else self.buckets[k - 1][0]
+        if self.deferred:
+            L.call("vae_deferred_reset")
         p._run(p.bwd_calls[lo:self.buckets[k][0]], st)
+        if self.deferred:
+            # (the same pointers at every run: each deferring call has a workspace of its own)
+            self._slabs, self._elbo = L.deferred_take()
         if k == 0 and self.comm is not None and getattr(p, "elbo_in_head", False):
             # the loss terms come from the head backward (vae_head_args.elbo), the first call of
             # segment 0's backward: copied behind it, reduced with the last bucket as before
@@ -176,6 +207,14 @@ class TrainStep:
 
     def _opt(self):
         # with the swapped copies refreshed by the next step's head, the optimizer skips its own pass
+        if self.deferred:
+            self.opt.apply_deferred(self.plan.grads, self._slabs, self._elbo, L.stream_ptr())
+            if getattr(self.net, "swap_descs", None) is not None:
+                if self._begin_swaps:
+                    self.net.swaps_stale = True
+                else:
+                    self.net.refresh_swaps(L.stream_ptr())
+            return
         self.opt.apply(self.plan.grads, L.stream_ptr(), refresh_swaps=not self._begin_swaps)
 
     def _capture(self):

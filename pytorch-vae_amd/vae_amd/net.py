@@ -302,6 +302,29 @@ class StepPlan:
             self.bwd_calls_raw = list(self.bwd_calls)
         self.batch_wgrads([len(self.bwd_calls_raw)])
 
+    def defer_reductions(self) -> bool:
+        """Leave the step's weight-gradient slab reductions — the head backward's filter partials,
+        the full-resolution ConvT backward's, the grouped weight gradients' K slices — and the loss
+        fused into the head backward to the optimizer launch (vaehip.h defer_reduce,
+        vae_adam_step_ex): three launches fewer per step.  For the one-rank fused step
+        (engine.TrainStep), whose only reader of the gradients is its own Adam; each deferring call
+        gets a workspace of its own, kept until the optimizer reads it.  bf16 training plans only;
+        returns whether anything is deferred."""
+        if self.net.dtype != torch.bfloat16 or not self.training:
+            return False
+        n = 0
+        for fn, ref in self.bwd_calls:
+            if fn == BATCH_FN:
+                for a in ref.args:
+                    a.defer_reduce = 1
+                    n += 1
+            elif fn in ("vae_convT2d_bwd", "vae_head_bwd") and ref is not None and not isinstance(ref, tuple):
+                ref._obj.defer_reduce = 1
+                n += 1
+        if n:
+            size_workspaces(self, [self.fwd_calls, self.bwd_calls])
+        return n > 0
+
     def batch_wgrads(self, ends):
         """Rebuild bwd_calls from bwd_calls_raw with the conv / convT weight gradients of each
         backward segment (calls [ends[k-1], ends[k]) of the raw list) moved into one
@@ -1028,13 +1051,19 @@ def size_workspaces(plan, call_lists):
             if fn == BATCH_FN:
                 arg = ref
                 b = ref.workspace_size()
+                deferred = any(getattr(a, "defer_reduce", 0) for a in ref.args)
             elif fn not in L.WS_QUERY:
                 continue
             else:
                 arg = ref._obj
                 b = L.workspace_size(fn, arg)
+                deferred = bool(getattr(arg, "defer_reduce", 0))
             on_side = (fn == BATCH_FN and getattr(ref, "side", False)) or (getattr(plan, "side_all", True) and fn in SIDE_FNS)
             chain = "side" if side_on and on_side else "main"
+            if deferred and b > 0:
+                # partial rows read later by the optimizer (vae_adam_step_ex): a buffer of its own
+                chain = f"deferred{len(need)}"
+                need[chain] = 0
             need[chain] = max(need[chain], b)
             sized.append((arg, b, chain))
     bufs = {c: torch.empty(max(1, (n + 3) // 4), dtype=torch.float32, device=dev) for c, n in need.items()}
@@ -1045,6 +1074,7 @@ def size_workspaces(plan, call_lists):
         else:
             arg.workspace, arg.workspace_bytes = None, 0
     plan.workspace, plan.workspace_side, plan.workspace_need = bufs["main"], bufs["side"], need
+    plan.workspace_deferred = [v for k, v in bufs.items() if k.startswith("deferred")]
 
 
 SIDE_FNS = frozenset(("vae_conv2d_bwd_filter", "vae_convT2d_bwd_filter", "vae_linear_bwd_filter",

@@ -10,7 +10,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 def declared_functions():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(vae_\w+)\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|int32_t|int64_t|const char\*)\s+(vae_\w+)\(", src, flags=re.M)))
 
 
 def test_library_loads_and_abi_version():
