@@ -178,8 +178,9 @@ typedef struct vae_conv_args {
   /* bwd_filter (bf16 grouped weight gradients of vae_conv_bwd_filter_batch, and the full-resolution
    * vae_convT2d_bwd): 1 = leave this weight gradient as fp32 partial rows in the workspace instead
    * of summing them into dw — no reduction launch; the call records a vae_grad_slab descriptor
-   * (vae_deferred_take) for the caller to reduce later (vae_adam_step_ex), and dw is then written
-   * (not accumulated) by that reduction.  The workspace must stay untouched until then. */
+   * (vae_deferred_take) for the caller to reduce later (vae_adam_step_ex).  dw is then WRITTEN, not
+   * accumulated: by that reduction, or by the call itself where one workgroup covers the whole pixel
+   * range (no partial rows, no descriptor).  The workspace must stay untouched until then. */
   int32_t defer_reduce;
 } vae_conv_args;
 
@@ -408,6 +409,7 @@ int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v,
  * in a per-host-thread list instead of launching its reduction (the fused ELBO of vae_head_args
  * likewise).  vae_deferred_take copies the list out (up to max descriptors; returns how many there
  * are; *has_elbo / *elbo: the deferred loss, if any) and clears it; vae_deferred_reset clears it.
+ * A gradient deferred again before it was taken (the same dst) replaces its earlier descriptor.
  * Workspace queries record nothing.
  * vae_adam_step_ex: vae_adam_step over the flat buffers, with the slab descriptors reduced in the
  * same launch (each dst inside g: the reduced gradient is written there, then that element's Adam

@@ -74,6 +74,11 @@ inline Deferred& deferred() {
 inline bool defer_slab(float* dst, long count, const float* slab, int rows, long ld) {
   if (querying()) return true;
   Deferred& d = deferred();
+  for (int i = 0; i < d.n; ++i)                 // the same gradient deferred again (a call re-run
+    if (d.s[i].dst == dst) {                    // before the reduction): its latest partials count
+      d.s[i] = vae_grad_slab{dst, count, slab, rows, ld};
+      return true;
+    }
   if (d.n >= VAE_SLAB_MAX) {
     fail(VAE_E_UNSUPPORTED, "deferred reductions: more than %d outstanding", VAE_SLAB_MAX);
     return false;

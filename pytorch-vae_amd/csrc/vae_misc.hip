@@ -872,16 +872,17 @@ extern "C" int32_t vae_deferred_take(vae_grad_slab* out, int32_t max, vae_elbo_a
 
 namespace {
 
-// vae_adam_step_ex in one grid:
-//   [0, nreg)                 vae_adam_step over the elements no descriptor covers (grid-stride,
-//                             16-byte accesses; quads inside a descriptor's range are skipped)
-//   [nreg, nreg + nslabblk)   per descriptor: "tall" slabs (rows >= kTallRows: the head's and the
+// vae_adam_step_ex in one grid (the slab workgroups first: dispatched first, their longer
+// reductions overlap the streaming of the plain elements instead of trailing it):
+//   [0, nslabblk)             per descriptor: "tall" slabs (rows >= kTallRows: the head's and the
 //                             full-resolution ConvT's per-workgroup partials) as 16 columns x 16 row
 //                             parts per workgroup, parts combined in LDS in ascending order; "short"
 //                             slabs (K slices of the grouped weight gradients) as 256 quads per
 //                             workgroup, each thread summing its quad's rows in ascending order —
 //                             then g = that sum is written and the element's Adam update runs
-//   [last]                    the deferred loss (elbo_block), when present
+//   [nslabblk]                the deferred loss (elbo_block), when present
+//   [.., + nreg)              vae_adam_step over the elements no descriptor covers (grid-stride,
+//                             16-byte accesses; quads inside a descriptor's range are skipped)
 constexpr int kTallRows = 64;
 struct AdamEx {
   long n;
@@ -932,29 +933,38 @@ __device__ __forceinline__ void adam_quad(const AdamEx& a, const AdamK& k, long 
   if (LOWP) reinterpret_cast<bf16x4*>(a.lowp)[i] = bf16x4{(__bf16)pe[0], (__bf16)pe[1], (__bf16)pe[2], (__bf16)pe[3]};
 }
 
+// (a streaming kernel: <= 64 VGPRs keeps 8 waves per SIMD; at 104 it ran 4 and took 33 us for the
+// 19.6 us of bytes of vae_adam_step plus the slabs)
 template <bool LOWP>
-__global__ void __launch_bounds__(256) adam_ex_kernel(const AdamEx ka) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) adam_ex_kernel(const AdamEx ka) {
   kernarg_prefetch<1024>();
   // fields read in place (a runtime descriptor index would copy the by-value block to scratch)
   (void)ka;
   const AdamEx& a = *(const AdamEx*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int nslabblk = a.blk0[a.nslab];
-  if (a.has_elbo && b == a.nreg + nslabblk) {
+  if (a.has_elbo && (int)blockIdx.x == nslabblk) {
     __shared__ float kld_row[1024];
     __shared__ float ered[4][4];
     elbo_block(a.e, kld_row, ered);
     return;
   }
   const AdamK k = adam_k(a);
-  if (b < a.nreg) {
+  if ((int)blockIdx.x >= nslabblk) {
+    const int b = (int)blockIdx.x - nslabblk - (a.has_elbo ? 1 : 0);
     const long nq = a.n / 4;
     const long stride = (long)a.nreg * 256;
-    int j = 0;                                     // descriptors are in ascending q0
-    for (long i = (long)b * 256 + tid; i < nq; i += stride) {
-      while (j < a.nslab && a.q1[j] <= i) ++j;
-      if (j < a.nslab && i >= a.q0[j]) continue;   // a descriptor's slab workgroups own this quad
-      adam_quad<LOWP>(a, k, i, reinterpret_cast<const f32x4*>(a.g)[i]);
+    // the workgroup's 256 quads of an iteration start at ib (uniform): the descriptor ranges they
+    // can meet are found with scalar loads, each lane then tests only those (ascending q0)
+    int j = 0;
+    for (long ib = (long)b * 256; ib < nq; ib += stride) {
+      while (j < a.nslab && a.q1[j] <= ib) ++j;
+      j = __builtin_amdgcn_readfirstlane(j);
+      const long i = ib + tid;
+      if (i >= nq) break;
+      bool own = true;
+      for (int t = j; t < a.nslab && a.q0[t] < ib + 256; ++t) own = own && !(i >= a.q0[t] && i < a.q1[t]);
+      if (own) adam_quad<LOWP>(a, k, i, reinterpret_cast<const f32x4*>(a.g)[i]);
     }
     if (b == 0 && tid < a.n - nq * 4) {
       const long i = nq * 4 + tid;
@@ -963,7 +973,7 @@ __global__ void __launch_bounds__(256) adam_ex_kernel(const AdamEx ka) {
     return;
   }
   // the descriptor of this workgroup
-  const int sb = b - a.nreg;
+  const int sb = (int)blockIdx.x;
   int d = 0;
   while (d + 1 < a.nslab && sb >= a.blk0[d + 1]) ++d;
   d = __builtin_amdgcn_readfirstlane(d);
@@ -976,6 +986,11 @@ __global__ void __launch_bounds__(256) adam_ex_kernel(const AdamEx ka) {
     __shared__ float red[16][17];
     const int c = tid & 15, part = tid >> 4;
     const long col = (long)lb * 16 + c;
+    // the element's optimizer state goes out first: its round trip overlaps the column sums
+    const long e = (long)lb * 16 + tid;
+    const bool upd = tid < 16 && e < ((count + 15) & ~15L);
+    float pi = 0.f, mi = 0.f, vi = 0.f;
+    if (upd) { pi = a.p[base + e]; mi = a.m[base + e]; vi = a.v[base + e]; }
     float acc = 0.f;
     if (col < count) {
       int r = part;
@@ -990,34 +1005,38 @@ __global__ void __launch_bounds__(256) adam_ex_kernel(const AdamEx ka) {
     }
     red[part][c] = acc;
     __syncthreads();
-    if (tid < 16) {
+    if (upd) {
       float t = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) t += red[q][tid];
-      const long e = (long)lb * 16 + tid;
       // (columns past count up to the 16-column boundary are the parameter's zero padding)
       const float gv = e < count ? t : 0.f;
-      if (e < ((count + 15) & ~15L)) {
-        a.g[base + e] = gv;
-        adam_one<LOWP>(a, k, base + e, gv);
-      }
+      a.g[base + e] = gv;
+      adam_elem(k, pi, gv, mi, vi);
+      a.m[base + e] = mi; a.v[base + e] = vi; a.p[base + e] = pi;
+      if (LOWP) a.lowp[base + e] = (__bf16)pi;
     }
     return;
   }
-  // short: one quad per thread, rows in ascending order
+  // short: one quad per thread, rows in ascending order (the K slices of a grouped weight gradient:
+  // 1-32 rows), the quad's optimizer state loaded first so both round trips overlap
   const long q = (long)lb * 256 + tid;
   const long e0 = q * 4;
   if (e0 >= count) return;
+  const long gi = (base + e0) / 4;
+  f32x4 p4 = reinterpret_cast<const f32x4*>(a.p)[gi];
+  f32x4 m4 = reinterpret_cast<const f32x4*>(a.m)[gi];
+  f32x4 v4 = reinterpret_cast<const f32x4*>(a.v)[gi];
   const bool vec = (((uintptr_t)s.slab) & 15) == 0 && (ld & 3) == 0;
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   if (vec && e0 + 4 <= count) {
     int r = 0;
-    for (; r + 8 <= rows; r += 8) {
-      f32x4 t[8];
+    for (; r + 6 <= rows; r += 6) {
+      f32x4 t[6];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = *reinterpret_cast<const f32x4*>(s.slab + (long)(r + u) * ld + e0);
+      for (int u = 0; u < 6; ++u) t[u] = *reinterpret_cast<const f32x4*>(s.slab + (long)(r + u) * ld + e0);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc += t[u];
+      for (int u = 0; u < 6; ++u) acc += t[u];
     }
     for (; r < rows; ++r) acc += *reinterpret_cast<const f32x4*>(s.slab + (long)r * ld + e0);
   } else {
@@ -1026,9 +1045,17 @@ __global__ void __launch_bounds__(256) adam_ex_kernel(const AdamEx ka) {
       for (int u = 0; u < 4; ++u)
         if (e0 + u < count) acc[u] += s.slab[(long)r * ld + e0 + u];
   }
-  const long gi = (base + e0) / 4;
   reinterpret_cast<f32x4*>(a.g)[gi] = acc;
-  adam_quad<LOWP>(a, k, gi, acc);
+  float pe[4], me[4], ve[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    pe[u] = p4[u]; me[u] = m4[u]; ve[u] = v4[u];
+    adam_elem(k, pe[u], acc[u], me[u], ve[u]);
+  }
+  reinterpret_cast<f32x4*>(a.p)[gi] = f32x4{pe[0], pe[1], pe[2], pe[3]};
+  reinterpret_cast<f32x4*>(a.m)[gi] = f32x4{me[0], me[1], me[2], me[3]};
+  reinterpret_cast<f32x4*>(a.v)[gi] = f32x4{ve[0], ve[1], ve[2], ve[3]};
+  if (LOWP) reinterpret_cast<bf16x4*>(a.lowp)[gi] = bf16x4{(__bf16)pe[0], (__bf16)pe[1], (__bf16)pe[2], (__bf16)pe[3]};
 }
 
 }  // namespace

@@ -41,7 +41,9 @@ struct WgParams {
   float* slab;                       // non-NULL: K slice s stores its partial dW at slab + s*slab_ld
   long slab_ld;                      //   (plain stores; wg_slab_reduce adds the slices into dw)
   int own;                           // one K slice: each dW element has one writer, so it is
-                                     // accumulated with a plain load + store instead of an atomic
+                                     // accumulated with a plain load + store instead of an atomic;
+                                     // 2: written with a plain store (dW is this call's alone:
+                                     // vae_conv_args.defer_reduce), no load of the old value
   int jst;                           // stored j extent of dw (0: J): dW is [M][R][R][jst], j >= jst
                                      // dropped (vae_conv_args.dw_inner: a zero-padded operand)
 };
@@ -73,6 +75,18 @@ template <int TM, int TJ>
 __device__ __forceinline__ void wg_epilogue(const WgParams& p, float* part, const f32x4 (&acc)[TM][TJ], int mrow,
                                             int jcol, long rowstride, long coff) {
   const int jst = p.jst > 0 ? p.jst : p.J;
+  if (!part && p.own == 2) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int mm = mrow + i * 16 + e, jj = jcol + j * 16;
+          if (mm < p.M && jj < jst) p.dw[mm * rowstride + coff + jj] = acc[i][j][e];
+        }
+    return;
+  }
   if (!part && p.own) {
     // in groups of fragment rows holding <= 32 values (registers: the 128 x 128 tiles run at 256)
     constexpr int GI = TJ * 4 * TM <= 32 ? TM : (32 / (TJ * 4) > 0 ? 32 / (TJ * 4) : 1);

@@ -292,10 +292,11 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       }
       L.p.slab = nullptr;
       L.p.slab_ld = L.cols;
-      // a deferred layer (vae_conv_args.defer_reduce) keeps even a single K slice in its slab: the
-      // caller's reduction writes dW (no read-modify-write of dW in the epilogue)
-      const bool slab = L.slices > 1 || defer_of[l];
-      L.p.own = slab ? 0 : 1;
+      // a deferred layer (vae_conv_args.defer_reduce): its K slices stay in the slab for the
+      // caller's reduction, which writes dW; with one slice the epilogue writes dW itself, no
+      // read-modify-write (the reduction would read back exactly that slice)
+      const bool slab = L.slices > 1;
+      L.p.own = slab ? 0 : (defer_of[l] ? 2 : 1);
       slab_off[l] = total;
       if (slab) total += (L.slices * L.cols * 4 + 255) / 256 * 256;
       const long li = (L.slices * L.tiles + L.tpi - 1) / L.tpi;
@@ -340,7 +341,7 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   int ni = 0;
   for (int l = 0; l < nl; ++l) {
     Wg3Layer& L = lay[l];
-    if (L.slices > 1 || defer_of[l]) L.p.slab = static_cast<float*>(region(slab_off[l]));
+    if (L.slices > 1) L.p.slab = static_cast<float*>(region(slab_off[l]));
     g.p[l] = L.p;
     g.var[l] = L.var;
     g.tpi[l] = (int)L.tpi;
@@ -392,7 +393,7 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   Wg3Reduce r;
   memset(&r, 0, sizeof(r));
   for (int l = 0; l < nl; ++l) {
-    if (defer_of[l]) {                             // the slices stay for vae_adam_step_ex
+    if (defer_of[l] && lay[l].slices > 1) {        // the slices stay for vae_adam_step_ex
       if (!defer_slab(g.p[l].dw, lay[l].cols, g.p[l].slab, (int)lay[l].slices, lay[l].cols)) return VAE_E_UNSUPPORTED;
       continue;
     }

@@ -23,6 +23,7 @@
 #   kprobe           per-block phase probe (needs `make probe`)
 #   kbench[:ARGS]    per-launch microbench under a kernel trace (tools/kbench.py, ARGS comma-separated)
 #   headbench        the decoder-head kernels back to back (tools/headbench.py): fwd, bwd, bwd halves
+#   adambench        vae_adam_step_ex with each class of deferred reductions (tools/adambench.py)
 #   c3bench[:ENV]    the VQ-VAE image-tile kernels back to back (tools/c3bench.py), ENV e.g.
 #                    VAE_C3_DBG=5 (phase ablation: 1 no chunk loads, 2 no MFMAs, 4 no LDS stores)
 #   c3trace          tools/c3bench.py under rocprofv3 --kernel-trace --stats
@@ -79,6 +80,7 @@ for step in "$@"; do
     prof) if [ -n "$a1" ]; then prof prof_$a1 --arch $a1 --batch $a2; else prof prof; fi ;;
     pmc) if [ -n "$a1" ]; then pmc pmc_$a1 --arch $a1 --batch $a2; else pmc pmc; fi ;;
     headbench) run headbench 200 python3 -u tools/headbench.py ;;
+    adambench) run adambench 200 python3 -u tools/adambench.py ;;
     hbenv) run hbenv_${a1//[=,]/_} 200 env ${a1//,/ } python3 -u tools/headbench.py ;;
     kprobe) run kprobe 200 env VAE_HIP_LIB=probe python3 -u tools/kprobe.py --out $O/${TAG}_kp.json ;;
     kbench) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \

@@ -63,13 +63,23 @@ class Check:
 
 
 class BN:
-    """Train-mode BatchNorm of a stored pre-BN map y (NCHW fp64) with the fp32 master gamma / beta."""
+    """Train-mode BatchNorm of a stored pre-BN map y (NCHW fp64) with the fp32 master gamma / beta.
 
-    def __init__(self, y, gamma, beta):
+    Teacher-forced statistics: `fsum` = the producer's own replicated sums (StepPlan.bnfwd:
+    [2][reps][C] of y - shift, shift the producing conv's bias) give the mean / variance the
+    consuming kernels used; `bsum` (StepPlan.bnbwd: sum g*xhat, sum g) the BatchNorm-backward's.
+    Without them the statistics come from the stored tensors (fp64)."""
+
+    def __init__(self, y, gamma, beta, fsum=None, shift=None):
         self.y = y
         self.M = y.shape[0] * y.shape[2] * y.shape[3]
-        self.mean = y.mean((0, 2, 3))
-        self.var = y.var((0, 2, 3), unbiased=False)
+        if fsum is not None:
+            s0, s1 = fsum[0] / self.M, fsum[1] / self.M
+            self.mean = s0 + shift
+            self.var = torch.clamp(s1 - s0 * s0, min=0.0)
+        else:
+            self.mean = y.mean((0, 2, 3))
+            self.var = y.var((0, 2, 3), unbiased=False)
         self.invstd = 1.0 / torch.sqrt(self.var + BN_EPS)
         self.gamma, self.beta = gamma, beta
         v = lambda t: t.view(1, -1, 1, 1)
@@ -81,18 +91,21 @@ class BN:
         return bf(lrelu(self.z))
 
     def ambiguous(self):
-        return self.z.abs() < 1e-4 * self.z.abs().max()
+        return self.z.abs() < 1e-5 * self.z.abs().max()
 
     def lrelu_back(self, dact):
         """dL/dz from dL/d lrelu(z)."""
         return torch.where(self.z > 0, dact, dact * SLOPE)
 
-    def dy(self, g):
+    def dy(self, g, bsum=None):
         """dL/dy from g = dL/dz (BatchNorm backward, batch statistics), rounded to bf16 as the
-        consuming kernel stages it: a*g + b*y + c."""
+        consuming kernel stages it: a*g + b*y + c.  bsum: the producer's (sum g*xhat, sum g)."""
         v = lambda t: t.view(1, -1, 1, 1)
-        mg = g.mean((0, 2, 3))
-        mgx = (g * self.xhat).mean((0, 2, 3))
+        if bsum is not None:
+            mgx, mg = bsum[0] / self.M, bsum[1] / self.M
+        else:
+            mg = g.mean((0, 2, 3))
+            mgx = (g * self.xhat).mean((0, 2, 3))
         a = self.gamma * self.invstd
         b = -a * self.invstd * mgx
         c = -a * (mg - self.mean * self.invstd * mgx)
@@ -106,23 +119,19 @@ class BN:
 
 
 def cmp_bf16(got, ref, mask=None):
-    err = (got - ref).abs()
-    rms = float(ref.pow(2).mean().sqrt())
-    bound = 2.0 ** -7 * ref.abs() + 2e-3 * rms
-    bad = err > bound
+    """A bf16 output: relative norm <= 3e-3 (its rounding is 2^-9 relative per element) and
+    max |got - ref| <= 2^-7 max |ref| (two bf16 ulps at the largest magnitude); elements whose
+    LeakyReLU branch is ambiguous (mask) are excluded and counted."""
     n_amb = 0
     if mask is not None:
         n_amb = int(mask.sum())
-        bad = bad & ~mask
         keep = ~mask
-        rn = float((got - ref)[keep].norm() / ref[keep].norm().clamp_min(1e-30))
-    else:
-        rn = float((got - ref).norm() / ref.norm().clamp_min(1e-30))
-    nbad = int(bad.sum())
-    worst = float((err / bound).max())
-    ok = nbad == 0 and rn <= 4e-3 and (mask is None or n_amb <= 1e-3 * ref.numel())
-    return ok, {"relnorm": rn, "n_bad": nbad, "worst_err_over_bound": worst, "ambiguous": n_amb,
-                "elements": ref.numel()}
+        got, ref = got[keep], ref[keep]
+    d = got - ref
+    rn = float(d.norm() / ref.norm().clamp_min(1e-30))
+    rm = float(d.abs().max() / ref.abs().max().clamp_min(1e-30))
+    ok = rn <= 3e-3 and rm <= 2.0 ** -7 and n_amb <= 1e-3 * (ref.numel() + n_amb)
+    return ok, {"relnorm": rn, "relmax": rm, "ambiguous": n_amb, "elements": ref.numel() + n_amb}
 
 
 def cmp_f32(got, ref, relmax_bar=2e-3, relnorm_bar=1e-3):
@@ -159,13 +168,40 @@ class StepCheck:
         self.checks: List[Check] = []
         self.h = net.hidden_dims
         self.B, self.S = plan.B, plan.S
+        # which call produced each BatchNorm's forward sums (the conv / convT feeding it) and its
+        # backward sums (the data gradient whose epilogue applies its LeakyReLU backward)
+        h, nd = self.h, len(self.h) - 1
+        self._stat_call = {f"encoder.{i}.1": ("vae_conv2d_fwd", i) for i in range(len(h))}
+        self._stat_call.update({f"decoder.{i}.1": ("vae_convT2d_fwd", i) for i in range(nd)})
+        self._stat_call["final_layer.1"] = ("vae_convT2d_fwd", nd)
+        self._bstat_call = {"final_layer.1": ("vae_head_bwd", 0), f"decoder.{nd - 1}.1": ("vae_convT2d_bwd", 0),
+                            f"encoder.{len(h) - 1}.1": ("vae_latent_fc_bwd", 0)}
+        self._bstat_call.update({f"decoder.{i}.1": ("vae_convT2d_bwd_data", nd - 2 - i) for i in range(nd - 1)})
+        self._bstat_call.update({f"encoder.{i}.1": ("vae_conv2d_bwd_data", len(h) - 2 - i) for i in range(len(h) - 1)})
 
     def add(self, name, call, res):
         ok, det = res
         self.checks.append(Check(name, call, bool(ok), det))
 
     def bn(self, y, prefix):
-        return BN(y, self.P[prefix + ".weight"], self.P[prefix + ".bias"])
+        """The BatchNorm `prefix` of stored map y with the producer's own statistics (teacher forcing),
+        and a check of those statistics against the stored tensor's."""
+        fs = cpu64(self.plan.bnfwd[prefix]).sum(1)                      # [2][C]
+        conv = prefix[:-2] + ".0.bias"
+        bn = BN(y, self.P[prefix + ".weight"], self.P[prefix + ".bias"], fs, self.P[conv])
+        sh = self.P[conv].view(1, -1, 1, 1)
+        want = torch.stack([(y - sh).sum((0, 2, 3)), ((y - sh) ** 2).sum((0, 2, 3))])
+        # (the producer sums its fp32 accumulators before the bf16 store: relative 1e-3 is that rounding)
+        self.add(f"{prefix} forward statistics", self._stat_call.get(prefix, ("?", 0)),
+                 cmp_f32(fs, want, 5e-3, 2e-3))
+        return bn
+
+    def bsum(self, prefix, bn, g):
+        """The producer's BatchNorm-backward sums of `prefix`, checked against the stored gradient."""
+        bs = cpu64(self.plan.bnbwd[prefix]).sum(1)                      # [sum g*xhat, sum g][C]
+        self.add(f"{prefix} backward statistics", self._bstat_call.get(prefix, ("?", 0)),
+                 cmp_f32(bs, torch.stack([bn.dgamma(g), bn.dbeta(g)]), 1e-2, 5e-3))
+        return bs
 
     # -------------------------------------------------------------------------------- forward
     def run(self):
@@ -259,7 +295,8 @@ class StepCheck:
         wgrad_refs = {}
         for i in reversed(range(len(names))):
             pre = names[i]
-            dy = dbns[i].dy(g_outs[i])
+            bs = self.bsum(pre + ".1", dbns[i], g_outs[i])
+            dy = dbns[i].dy(g_outs[i], bs)
             x_in = dbns[i - 1].act() if i > 0 else h0
             dx, dw = conv_grads("convT", x_in, self.W[pre + ".0.weight"], dy, 2, 1, 1)
             wgrad_refs[pre + ".0.weight"] = dw
@@ -269,7 +306,7 @@ class StepCheck:
                          cmp_bf16(g_outs[i - 1], dbns[i - 1].lrelu_back(dx), dbns[i - 1].ambiguous()))
             else:
                 self.add(f"{pre} convT bwd data (d decoder_input)", call, cmp_bf16(g_h0, dx))
-            self._bn_param_grads(pre + ".1", dbns[i], g_outs[i])
+            self._bn_param_grads(pre + ".1", bs)
         # bottleneck backward (vae_latent_dec_bwd / vae_latent_fc_bwd)
         gh = g_h0.flatten(1)
         self.add("decoder_input.weight grad", ("vae_latent_dec_bwd", 0),
@@ -284,28 +321,30 @@ class StepCheck:
         dmulv = torch.cat([dmu, dlv], 1)
         self.add("d mu|logvar", ("vae_latent_dec_bwd", 0), cmp_f32(cpu64(p.dmulv).view(B, -1), dmulv))
         gd = cpu64(p.dmulv).view(B, -1)
+        g16 = bf(gd)                     # (the bottleneck kernels stage d[mu|logvar] as a bf16 operand)
         self.add("fc_mu.weight grad", ("vae_latent_fc_bwd", 0),
-                 cmp_f32(self.G["fc_mu.weight"], gd[:, :gd.shape[1] // 2].t() @ act4))
+                 cmp_f32(self.G["fc_mu.weight"], g16[:, :gd.shape[1] // 2].t() @ act4))
         self.add("fc_var.weight grad", ("vae_latent_fc_bwd", 0),
-                 cmp_f32(self.G["fc_var.weight"], gd[:, gd.shape[1] // 2:].t() @ act4))
+                 cmp_f32(self.G["fc_var.weight"], g16[:, gd.shape[1] // 2:].t() @ act4))
         self.add("fc_mu|fc_var bias grad", ("vae_latent_fc_bwd", 0),
                  cmp_f32(torch.cat([self.G["fc_mu.bias"], self.G["fc_var.bias"]]), gd.sum(0)))
         wcat = torch.cat([self.W["fc_mu.weight"], self.W["fc_var.weight"]], 0)
-        dact4 = (gd @ wcat).view_as(bns[-1].y)
+        dact4 = (g16 @ wcat).view_as(bns[-1].y)
         g_enc = [nchw(t) for t in p.g_enc]
         self.add("fc bwd data (g encoder.4)", ("vae_latent_fc_bwd", 0),
                  cmp_bf16(g_enc[-1], bns[-1].lrelu_back(dact4), bns[-1].ambiguous()))
         # encoder backward
         for i in reversed(range(len(h))):
             pre = f"encoder.{i}"
-            dy = bns[i].dy(g_enc[i])
+            bs = self.bsum(pre + ".1", bns[i], g_enc[i])
+            dy = bns[i].dy(g_enc[i], bs)
             x_in = bns[i - 1].act() if i > 0 else bf(x)
             dx, dw = conv_grads("conv", x_in, self.W[pre + ".0.weight"], dy, 2, 1)
             wgrad_refs[pre + ".0.weight"] = dw
             if i > 0:
                 self.add(f"{pre} conv bwd data", ("vae_conv2d_bwd_data", len(h) - 1 - i),
                          cmp_bf16(g_enc[i - 1], bns[i - 1].lrelu_back(dx), bns[i - 1].ambiguous()))
-            self._bn_param_grads(pre + ".1", bns[i], g_enc[i])
+            self._bn_param_grads(pre + ".1", bs)
         # every conv / convT weight gradient (the grouped launch vae_conv_bwd_filter_batch)
         for k, ref in wgrad_refs.items():
             call = ("vae_convT2d_bwd", 0) if k == "final_layer.0.weight" else ("vae_conv_bwd_filter_batch", 0)
@@ -335,12 +374,13 @@ class StepCheck:
         hc = torch.full((B,), 2.0 / (B * E), dtype=D64)
         return hc, torch.full((B,), klc / B, dtype=D64), torch.stack([loss, recon, rep])
 
-    def _bn_param_grads(self, prefix, bn, g):
-        # published by the weight-gradient call of the conv feeding the BatchNorm (StepPlan.bwd_extras):
-        # the full-resolution ConvT's own call for final_layer.1, the grouped launch for the rest
+    def _bn_param_grads(self, prefix, bs):
+        """dL/dgamma, dL/dbeta as the weight-gradient call of the conv feeding the BatchNorm publishes
+        them (StepPlan.bwd_extras; the full-resolution ConvT's own call for final_layer.1): the sums
+        the backward produced (checked against the stored gradient by bsum)."""
         call = ("vae_convT2d_bwd", 0) if prefix == "final_layer.1" else ("vae_conv_bwd_filter_batch", 0)
-        self.add(f"{prefix}.weight grad (dgamma)", call, cmp_f32(self.G[prefix + ".weight"], bn.dgamma(g)))
-        self.add(f"{prefix}.bias grad (dbeta)", call, cmp_f32(self.G[prefix + ".bias"], bn.dbeta(g)))
+        self.add(f"{prefix}.weight grad (dgamma)", call, cmp_f32(self.G[prefix + ".weight"], bs[0], 1e-5, 1e-5))
+        self.add(f"{prefix}.bias grad (dbeta)", call, cmp_f32(self.G[prefix + ".bias"], bs[1], 1e-5, 1e-5))
 
     def _check_running(self, pairs, tag):
         lay = self.net.layout
@@ -412,6 +452,9 @@ def run_bench_step(arch: str, batch: int, seed: int = 1265):
         per_call[("adam", 0)] = launched(lambda: opt.apply_deferred(plan.grads, step._slabs, step._elbo, sp))
     else:
         per_call[("adam", 0)] = launched(lambda: opt.apply(plan.grads, sp, refresh_swaps=False))
+    # what TrainStep's capture ran besides the step (it restores the state the warm-up step changed
+    # and refreshes the bf16 weight copies: net.sync_lowp) — not part of the replayed step
+    per_call[("restore", 0)] = launched(net.sync_lowp)
     torch.cuda.synchronize()
     return checks, names_step, per_call
 
@@ -435,9 +478,13 @@ def coverage(checks: List[Check], names_step: str, per_call: Dict[Tuple[str, int
             ok_by_call.setdefault(c.call, []).append(c.name)
     cov: Dict[str, List[str]] = {}
     for call, text in per_call.items():
+        if call[0] == "restore":
+            continue
         for k in kernel_names(text):
             cov.setdefault(k, [])
             cov[k] += ok_by_call.get(call, [])
-    step_kernels = kernel_names(names_step)
+    restore = set(kernel_names(per_call.get(("restore", 0), "")))
+    # every kernel the step launched belongs to a call of the step (or to the capture's restore)
+    step_kernels = [k for k in kernel_names(names_step) if k in cov or k not in restore]
     missing = [k for k in step_kernels if not cov.get(k)]
     return cov, step_kernels, missing
