@@ -79,6 +79,11 @@ def parse():
                          "VanillaVAE family measured 0.88 vs 0.77 ms (r1: the graph's per-call fork/join edges cost "
                          "more than the overlap gains), VQ-VAE 3.436 on vs 3.330 off at r4 (it was 9.96 -> 8.51 ms "
                          "in r1, before the image-tile kernels filled the chip on their own)")
+    ap.add_argument("--wg-overlap", action="store_true",
+                    help="the decoder's weight gradients as their own batch on a side stream in the graph "
+                         "(StepPlan(wg_overlap=True)), beside the encoder's data gradients")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="keep the slab reductions as launches of their own (TrainStep(defer_reductions=False))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernel-breakdown", action="store_true", help="print per-kernel times to stderr")
@@ -617,7 +622,8 @@ def main():
         loss = {"vanilla": "vanilla", "betaH": "betaH", "iwae": "iwae"}[args.arch]
         kld = {"vanilla": 1e-8, "betaH": 2.5e-4, "iwae": 2.5e-4}[args.arch]
         lr = {"vanilla": 0.005, "betaH": 0.005, "iwae": 0.007}[args.arch]
-        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S, concurrent=args.concurrent == "on")
+        plan = StepPlan(net, args.batch, loss=loss, kld_weight=kld, samples=S, concurrent=args.concurrent == "on",
+                        wg_overlap=args.wg_overlap)
         opt = FusedAdam(net, lr=lr)
     # synthetic data resident in HBM (per-rank seed 1265+rank): U[0,1) images, N(0,1) eps
     g = torch.Generator(device="cuda").manual_seed(1265 + rank)
@@ -626,7 +632,8 @@ def main():
     # vanilla_vae.py:116) where the fused bottleneck does it; otherwise a resident N(0,1) draw
     ae = args.arch in AE_WIDTHS
     step = TrainStep(net, plan, opt, graph=not args.no_graph, device_eps=None if ae or args.arch == "vq" else 1265 + rank,
-                     graph_comm=not args.host_comm, force_buckets=args.force_buckets, nbuckets=args.buckets)
+                     graph_comm=not args.host_comm, force_buckets=args.force_buckets, nbuckets=args.buckets,
+                     defer_reductions=not args.no_defer)
     if hasattr(plan, "eps") and not ae and not step.device_eps:
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
 

@@ -16,10 +16,25 @@ what pins THOSE kernels at step level, at the benchmarked shapes:
 Bar: every gradient's relative-norm error against the fp32 oracle within
 2x the autocast oracle's own error on that tensor + 2e-3; the loss terms within 2x the autocast
 oracle's error + 1e-4 relative."""
+import json
+import os
+
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _record_coverage(tag, test, names):
+    """The kernels a passing step-level test ran (vae_launch_log), for tools/kernel_coverage.py."""
+    from stepcheck import kernel_names
+    out = os.path.join(REPO, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"kernel_coverage_{tag}.json"), "w") as f:
+        json.dump({"test": f"tests/test_gpu_bf16_shapes.py::{test}", "step_kernels": kernel_names(names),
+                   "coverage": {k: [test] for k in kernel_names(names)}}, f, indent=1)
 
 
 def _loss_bar(got, o32, oac, keys):
@@ -110,7 +125,9 @@ def test_big_ae_b64_bf16_tracks_autocast_oracle():
                                       device="cuda")
     model.load_reference_state_dict(sd)
     step = model.fused_train_step(64, 0.0, lr=0.0005, graph=True)
-    step(x.cuda())
+    from gpu_util import launched
+    xs = x.cuda()
+    names = launched(lambda: step(xs))
     torch.cuda.synchronize()
     got = step.loss_terms()
     o32, oac = _oracles("Autoencoder", sd, x, None, M_N=0.0, hidden_dims=hd)
@@ -118,6 +135,7 @@ def test_big_ae_b64_bf16_tracks_autocast_oracle():
     g_all = {k: v.cpu() for k, v in model.net.layout.export_reference(step.plan.grads).items()}
     g16 = {n: g_all["fc_mu." + n[3:] if n.startswith("fc.") else n] for n in o32["grads"]}
     assert _grad_bar(g16, o32, oac, "big_ae B=64", _pre_bn_bias) >= 30
+    _record_coverage("ae_big_64", "test_big_ae_b64_bf16_tracks_autocast_oracle", names)
 
 
 def test_vq_b128_bf16_tracks_autocast_oracle_every_gradient():
@@ -132,11 +150,14 @@ def test_vq_b128_bf16_tracks_autocast_oracle_every_gradient():
     net.load_reference_state_dict(sd)
     plan = VQStepPlan(net, B, beta=0.25)
     opt = FusedAdam(net, lr=0.005)
-    plan.x.copy_(x)
-    st = L.stream_ptr()
-    L.call("vae_step_begin", plan.zero.data_ptr(), plan.zero.numel() * 4, opt.step.data_ptr(), st)
-    plan.forward(st)
-    plan.backward(st)
+    from gpu_util import launched
+    from vae_amd.engine import TrainStep
+    # bench.py --arch vq's step: the graph-replayed TrainStep (step head, forward, loss, backward,
+    # Adam); the capture restores the state its warm-up step changed, so the replay is one step
+    # from these parameters (the gradients stay in plan.grads)
+    step = TrainStep(net, plan, opt, graph=True)
+    xs = x.cuda()
+    names = launched(lambda: step(xs))
     torch.cuda.synchronize()
     idx = plan.indices.cpu()
     o32, oac = _oracles("VQVAE", sd, x, None, M_N=0.0, vq_beta=0.25, vq_indices=idx)
@@ -146,3 +167,4 @@ def test_vq_b128_bf16_tracks_autocast_oracle_every_gradient():
     n = _grad_bar(g16, o32, oac, "VQ B=128")
     assert n == len(o32["grads"]), (n, len(o32["grads"]))       # every tensor has a gradient and is checked
     assert any("res" in k or "encoder.3" in k for k in o32["grads"])
+    _record_coverage("vq_128", "test_vq_b128_bf16_tracks_autocast_oracle_every_gradient", names)
