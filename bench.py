@@ -68,7 +68,12 @@ def parse():
                          "ae_vvbig: the Autoencoder of configs/big_ae.yaml / patient_vbig_ae.yaml / "
                          "patient_vvbig_ae.yaml (MSE, no KL)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--buckets", type=int, default=1, help="N > 1: gradient buckets (all-reduces) per step")
+    ap.add_argument("--buckets", type=int, default=2,
+                    help="N > 1: gradient buckets (all-reduces) per step; with more than one the weight "
+                         "gradients closing each bucket but the last overlap the next backward segment")
+    ap.add_argument("--no-overlap", action="store_true", help="N > 1: no overlap stream (TrainStep(overlap=False))")
+    ap.add_argument("--comm-bf16", action="store_true",
+                    help="N > 1: all-reduce the gradients in bf16 (TrainStep(comm_dtype=torch.bfloat16); opt-in)")
     ap.add_argument("--force-buckets", action="store_true",
                     help="run the bucketed all-reduce path even at one rank (under torch.distributed.run)")
     ap.add_argument("--host-comm", action="store_true",
@@ -633,7 +638,8 @@ def main():
     ae = args.arch in AE_WIDTHS
     step = TrainStep(net, plan, opt, graph=not args.no_graph, device_eps=None if ae or args.arch == "vq" else 1265 + rank,
                      graph_comm=not args.host_comm, force_buckets=args.force_buckets, nbuckets=args.buckets,
-                     defer_reductions=not args.no_defer)
+                     defer_reductions=not args.no_defer, overlap=not args.no_overlap,
+                     comm_dtype=torch.bfloat16 if args.comm_bf16 else torch.float32)
     if hasattr(plan, "eps") and not ae and not step.device_eps:
         plan.eps.copy_(torch.randn(plan.eps.shape, generator=g, device="cuda"))
 
@@ -743,7 +749,10 @@ def main():
                                 f"64x64 train step (fwd+ELBO+bwd+Adam){' IWAE K=5' if S > 1 else ''}"),
                    "per_gpu_batch": args.batch, "global_batch": world * args.batch,
                    "parallelism": f"dp{world}", "graph": not args.no_graph,
-                   "comm": comm + (" (in-graph)" if getattr(step, "graph_comm", False) else ""),
+                   "comm": comm + (" (in-graph)" if getattr(step, "graph_comm", False) else "") +
+                           (f", {len(step.buckets)} buckets" if step.comm is not None else "") +
+                           (", overlapped" if getattr(step, "overlap", False) else "") +
+                           (", bf16 gradients" if getattr(step, "comm_dtype", None) == torch.bfloat16 else ""),
                    "devices_used": min(world, ndev)},
         "elbo": ({"loss": loss_terms[0], "Reconstruction_Loss": loss_terms[1], "finite": finite}
                  if args.arch in AE_WIDTHS else      # (the Autoencoder's loss is the MSE alone)

@@ -411,6 +411,9 @@ int vae_adam_step(int64_t n, float* p, const float* g, float* m, float* v,
  * are; *has_elbo / *elbo: the deferred loss, if any) and clears it; vae_deferred_reset clears it.
  * A gradient deferred again before it was taken (the same dst) replaces its earlier descriptor.
  * Workspace queries record nothing.
+ * A descriptor with rows == 0 (slab NULL) records a gradient the call wrote whole itself (one K
+ * slice: no reduction left); vae_adam_step_ex treats it as a plain gradient, and a step head may
+ * leave it out of its zeroing (vae_step_begin_args.keep).
  * vae_adam_step_ex: vae_adam_step over the flat buffers, with the slab descriptors reduced in the
  * same launch (each dst inside g: the reduced gradient is written there, then that element's Adam
  * update runs), and the deferred loss evaluated by one extra workgroup — the step's three slab
@@ -528,6 +531,11 @@ typedef struct vae_step_begin_args {
    * before the first GEMM that reads them — instead of a launch of their own behind the optimizer */
   int32_t nswap;
   vae_swap_desc swap[VAE_SWAP_MAX];
+  /* byte ranges [off, off + bytes) of the zero region left as they are: gradients the step writes
+   * whole instead of accumulating (defer_reduce: the deferred reductions' destinations and the
+   * weight gradients a call writes itself — vae_deferred_take lists both); 16-byte multiples */
+  int32_t nkeep;
+  struct { int64_t off, bytes; } keep[VAE_SLAB_MAX];
 } vae_step_begin_args;
 int vae_step_begin_ex(const vae_step_begin_args* a, void* stream);
 

@@ -1009,8 +1009,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) a
       float t = 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q) t += red[q][tid];
-      // (columns past count up to the 16-column boundary are the parameter's zero padding)
-      const float gv = e < count ? t : 0.f;
+      // (elements past count up to the 16-column boundary are not the descriptor's: their own
+      // gradient)
+      const float gv = e < count ? t : a.g[base + e];
       a.g[base + e] = gv;
       adam_elem(k, pi, gv, mi, vi);
       a.m[base + e] = mi; a.v[base + e] = vi; a.p[base + e] = pi;
@@ -1044,6 +1045,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) a
 #pragma unroll
       for (int u = 0; u < 4; ++u)
         if (e0 + u < count) acc[u] += s.slab[(long)r * ld + e0 + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (e0 + u >= count) acc[u] = a.g[base + e0 + u];     // (past the descriptor: its own gradient)
   }
   reinterpret_cast<f32x4*>(a.g)[gi] = acc;
   float pe[4], me[4], ve[4];
@@ -1076,11 +1080,13 @@ extern "C" int vae_adam_step_ex(const vae_adam_args* a, void* stream) {
   k.b1 = a->beta1; k.b2 = a->beta2; k.eps = a->eps; k.wd = a->weight_decay;
   k.lowp = static_cast<__bf16*>(a->p_lowp);
   // descriptors sorted by their position in g; each must start on a quad and not overlap the next
-  int order[VAE_SLAB_MAX];
-  for (int i = 0; i < a->nslab; ++i) order[i] = i;
-  std::sort(order, order + a->nslab, [&](int x, int y) { return a->slab[x].dst < a->slab[y].dst; });
+  // (rows == 0: a gradient its call wrote whole — a plain gradient here)
+  int order[VAE_SLAB_MAX], ns = 0;
+  for (int i = 0; i < a->nslab; ++i)
+    if (a->slab[i].rows != 0) order[ns++] = i;
+  std::sort(order, order + ns, [&](int x, int y) { return a->slab[x].dst < a->slab[y].dst; });
   int blk = 0;
-  for (int j = 0; j < a->nslab; ++j) {
+  for (int j = 0; j < ns; ++j) {
     const vae_grad_slab& s = a->slab[order[j]];
     const long off = (long)(s.dst - a->g);
     if (!s.dst || !s.slab || s.count <= 0 || s.rows <= 0 || s.ld < s.count || off < 0 || off + s.count > a->n || off % 4)
@@ -1096,8 +1102,8 @@ extern "C" int vae_adam_step_ex(const vae_adam_args* a, void* stream) {
     k.blk0[j] = blk;
     blk += (int)(k.tall[j] ? (s.count + 15) / 16 : (s.count + 1023) / 1024);
   }
-  k.nslab = a->nslab;
-  k.blk0[a->nslab] = blk;
+  k.nslab = ns;
+  k.blk0[ns] = blk;
   k.nreg = grid_for((a->n + 3) / 4);
   k.has_elbo = a->has_elbo;
   if (a->has_elbo) k.e = a->elbo;

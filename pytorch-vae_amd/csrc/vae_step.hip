@@ -11,16 +11,22 @@
 // The reference's step (experiment.py:45-49) feeds the image straight into the first Conv2d
 // (models/vanilla_vae.py:84); the padding exists only so that the first layer runs on the packed
 // 16-byte GEMM operand path.  profiles/r3a: the three separate launches took 6.5 + 5.2 + 4.8 us.
+#include <algorithm>
+
 #include "vae_common.hpp"
 
 namespace vae {
 namespace {
 
+constexpr int kZeroRanges = VAE_SLAB_MAX + 1;
 struct StepBegin {
   vae_step_begin_args a;
-  long n16;              // 16-byte words to zero
+  long n16;              // 16-byte words of the zero region
   int ntail;             // bytes after them
   int nz, nx;            // blocks of the zeroing and of the image ranges
+  int nzr;                          // zeroed ranges (the region minus its keep ranges)
+  int zb0[kZeroRanges + 1];         // first block of each range
+  long zoff[kZeroRanges], zlen[kZeroRanges];   // in 16-byte words
   int pad0[VAE_PAD_MAX + 1];   // first block of each pad descriptor (relative to nz + nx)
   int np;                      // blocks of the pad range
   int swap0[VAE_SWAP_MAX + 1]; // first block of each swap descriptor (relative to nz + nx + np)
@@ -50,7 +56,11 @@ __global__ void __launch_bounds__(256) step_begin_ex_kernel(const StepBegin s) {
   const int b = blockIdx.x, tid = threadIdx.x;
   if (b < s.nz) {
     f32x4* z = static_cast<f32x4*>(s.a.zero);
-    for (long i = (long)b * 256 + tid; i < s.n16; i += (long)s.nz * 256) z[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    while (k + 1 < s.nzr && b >= s.zb0[k + 1]) ++k;
+    const int lb = b - s.zb0[k], nb = s.zb0[k + 1] - s.zb0[k];
+    f32x4* zr = z + s.zoff[k];
+    for (long i = (long)lb * 256 + tid; i < s.zlen[k]; i += (long)nb * 256) zr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (b == 0 && tid < s.ntail) reinterpret_cast<unsigned char*>(z + s.n16)[tid] = 0;
     if (b == 0 && tid == 0 && s.a.step) *s.a.step += 1;
     return;
@@ -93,8 +103,34 @@ extern "C" int vae_step_begin_ex(const vae_step_begin_args* a, void* stream) {
   s.a = *a;
   s.n16 = a->bytes / 16;
   s.ntail = (int)(a->bytes - s.n16 * 16);
-  long zb = (s.n16 + 255) / 256;
-  s.nz = (int)(zb < 1 ? 1 : (zb > 2048 ? 2048 : zb));
+  // the zeroed ranges: the region minus its keep ranges (sorted, clipped, 16-byte words inward)
+  if (a->nkeep < 0 || a->nkeep > VAE_SLAB_MAX) return fail(VAE_E_BADARG, "step_begin_ex: %d keep ranges", a->nkeep);
+  long ko[VAE_SLAB_MAX], ke[VAE_SLAB_MAX];
+  int nk = 0;
+  for (int k = 0; k < a->nkeep; ++k) {
+    const long o = (a->keep[k].off + 15) / 16, e = (a->keep[k].off + a->keep[k].bytes) / 16;
+    if (a->keep[k].off < 0 || a->keep[k].bytes < 0) return fail(VAE_E_BADARG, "step_begin_ex: keep %d", k);
+    const long oo = o < s.n16 ? o : s.n16, ee = e < s.n16 ? e : s.n16;
+    if (ee > oo) { ko[nk] = oo; ke[nk] = ee; ++nk; }
+  }
+  std::sort(ko, ko + nk);
+  std::sort(ke, ke + nk);              // (keep ranges do not overlap: the gradients of distinct tensors)
+  s.nzr = 0;
+  long pos = 0;
+  for (int k = 0; k <= nk; ++k) {
+    const long end = k < nk ? ko[k] : s.n16;
+    if (end > pos) { s.zoff[s.nzr] = pos; s.zlen[s.nzr] = end - pos; ++s.nzr; }
+    if (k < nk && ke[k] > pos) pos = ke[k];
+  }
+  if (s.nzr == 0) { s.zoff[0] = 0; s.zlen[0] = 0; s.nzr = 1; }
+  int zb = 0;
+  for (int k = 0; k < s.nzr; ++k) {
+    s.zb0[k] = zb;
+    const long nb = (s.zlen[k] + 255) / 256;
+    zb += (int)(nb < 1 ? 1 : (nb > 2048 ? 2048 : nb));
+  }
+  s.zb0[s.nzr] = zb;
+  s.nz = zb;
   s.nx = 0;
   if (a->x) {
     if (!a->y || a->n <= 0 || a->c <= 0 || a->h <= 0 || a->w <= 0 || a->cp < a->c)

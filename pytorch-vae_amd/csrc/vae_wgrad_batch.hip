@@ -183,6 +183,10 @@ struct Wg3Layer {
 // fixed parts of a work item (us, tools/wgprobe.py): its first round trip (tables + first K-steps,
 // queued behind every other workgroup's), a unit's refill when an item runs several, the epilogue
 constexpr double kWg3PrologueUs = 6.0, kWg3RefillUs = 2.0, kWg3EpilogueUs = 3.0;
+// the epilogue of a unit that writes its tile into dW without reading it back (a deferred layer's
+// single slice, WgParams.own == 2): the store only (tools/wgprobe.py: the deep layers' items ran
+// 27-30 us against the 37-40 us of the rest with the read-modify-write cost in the plan)
+constexpr double kWg3StoreEpilogueUs = 1.5;
 
 inline bool wg3_layer(const WgParams& w0, int idx, Wg3Layer* L) {
   const int var = wg_variant(w0);
@@ -286,7 +290,7 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       L.slices = (npix + L.p.kper - 1) / L.p.kper;
       L.tpi = 1;
       if (L.slices == 1) {
-        const double unit = ksteps * L.step_us + kWg3EpilogueUs;
+        const double unit = ksteps * L.step_us + (defer_of[l] ? kWg3StoreEpilogueUs : kWg3EpilogueUs);
         long t = (long)((T - kWg3PrologueUs + kWg3RefillUs) / (unit + kWg3RefillUs));
         L.tpi = t < 1 ? 1 : (t > L.tiles ? L.tiles : t);
       }
@@ -353,7 +357,8 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
       for (long u = it * L.tpi; u < (it + 1) * L.tpi && u < L.slices * L.tiles; ++u) {
         const long sl = u / L.tiles;
         const long px = (sl + 1) * L.p.kper < npix ? L.p.kper : npix - sl * L.p.kper;
-        us += (double)(px + L.KP - 1) / L.KP * L.step_us + kWg3EpilogueUs + (u > it * L.tpi ? kWg3RefillUs : 0.0);
+        const double epi = (L.slices == 1 && defer_of[l]) ? kWg3StoreEpilogueUs : kWg3EpilogueUs;
+        us += (double)(px + L.KP - 1) / L.KP * L.step_us + epi + (u > it * L.tpi ? kWg3RefillUs : 0.0);
       }
       list[ni++] = It{(unsigned short)((l << 12) | (int)it), (float)us};
       total_us += us;
@@ -393,8 +398,11 @@ extern "C" int vae_conv_bwd_filter_batch(int32_t n, const int32_t* kinds, const 
   Wg3Reduce r;
   memset(&r, 0, sizeof(r));
   for (int l = 0; l < nl; ++l) {
-    if (defer_of[l] && lay[l].slices > 1) {        // the slices stay for vae_adam_step_ex
-      if (!defer_slab(g.p[l].dw, lay[l].cols, g.p[l].slab, (int)lay[l].slices, lay[l].cols)) return VAE_E_UNSUPPORTED;
+    if (defer_of[l]) {
+      // the slices stay for vae_adam_step_ex; one slice: written whole by this call (rows 0)
+      const bool sl = lay[l].slices > 1;
+      if (!defer_slab(g.p[l].dw, lay[l].cols, sl ? g.p[l].slab : nullptr, sl ? (int)lay[l].slices : 0, lay[l].cols))
+        return VAE_E_UNSUPPORTED;
       continue;
     }
     if (lay[l].slices <= 1) continue;

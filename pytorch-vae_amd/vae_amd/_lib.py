@@ -158,11 +158,16 @@ class PadDesc(ctypes.Structure):
     _fields_ = [("rows", c_int64), ("c", c_int32), ("cp", c_int32), ("src", c_void_p), ("dst", c_void_p)]
 
 
+class KeepRange(ctypes.Structure):
+    _fields_ = [("off", c_int64), ("bytes", c_int64)]
+
+
 class StepBeginArgs(ctypes.Structure):
     _fields_ = [("zero", c_void_p), ("bytes", c_int64), ("step", c_void_p), ("dtype", c_int32),
                 ("n", c_int32), ("c", c_int32), ("h", c_int32), ("w", c_int32), ("cp", c_int32),
                 ("x", c_void_p), ("y", c_void_p), ("npad", c_int32), ("pad", PadDesc * PAD_MAX),
-                ("nswap", c_int32), ("swap", SwapDesc * SWAP_MAX)]
+                ("nswap", c_int32), ("swap", SwapDesc * SWAP_MAX), ("nkeep", c_int32),
+                ("keep", KeepRange * 32)]
 
 
 class LatentArgs(ctypes.Structure):

@@ -17,7 +17,7 @@ import torch.distributed as dist
 
 from . import _lib as L
 from .dp import BucketedAllReduce, broadcast_buffers, plan_buckets
-from .net import VAENet
+from .net import BATCH_FN, VAENet, call_one
 
 
 class FusedAdam:
@@ -117,8 +117,9 @@ class TrainStep:
     queued, so it runs on the communication stream while the rest of the backward computes."""
 
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
-                 nbuckets: int = 1, device_eps: Optional[int] = None, force_buckets: bool = False,
-                 graph_comm: bool = True, begin_ex: bool = True, defer_reductions: bool = True):
+                 nbuckets: int = 2, device_eps: Optional[int] = None, force_buckets: bool = False,
+                 graph_comm: bool = True, begin_ex: bool = True, defer_reductions: bool = True,
+                 overlap: bool = True, comm_dtype: torch.dtype = torch.float32):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -152,14 +153,43 @@ class TrainStep:
         # forked after its segment and joined before Adam — so a step is one replay, with no host
         # round trip per bucket.  Needs the "nccl" (RCCL) backend (gloo: host-issued); checked bit for
         # bit against the host-issued path at world size 1 (tests/test_gpu_zz_rccl.py).
-        # nbuckets = 1 by default: at one rank (bench.py --force-buckets) the step took 0.483 ms with
-        # one in-graph bucket, 0.542 with two, 0.585 with four (0.553 / 0.584 / 0.644 host-issued;
-        # 0.461 without the exchange) — each extra bucket splits the backward into another segment
-        # and another grouped weight-gradient launch, which costs more than the ~100 us of a
-        # 15.75 MB all-reduce it could hide (profiles/r5_notes.md).
+        # nbuckets = 2 by default (round 6): the first bucket's weight gradients run on the overlap
+        # stream (below), so its all-reduce hides behind the encoder's backward.  Round 5, without
+        # that stream, measured one bucket best at one rank (0.483 ms in-graph vs 0.542 with two:
+        # the second grouped weight-gradient launch sat on the critical path, profiles/r5_notes.md).
         self.graph_comm = (graph_comm and graph and self.comm is not None
                            and dist.get_backend(process_group) == "nccl")
         self.comm_stream = torch.cuda.Stream(device=net.device) if self.graph_comm else None
+        # overlap (in-graph exchange, two or more buckets): the weight-gradient batch that closes a
+        # bucket's backward segment runs on a stream of its own, forked from the segment's data-
+        # gradient chain; the bucket's all-reduce waits for it there, while the next segment's data
+        # gradients go on — the exchange of the decoder's gradients overlaps the encoder's backward
+        # (DDP's hook-driven overlap, run.py:86), and the batch itself is off the critical path.
+        # Each overlapped batch gets a workspace of its own (the main chain's is reused meanwhile).
+        self.overlap = bool(overlap and self.graph_comm and len(self.buckets) > 1)
+        # comm_dtype=torch.bfloat16 (in-graph exchange only; opt-in): each bucket is rounded to bf16,
+        # all-reduced (AVG) in bf16 and widened back into the fp32 gradients Adam reads — half the
+        # bytes over xGMI; the parity mode keeps fp32 (the reference's DDP all-reduces fp32)
+        if comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"comm_dtype {comm_dtype}")
+        self.comm_dtype = comm_dtype if self.graph_comm else torch.float32
+        self._comm_bufs = ([torch.empty(b1 - b0, dtype=torch.bfloat16, device=net.device) for _, b0, b1 in self.buckets]
+                           if self.comm_dtype == torch.bfloat16 else None)
+        self.wg_stream = torch.cuda.Stream(device=net.device) if self.overlap else None
+        self._wg_ws = []
+        self._wg_forked = False
+        if self.overlap:
+            from .net import BATCH_FN
+            lo = 0
+            for end, _, _ in self.buckets[:-1]:
+                seg = plan.bwd_calls[lo:end]
+                if seg and seg[-1][0] == BATCH_FN:
+                    b = seg[-1][1]
+                    need = b.workspace_size()
+                    ws = torch.empty(max(1, (need + 3) // 4), dtype=torch.float32, device=net.device)
+                    b.workspace, b.workspace_bytes = (ws.data_ptr(), ws.numel() * 4) if need > 0 else (None, 0)
+                    self._wg_ws.append(ws)
+                lo = end
         self.graphs = []
         self.g_opt: Optional[torch.cuda.CUDAGraph] = None
         self.stream = torch.cuda.Stream(device=net.device)
@@ -196,14 +226,41 @@ class TrainStep:
         lo = 0 if k == 0 else self.buckets[k - 1][0]
         if self.deferred:
             L.call("vae_deferred_reset")
-        p._run(p.bwd_calls[lo:self.buckets[k][0]], st)
+        seg = p.bwd_calls[lo:self.buckets[k][0]]
+        self._wg_forked = False
+        if self.overlap and k < len(self.buckets) - 1 and seg and seg[-1][0] == BATCH_FN:
+            # the segment's weight gradients on the overlap stream, behind its data gradients
+            p._run(seg[:-1], st)
+            ws = self.wg_stream
+            ws.wait_stream(torch.cuda.current_stream())
+            call_one(BATCH_FN, seg[-1][1], ws.cuda_stream)
+            self._wg_forked = True
+        else:
+            p._run(seg, st)
         if self.deferred:
             # (the same pointers at every run: each deferring call has a workspace of its own)
             self._slabs, self._elbo = L.deferred_take()
+            self._keep_written(p)
         if k == 0 and self.comm is not None and getattr(p, "elbo_in_head", False):
             # the loss terms come from the head backward (vae_head_args.elbo), the first call of
             # segment 0's backward: copied behind it, reduced with the last bucket as before
             p.metrics.copy_(p.out)
+
+    def _keep_written(self, p):
+        """The gradients the deferred calls write whole (their reductions' destinations and the
+        single-slice weight gradients: every descriptor) need no zeroing at the step head
+        (vae_step_begin_args.keep): the step-begin launch leaves them out from the next step on."""
+        if self._begin is None:
+            return
+        a = self._begin[0]
+        base, end = p.zero.data_ptr(), p.zero.data_ptr() + p.zero.numel() * 4
+        n = 0
+        for sl in self._slabs:
+            if sl.dst is None or not base <= sl.dst < end or n >= len(a.keep):
+                continue
+            a.keep[n] = L.KeepRange(off=sl.dst - base, bytes=sl.count * 4)
+            n += 1
+        a.nkeep = n
 
     def _opt(self):
         # with the swapped copies refreshed by the next step's head, the optimizer skips its own pass
@@ -226,6 +283,8 @@ class TrainStep:
         with torch.cuda.stream(s):
             for k in range(len(self.buckets)):
                 self._segment(k)
+            if self.overlap:
+                s.wait_stream(self.wg_stream)
             self._opt()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -245,11 +304,22 @@ class TrainStep:
                     self._segment(k)
                     _, b0, b1 = self.buckets[k]
                     cs.wait_stream(s)                   # this segment's gradients are complete
+                    if self._wg_forked:
+                        cs.wait_stream(self.wg_stream)  # (its weight gradients: the overlap stream)
                     with torch.cuda.stream(cs):
-                        dist.all_reduce(self.plan.zero[b0:b1], op=dist.ReduceOp.AVG, group=self.pg)
+                        grad = self.plan.zero[b0:b1]
+                        if self._comm_bufs is not None:
+                            buf = self._comm_bufs[k]
+                            buf.copy_(grad)
+                            dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.pg)
+                            grad.copy_(buf)
+                        else:
+                            dist.all_reduce(grad, op=dist.ReduceOp.AVG, group=self.pg)
                 with torch.cuda.stream(cs):
                     broadcast_buffers(self.net.running, self.pg)
                 s.wait_stream(cs)
+                if self.overlap:
+                    s.wait_stream(self.wg_stream)
                 self._opt()
             self.graphs.append(g)
             self.g_opt = None

@@ -414,9 +414,11 @@ class StepCheck:
         self.add("Adam bf16 weight copy", ("adam", 0), (eq == 1.0, {"equal_fraction": eq}))
 
 
-def run_bench_step(arch: str, batch: int, seed: int = 1265):
+def run_bench_step(arch: str, batch: int, seed: int = 1265, segments: int = 1, defer: bool = True):
     """One step of bench.py's plan for `arch` at `batch` (graph-replayed TrainStep, on-device eps),
-    with the pre/post state snapshots StepCheck needs and the kernels every call launched."""
+    with the pre/post state snapshots StepCheck needs and the kernels every call launched.
+    segments > 1: the weight gradients batched per backward segment as the data-parallel step cuts
+    it into gradient buckets (dp.plan_buckets; TrainStep's default of two at N > 1)."""
     from vae_amd import _lib as L
     from vae_amd.engine import FusedAdam, TrainStep
     from vae_amd.net import StepPlan, VAENet, call_one
@@ -428,10 +430,15 @@ def run_bench_step(arch: str, batch: int, seed: int = 1265):
     gen = torch.Generator().manual_seed(seed)
     net = VAENet(latent_dim=128, dtype=torch.bfloat16, device="cuda", generator=gen)
     plan = StepPlan(net, batch, loss=loss, kld_weight=kld, samples=S)
+    if segments > 1:
+        from vae_amd.dp import plan_buckets
+        ends = [b[0] for b in plan_buckets(plan.bwd_calls_raw, plan.grads, net.layout, segments)]
+        assert len(ends) == segments, ends
+        plan.batch_wgrads(ends)
     opt = FusedAdam(net, lr=lr)
     g = torch.Generator(device="cuda").manual_seed(seed)
     plan.x.copy_(torch.rand(plan.x.shape, generator=g, device="cuda"))
-    step = TrainStep(net, plan, opt, graph=True, device_eps=seed)
+    step = TrainStep(net, plan, opt, graph=True, device_eps=seed, defer_reductions=defer)
     assert step.device_eps and plan.latent_fused and plan.pad_rgb
     pre = (net.params.clone(), net.lowp.clone(), net.running.clone())
     names_step = launched(step)                 # capture (warm-up step + restore) and one replay

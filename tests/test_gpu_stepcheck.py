@@ -19,24 +19,33 @@ import torch
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = [("vanilla", 64), ("betaH", 32), ("iwae", 64)]
+CASES = [("vanilla", 64, 1, True), ("betaH", 32, 1, True), ("iwae", 64, 1, True),
+         ("betaH", 32, 2, False), ("vanilla", 16, 1, True), ("vanilla", 16, 1, False)]
+
+
+def _tag(a, b, s, d):
+    return f"{a}_{b}" + (f"_seg{s}" if s > 1 else "") + ("" if d else "_nodefer")
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("arch,batch", CASES, ids=[f"{a}_{b}" for a, b in CASES])
-def test_bench_step_every_op_teacher_forced(arch, batch):
+@pytest.mark.parametrize("arch,batch,segments,defer", CASES, ids=[_tag(*c) for c in CASES])
+def test_bench_step_every_op_teacher_forced(arch, batch, segments, defer):
+    """(segments = 2, defer False: the weight gradients as two batches each reducing its own slices,
+    as the N > 1 step's two gradient buckets run them at the per-GPU shape of configs[2]; B = 16:
+    the shape of the one-rank RCCL tests, with and without the deferred reductions)"""
     from stepcheck import coverage, run_bench_step
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    checks, names_step, per_call = run_bench_step(arch, batch)
+    checks, names_step, per_call = run_bench_step(arch, batch, segments=segments, defer=defer)
     for c in checks:
         print(("ok  " if c.ok else "BAD ") + f"{c.name} [{c.call[0]}#{c.call[1]}]: " +
               ", ".join(f"{k} {v:.3g}" if isinstance(v, float) else f"{k} {v}" for k, v in c.detail.items()))
     cov, step_kernels, missing = coverage(checks, names_step, per_call)
     out = os.path.join(REPO, "gpurun_out")
     os.makedirs(out, exist_ok=True)
-    with open(os.path.join(out, f"kernel_coverage_{arch}_{batch}.json"), "w") as f:
+    tag = _tag(arch, batch, segments, defer)
+    with open(os.path.join(out, f"kernel_coverage_{tag}.json"), "w") as f:
         json.dump({"arch": arch, "batch": batch, "test": f"tests/test_gpu_stepcheck.py::"
-                   f"test_bench_step_every_op_teacher_forced[{arch}_{batch}]",
+                   f"test_bench_step_every_op_teacher_forced[{tag}]",
                    "step_kernels": step_kernels, "coverage": cov,
                    "checks": [{"name": c.name, "call": list(c.call), "ok": c.ok, **c.detail} for c in checks]},
                   f, indent=1)
