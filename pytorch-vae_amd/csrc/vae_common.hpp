@@ -538,29 +538,61 @@ __device__ __forceinline__ void tab_build(const vae_xform& x, Tab t, bool epi, b
   tab_build(x, t, epi, update_running, scr);
 }
 
-// One 32x32 (a, b) tile of one tap of a swapped-axes weight copy (vae_swap_axes): dst[b][tap][a] =
-// bf16(src[a][tap][b]) (src fp32, or already bf16) through a padded LDS tile, so reads and writes are both 64-byte row segments
-// (an element-wise gather reads with a stride of rs*b elements).  blk < swap_tiles(d).
-__host__ __device__ inline int swap_tiles(const vae_swap_desc& d) { return ((d.a + 31) / 32) * ((d.b + 31) / 32) * d.rs; }
-__device__ __forceinline__ void swap_tile(const vae_swap_desc& d, int blk, float (*t)[33]) {
-  const int nb = (d.b + 31) / 32, na = (d.a + 31) / 32;
+// One 64x64 (a, b) tile of one tap of a swapped-axes weight copy (vae_swap_axes): dst[b][tap][a] =
+// bf16(src[a][tap][b]) (src fp32, or already bf16) through a padded LDS tile.  Each lane moves an
+// element PAIR, so a wave's 32 lanes of a row read or write one 128-byte
+// segment (32x32 tiles of single elements made 64-byte segments and four times the workgroups:
+// 8.7 us for the VanillaVAE step's copies, tools/beginbench.py).  blk < swap_tiles(d).
+constexpr int kSwapT = 64;
+__host__ __device__ inline int swap_tiles(const vae_swap_desc& d) {
+  return ((d.a + kSwapT - 1) / kSwapT) * ((d.b + kSwapT - 1) / kSwapT) * d.rs;
+}
+__device__ __forceinline__ void swap_tile(const vae_swap_desc& d, int blk, float (*t)[kSwapT + 1]) {
+  const int nb = (d.b + kSwapT - 1) / kSwapT, na = (d.a + kSwapT - 1) / kSwapT;
   const int bt = blk % nb; blk /= nb;
   const int at = blk % na;
   const int tap = blk / na;
-  const int a0 = at * 32, b0 = bt * 32;
+  const int a0 = at * kSwapT, b0 = bt * kSwapT;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  __bf16* dst = static_cast<__bf16*>(d.dst);
-  for (int j = ty; j < 32; j += 8) {
-    const int a = a0 + j, b = b0 + tx;
+  // rows a of the source tile: lane tx takes columns b0 + 2 tx, +1 — one 4-byte (bf16) / 8-byte
+  // (fp32) access when b is even (every channel count but the 3-channel RGB ends), else two
+  const bool vb = (d.b & 1) == 0, va = (d.a & 1) == 0;
+#pragma unroll
+  for (int j = ty; j < kSwapT; j += 8) {
+    const int a = a0 + j, b = b0 + 2 * tx;
     const long i = ((long)a * d.rs + tap) * d.b + b;
-    t[j][tx] = !(a < d.a && b < d.b) ? 0.f
-               : d.src_dtype == VAE_BF16 ? (float)static_cast<const __bf16*>(d.src)[i]
-                                         : static_cast<const float*>(d.src)[i];
+    float v0 = 0.f, v1 = 0.f;
+    if (a < d.a && b < d.b) {
+      if (d.src_dtype == VAE_BF16) {
+        const __bf16* sp = static_cast<const __bf16*>(d.src) + i;
+        if (vb) { const bf16x2 q = *reinterpret_cast<const bf16x2*>(sp); v0 = (float)q[0]; v1 = (float)q[1]; }
+        else { v0 = (float)sp[0]; v1 = b + 1 < d.b ? (float)sp[1] : 0.f; }
+      } else {
+        const float* sp = static_cast<const float*>(d.src) + i;
+        if (vb) { const f32x2 q = *reinterpret_cast<const f32x2*>(sp); v0 = q[0]; v1 = q[1]; }
+        else { v0 = sp[0]; v1 = b + 1 < d.b ? sp[1] : 0.f; }
+      }
+    }
+    t[j][2 * tx] = v0;
+    t[j][2 * tx + 1] = v1;
   }
   __syncthreads();
-  for (int j = ty; j < 32; j += 8) {
-    const int b = b0 + j, a = a0 + tx;
-    if (a < d.a && b < d.b) dst[((long)b * d.rs + tap) * d.a + a] = (__bf16)t[tx][j];
+  __bf16* dst = static_cast<__bf16*>(d.dst);
+#pragma unroll
+  for (int j = ty; j < kSwapT; j += 8) {
+    const int b = b0 + j, a = a0 + 2 * tx;
+    if (a < d.a && b < d.b) {
+      __bf16* dp = dst + ((long)b * d.rs + tap) * d.a + a;
+      if (va) {
+        bf16x2 o;
+        o[0] = (__bf16)t[2 * tx][j];
+        o[1] = (__bf16)t[2 * tx + 1][j];
+        *reinterpret_cast<bf16x2*>(dp) = o;
+      } else {
+        dp[0] = (__bf16)t[2 * tx][j];
+        if (a + 1 < d.a) dp[1] = (__bf16)t[2 * tx + 1][j];
+      }
+    }
   }
 }
 

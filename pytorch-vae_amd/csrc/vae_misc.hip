@@ -1214,7 +1214,7 @@ struct SwapBatch {
 
 __global__ void __launch_bounds__(256) swap_axes_kernel(const SwapBatch sb) {
   kernarg_prefetch<(sizeof(SwapBatch) < 1024 ? sizeof(SwapBatch) : 1024)>();
-  __shared__ float t[32][33];
+  __shared__ float t[kSwapT][kSwapT + 1];
   int i = 0;
   while (i + 1 < sb.count && (int)blockIdx.x >= sb.tiles0[i + 1]) ++i;
   swap_tile(sb.d[i], blockIdx.x - sb.tiles0[i], t);

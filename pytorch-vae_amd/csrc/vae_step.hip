@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(256) step_begin_ex_kernel(const StepBegin s) {
   }
   const int pb = b - s.nz - s.nx;
   if (pb >= s.np) {
-    __shared__ float t[32][33];
+    __shared__ float t[kSwapT][kSwapT + 1];
     const int sb = pb - s.np;
     int k = 0;
     while (k + 1 < s.a.nswap && sb >= s.swap0[k + 1]) ++k;
