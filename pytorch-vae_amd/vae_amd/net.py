@@ -338,7 +338,10 @@ class StepPlan:
         splits = []
         if self.wg_overlap and len(ends) == 1:
             raw = self.bwd_calls_raw
-            first_lin = next((i for i, (fn, _) in enumerate(raw) if fn == "vae_linear_bwd_data"), None)
+            # the decoder's backward ends where the bottleneck's begins (the fused latent kernels
+            # or the latent Linear layers)
+            first_lin = next((i for i, (fn, _) in enumerate(raw)
+                              if fn in ("vae_latent_dec_bwd", "vae_linear_bwd_data")), None)
             if first_lin is not None:
                 splits = [first_lin]
         if self.deterministic:

@@ -15,7 +15,9 @@ Inputs:
 Prints, per summary, each library kernel with the tests that pin it, and exits non-zero when a kernel
 of a summary has none (torch's own kernels of the bench's setup are not the library's and are listed
 apart).  A summary is matched with the coverage records of its own configuration (its bench
-arguments: --arch / --batch)."""
+arguments: --arch / --batch).  Library kernels launched fewer times than the summary's warmup + timed
+steps ran outside the step — the plan's setup and restore copies, bench.py's per-call timing of the
+op-by-op prologue — and are listed apart."""
 import argparse
 import glob
 import json
@@ -32,13 +34,17 @@ CONFIG_TAG = {("vanilla", 64): "vanilla_64", ("betaH", 32): "betaH_32", ("iwae",
 
 def workload(d):
     toks = str(d.get("config") or "").split()
-    arch, batch = "vanilla", 64
+    arch, batch, steps, warmup = "vanilla", 64, 0, 0
     for i, t in enumerate(toks[:-1]):
         if t == "--arch":
             arch = toks[i + 1]
         elif t == "--batch":
             batch = int(toks[i + 1])
-    return arch, batch
+        elif t == "--steps":
+            steps = int(toks[i + 1])
+        elif t == "--warmup":
+            warmup = int(toks[i + 1])
+    return arch, batch, steps + warmup
 
 
 def is_library_kernel(name: str) -> bool:
@@ -69,11 +75,16 @@ def main():
     bad = 0
     for f in kst:
         d = json.load(open(f))
-        wl = workload(d)
+        arch, batch, steps = workload(d)
+        wl = (arch, batch)
         tag = CONFIG_TAG.get(wl)
         m = cov.get(tag, {}) if tag else {}
-        lib = [k for k in d.get("kernels", {}) if is_library_kernel(k)]
-        other = [k for k in d.get("kernels", {}) if not is_library_kernel(k)]
+        kern = d.get("kernels", {})
+        # a kernel launched fewer times than the warmup + timed steps is not part of the step: bench.py's
+        # per-call timing pass (the op-by-op prologue calls) and the plan's setup / restore copies
+        setup = [k for k in kern if is_library_kernel(k) and kern[k].get("calls", steps) < steps]
+        lib = [k for k in kern if is_library_kernel(k) and k not in setup]
+        other = [k for k in kern if not is_library_kernel(k)]
         print(f"== {os.path.relpath(f, REPO)}  ({wl[0]} B={wl[1]}; digest {d.get('digest')}; coverage {tag})")
         for k in lib:
             tests = sorted(m.get(norm(k), []))
@@ -82,6 +93,8 @@ def main():
             print(f"  {'ok ' if tests else 'NO '} {k[:100]}")
             for t in tests:
                 print(f"        {t}")
+        for k in setup:
+            print(f"  --  {k[:100]}  ({kern[k].get('calls')} launches < {steps} warmup + timed steps: outside the step)")
         if other:
             print(f"  (not library kernels, bench setup: {len(other)})")
     if not kst:
