@@ -45,12 +45,9 @@ def _written_grad_ptrs(arg) -> List[int]:
     return out
 
 
-def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4,
-                 min_bucket_bytes: int = 1 << 20) -> List[Tuple[int, int, int]]:
-    """Split the backward launch list into segments whose completion finishes a flat prefix of
-    the gradient buffer.  Returns [(end_call, start_elem, end_elem)]: after calls[:end_call]
-    have run, grads[start_elem:end_elem] is final.  The last bucket ends at len(calls) and
-    covers the rest of the buffer."""
+def last_writers(calls: Sequence, grads: torch.Tensor, layout):
+    """The parameters in buffer order and, for each, the index of the last call of `calls` that
+    writes its gradient (-1: none) — read from the gradient pointers of every call's arguments."""
     base = grads.data_ptr()
     params = sorted(layout.params, key=lambda p: p.offset)
     starts = [p.offset for p in params]
@@ -60,6 +57,7 @@ def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4
             continue
         if hasattr(ref, "args"):                # a batch of weight-gradient calls (net.FilterBatch)
             ptrs = [p for a in ref.args for p in _written_grad_ptrs(a)]
+            ptrs += [r[4] for f, r in getattr(ref, "after", []) if f == "vae_unpad_accumulate"]
         elif isinstance(ref, tuple):            # scalar-argument entry points
             ptrs = [ref[4]] if fn == "vae_unpad_accumulate" else []
         else:
@@ -77,6 +75,28 @@ def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4
                 else:
                     hi = mid - 1
             last[lo] = max(last[lo], i)
+    return params, last
+
+
+def final_prefix(calls: Sequence, upto: int, grads: torch.Tensor, layout) -> int:
+    """Elements of the leading run of parameters whose gradients are final once calls[:upto + 1]
+    have run (no later call writes them)."""
+    params, last = last_writers(calls, grads, layout)
+    t = 0
+    for k, p in enumerate(params):
+        if last[k] > upto:
+            break
+        t = params[k + 1].offset if k + 1 < len(params) else layout.total
+    return t
+
+
+def plan_buckets(calls: Sequence, grads: torch.Tensor, layout, nbuckets: int = 4,
+                 min_bucket_bytes: int = 1 << 20) -> List[Tuple[int, int, int]]:
+    """Split the backward launch list into segments whose completion finishes a flat prefix of
+    the gradient buffer.  Returns [(end_call, start_elem, end_elem)]: after calls[:end_call]
+    have run, grads[start_elem:end_elem] is final.  The last bucket ends at len(calls) and
+    covers the rest of the buffer."""
+    params, last = last_writers(calls, grads, layout)
     # complete[i] = number of leading params final after call i
     total = layout.total
     target = max(min_bucket_bytes // 4, total // max(1, nbuckets))

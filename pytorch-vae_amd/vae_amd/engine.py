@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
-from .dp import BucketedAllReduce, broadcast_buffers, plan_buckets
+from .dp import BucketedAllReduce, broadcast_buffers, final_prefix, plan_buckets
 from .net import BATCH_FN, VAENet, call_one
 
 
@@ -38,18 +38,24 @@ class FusedAdam:
     def set_lr(self, lr: float):
         self.lr.fill_(float(lr))
 
-    def apply_deferred(self, grads: torch.Tensor, slabs, elbo, stream=None):
+    def apply_deferred(self, grads: torch.Tensor, slabs, elbo, stream=None, lo: int = 0, hi: Optional[int] = None):
         """apply() with the weight-gradient reductions the backward deferred (L.deferred_take) done in
         the same launch (vae_adam_step_ex): each reduced gradient is written into `grads` before its
-        elements' update, and a deferred loss is evaluated by one extra workgroup."""
+        elements' update, and a deferred loss is evaluated by one extra workgroup.  [lo, hi): the
+        elements this launch updates (a multiple of 4 apart from 0; the descriptors must lie inside)."""
         net = self.net
         if len(slabs) > L.SLAB_MAX:
             raise ValueError(f"{len(slabs)} deferred reductions > {L.SLAB_MAX}")
-        a = self._ex = getattr(self, "_ex", None) or L.AdamArgs()
-        a.n, a.p, a.g, a.m, a.v = net.params.numel(), net.params.data_ptr(), grads.data_ptr(), self.m.data_ptr(), self.v.data_ptr()
+        hi = net.params.numel() if hi is None else hi
+        if lo % 4 or not 0 <= lo < hi <= net.params.numel():
+            raise ValueError(f"apply_deferred range [{lo}, {hi})")
+        ex = self.__dict__.setdefault("_ex", {})
+        a = ex.get(lo) or ex.setdefault(lo, L.AdamArgs())
+        a.n, a.p, a.g = hi - lo, net.params.data_ptr() + 4 * lo, grads.data_ptr() + 4 * lo
+        a.m, a.v = self.m.data_ptr() + 4 * lo, self.v.data_ptr() + 4 * lo
         a.step, a.lr = self.step.data_ptr(), self.lr.data_ptr()
         a.beta1, a.beta2, a.eps, a.weight_decay = self.betas[0], self.betas[1], self.eps, self.weight_decay
-        a.p_lowp = net.lowp.data_ptr() if net.lowp is not None else None
+        a.p_lowp = net.lowp.data_ptr() + 2 * lo if net.lowp is not None else None
         a.nslab = len(slabs)
         for i, sl in enumerate(slabs):
             a.slab[i] = sl
@@ -119,7 +125,7 @@ class TrainStep:
     def __init__(self, net, plan, opt: FusedAdam, *, graph: bool = True, process_group=None,
                  nbuckets: int = 2, device_eps: Optional[int] = None, force_buckets: bool = False,
                  graph_comm: bool = True, begin_ex: bool = True, defer_reductions: bool = True,
-                 overlap: bool = True, comm_dtype: torch.dtype = torch.float32):
+                 overlap: bool = True, comm_dtype: torch.dtype = torch.float32, split_adam: bool = True):
         self.net, self.plan, self.opt = net, plan, opt
         # device_eps = seed: the forward draws eps itself every step (StepPlan.use_device_eps, keyed
         # by the optimizer's step counter) — the reference's per-step randn_like inside the step
@@ -179,7 +185,6 @@ class TrainStep:
         self._wg_ws = []
         self._wg_forked = False
         if self.overlap:
-            from .net import BATCH_FN
             lo = 0
             for end, _, _ in self.buckets[:-1]:
                 seg = plan.bwd_calls[lo:end]
@@ -203,6 +208,18 @@ class TrainStep:
         self.deferred = (self.comm is None and defer_reductions and hasattr(plan, "defer_reductions")
                          and plan.defer_reductions())
         self._slabs, self._elbo = [], None
+        # one rank, the decoder's weight gradients on the plan's side stream (StepPlan(wg_overlap=True)):
+        # the optimizer splits at the gradients final once that batch has run (their prefix of the
+        # buffer, ordered by backward completion) — Adam over the prefix runs on the side stream right
+        # behind the batch, beside the encoder's backward; Adam over the rest on the main stream
+        self._adam_split = 0
+        if self.deferred and split_adam and getattr(plan, "wg_overlap", False) and getattr(plan, "side", None) is not None:
+            si = next((i for i, (fn, ref) in enumerate(plan.bwd_calls)
+                       if fn == BATCH_FN and getattr(ref, "side", False)), None)
+            if si is not None:
+                t = final_prefix(plan.bwd_calls, si, plan.grads, net.layout)
+                if 0 < t < plan.grads.numel() and t % 4 == 0:
+                    self._adam_split = t
 
     # -------------------------------------------------------------- eager pieces
     def _segment(self, k: int):
@@ -264,8 +281,22 @@ class TrainStep:
 
     def _opt(self):
         # with the swapped copies refreshed by the next step's head, the optimizer skips its own pass
-        if self.deferred:
+        if self.deferred and self._adam_split:
+            t, g = self._adam_split, self.plan.grads
+            end = g.data_ptr() + 4 * t
+            head = [sl for sl in self._slabs if sl.dst < end]
+            tail = [sl for sl in self._slabs if sl.dst >= end]
+            if any(sl.dst + 4 * sl.count > end for sl in head):
+                raise RuntimeError("deferred reduction across the optimizer split")
+            side, main = self.plan.side, torch.cuda.current_stream()
+            # (the side stream's last work is the decoder's weight-gradient batch; the forward and the
+            # backward calls before it were queued behind the fork)
+            self.opt.apply_deferred(g, head, self._elbo, side.cuda_stream, 0, t)
+            self.opt.apply_deferred(g, tail, None, main.cuda_stream, t)
+            main.wait_stream(side)
+        elif self.deferred:
             self.opt.apply_deferred(self.plan.grads, self._slabs, self._elbo, L.stream_ptr())
+        if self.deferred:
             if getattr(self.net, "swap_descs", None) is not None:
                 if self._begin_swaps:
                     self.net.swaps_stale = True

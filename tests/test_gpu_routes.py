@@ -7,7 +7,8 @@ autocast oracle's own error + 2e-3; loss terms within 2x + 1e-4):
                                   (models/vanilla_vae.py:36-43, 107-117) instead of vae_latent_*
   StepPlan(pad_rgb=False)         the first conv reads the NCHW fp32 image directly
   StepPlan(batch_wgrads=False)    one weight-gradient call per layer (no vae_conv_bwd_filter_batch)
-  StepPlan(wg_overlap=True)       the decoder's weight gradients on a side stream in the graph
+  StepPlan(wg_overlap=True)       the decoder's weight gradients on a side stream in the graph, and
+                                  Adam over their prefix of the buffer right behind them there
   TrainStep(begin_ex=False)       vae_step_begin + padding calls instead of vae_step_begin_ex
   StepPlan(head_kernels=False)    a 64-channel final layer on the conv-GEMM + vae_recon_fwd route
   StepPlan(materialise=..., mat_min_flops=...)  materialised vs fused BatchNorm operands
@@ -59,6 +60,18 @@ def test_vanilla_family_route(name, plan_kw, step_kw, must, must_not):
     o32, oac = _oracles("BetaVAE", sd, x, eps, M_N=2.5e-4, beta=4.0, loss_type="H")
     _loss_bar(step.loss_terms(), o32, oac, ("loss", "Reconstruction_Loss", "KLD"))
     assert _grad_bar(g16, o32, oac, f"route {name}", _pre_bn_bias) >= 30
+    if name == "wg_overlap":
+        # the optimizer split in two launches at the decoder's gradients (TrainStep._adam_split: the
+        # prefix on the side stream): the parameters are torch Adam's first step on these gradients
+        assert step._adam_split > 0
+        p_got = {k: v.cpu() for k, v in net.layout.export_reference(net.params).items()}
+        for k, g in g16.items():
+            p0 = sd[k].clone().float().requires_grad_(True)
+            ref = torch.optim.Adam([p0], lr=0.005)
+            p0.grad = g.float().reshape(p0.shape)
+            ref.step()
+            err = (p_got[k].reshape(p0.shape) - p0.detach()).abs().max().item()
+            assert err <= 1e-5, (k, err)
 
 
 AE_ROUTES = [
