@@ -85,7 +85,8 @@ def _worker(port, q):
         # backward (elbo_in_head) and the swapped weight copies are refreshed in the step head
         bf = [_run(False, x, eps, dtype=torch.bfloat16),
               _run(True, x, eps, graph_comm=False, nbuckets=2, dtype=torch.bfloat16),
-              _run(True, x, eps, graph_comm=True, nbuckets=2, dtype=torch.bfloat16)]
+              _run(True, x, eps, graph_comm=True, nbuckets=2, dtype=torch.bfloat16),
+              _run(False, x, eps, dtype=torch.bfloat16)]        # (the collective-free step again: noise)
         # the opt-in bf16 exchange at one rank: AVG over one contribution of the bf16-rounded bucket,
         # so the gradients are exactly the fp32 ones rounded to bf16
         ge, _, _, _ = _run(True, x, eps, graph_comm=True, nbuckets=2, comm_dtype=torch.bfloat16)
@@ -138,7 +139,12 @@ def test_rccl_bucketed_step_matches_one_graph_step():
     for k, (got, f32) in bf16_comm.items():
         want = torch.from_numpy(f32).to(torch.bfloat16).float().numpy()
         assert np.array_equal(got, want), ("bf16 exchange", k)
+    g0n = bf.pop()[0]                     # the collective-free step rerun: its own run-to-run noise
     (g0, s0, t0, _), *others = bf
+
+    def rel(a, b):
+        d = np.linalg.norm(b.astype(np.float64))
+        return np.linalg.norm(a.astype(np.float64) - b) / d if d else 0.0
     for tag, (g1, s1, t1, _) in zip(("host-issued", "in-graph"), others):
         t0a, t1a = np.array(t0[0], dtype=np.float64), np.array(t1[0], dtype=np.float64)
         assert np.all(np.abs(t1a - t0a) <= 1e-3 * np.abs(t0a) + 1e-6), (tag, t0, t1)
@@ -147,11 +153,9 @@ def test_rccl_bucketed_step_matches_one_graph_step():
             # value is rounding noise, no relative comparison means anything)
             if k.startswith("step2/") or (k.endswith(".0.bias") and not k.startswith("final_layer.3")):
                 continue
-            d = np.linalg.norm(g0[k].astype(np.float64))
-            if d == 0.0:
-                continue
-            e = np.linalg.norm(g1[k].astype(np.float64) - g0[k]) / d
+            e = rel(g1[k], g0[k])
             # (bf16 run to run: atomics-order noise in the BatchNorm statistics flips bf16 roundings
-            # that the backward amplifies — 2e-2 measured on decoder.3.0.weight at B = 16, while the
-            # teacher-forced op checks pin every kernel of both paths, tests/test_gpu_stepcheck.py)
-            assert e <= 1e-1, (tag, k, e)
+            # that the backward amplifies — 2e-2 to 1.1e-1 measured on decoder weights at B = 16 —
+            # so the bar is the collective-free step's own rerun distance, while the teacher-forced op
+            # checks pin every kernel of both paths, tests/test_gpu_stepcheck.py)
+            assert e <= max(1e-1, 4.0 * rel(g0n[k], g0[k])), (tag, k, e, rel(g0n[k], g0[k]))
