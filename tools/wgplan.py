@@ -99,10 +99,6 @@ def main():
     print(f"  work {tot:.0f} slot-us, {tot / SLOTS:.1f} us per slot")
 
 
-if __name__ == "__main__":
-    main()
-
-
 def simulate(L, T, epi_all, true, per_xcd_cap=None, order="lpt"):
     """Item list as vae_wgrad_batch.hip builds it at target T, cut into 8 XCD runs of equal modelled
     time (at most per_xcd_cap items each when given), each run list-scheduled on 64 slots in LPT
@@ -133,3 +129,7 @@ def simulate(L, T, epi_all, true, per_xcd_cap=None, order="lpt"):
             heapq.heappush(slots, s + t)
         span = max(span, max(slots))
     return n, span
+
+
+if __name__ == "__main__":
+    main()
